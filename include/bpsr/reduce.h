@@ -1,0 +1,149 @@
+/*
+ * bpsr/reduce.h — C ABI of libbpsr.so, the MI355X (gfx950) gradient-bucket
+ * reducer that replaces the host-side CpuReducer of Prophet/BytePS.
+ *
+ * Every exported name matches `*byteps*`, so it survives the reference's own
+ * linker version script (byteps.lds:1-8 exports only *byteps*, *PyInit*,
+ * *initc_lib*).  No torch, HIP or C++ types cross this boundary: pointers are
+ * device pointers (or host pointers registered/allocated for device access),
+ * lengths are BYTES exactly as in the reference, streams are opaque
+ * hipStream_t handles passed as void* (NULL = the calling thread's default
+ * stream, hipStreamPerThread).
+ *
+ * Reference interfaces replaced (byteps/common/cpu_reducer.h:41-58):
+ *   CpuReducer::sum(void* dst, void* src, size_t len, DataType)      -> byteps_reduce_sum
+ *   CpuReducer::sum(void* dst, void* s1, void* s2, size_t, DataType) -> byteps_reduce_sum3
+ *   CpuReducer::copy(void* dst, void* src, size_t len)               -> byteps_reduce_copy
+ *   the server's per-key fold, byteps/server/server.cc:216-273
+ *   (first arrival = accumulator, N-1 SUM_RECV jobs, COPY_MERGED)    -> byteps_reduce_sum_n
+ *   one Prophet block of buckets released together
+ *   (byteps/common/scheduled_queue.cc:244-296)                       -> byteps_reduce_sum_batched
+ *
+ * Semantics (bit-exact parity with the compiled reference):
+ *   - sum: dst[i] = dst[i] + src[i] for i < len / sizeof(T); the trailing
+ *     len % sizeof(T) bytes are NOT touched (cpu_reducer.cc:88).
+ *   - fp16: fp32 add then round-to-nearest-even to fp16 after EVERY add
+ *     (cpu_reducer.cc:101-125); NaN payload rules of the F16C body for
+ *     i < floor(n/8)*8 and 0x7fff for the scalar tail (cpu_reducer.h:77-173).
+ *   - integers wrap (two's complement).
+ *   - copy: all len bytes (cpu_reducer.cc:209-220).
+ *   - sum_n: strict left fold ((s0 + s1) + s2) + ... in the given order.
+ *
+ * Errors: 0 on success, a negative BYTEPS_REDUCE_E* code otherwise.  Nothing
+ * aborts across this ABI (the reference BPS_CHECK-aborts on a bad dtype,
+ * cpu_reducer.cc:79-80).  byteps_reduce_last_error() returns a thread-local
+ * message for the last failing call on the calling thread.
+ *
+ * Threading: calls are thread-safe for distinct buffers (the reference calls
+ * CpuReducer from BYTEPS_SERVER_ENGINE_THREAD engine threads on distinct
+ * keys, server.cc:70-145).  All compute calls are asynchronous on `stream`;
+ * byteps_reduce_sync(stream) completes them.
+ */
+#ifndef BPSR_REDUCE_H
+#define BPSR_REDUCE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BYTEPS_REDUCE_ABI_VERSION 1
+
+/* Data type ids: byteps/common/common.h:52-65 (mshadow order), plus bf16 as a
+ * build extension (the reference has none). */
+enum byteps_reduce_dtype {
+  BYTEPS_REDUCE_FLOAT32 = 0,
+  BYTEPS_REDUCE_FLOAT64 = 1,
+  BYTEPS_REDUCE_FLOAT16 = 2,
+  BYTEPS_REDUCE_UINT8 = 3,
+  BYTEPS_REDUCE_INT32 = 4,
+  BYTEPS_REDUCE_INT8 = 5,
+  BYTEPS_REDUCE_INT64 = 6,
+  BYTEPS_REDUCE_BFLOAT16 = 11
+};
+
+/* Rounding mode for the 16-bit float types (ignored for the others). */
+enum byteps_reduce_mode {
+  /* Round to the storage type after every pairwise add: bit-exact with the
+   * reference CpuReducer fold.  Default. */
+  BYTEPS_REDUCE_MODE_REFERENCE = 0,
+  /* Accumulate all N inputs in fp32 and round once at the end (more accurate,
+   * not bit-exact; documented tolerance <= 1 ulp of the exact sum for N <= 32). */
+  BYTEPS_REDUCE_MODE_ACCUM_F32 = 1
+};
+
+enum byteps_reduce_status {
+  BYTEPS_REDUCE_OK = 0,
+  BYTEPS_REDUCE_EDTYPE = -1,   /* unsupported data type                      */
+  BYTEPS_REDUCE_EARGS = -2,    /* bad pointer / count / overlap / mode        */
+  BYTEPS_REDUCE_EHIP = -3,     /* HIP runtime error (launch, copy, event)     */
+  BYTEPS_REDUCE_ERCCL = -4     /* collective error (reserved for shard APIs)  */
+};
+
+/* Most sources one kernel launch folds; byteps_reduce_sum_n chains launches
+ * for more (still a strict left fold). */
+#define BYTEPS_REDUCE_MAX_SRCS 32
+
+/* One bucket of a batched (Prophet block) reduction: dst = fold(srcs[0..n-1]).
+ * dst may alias srcs[0]. */
+typedef struct byteps_bucket_desc {
+  void* dst;
+  const void* srcs[BYTEPS_REDUCE_MAX_SRCS];
+  size_t len;   /* bytes */
+  int n;        /* 1 <= n <= BYTEPS_REDUCE_MAX_SRCS */
+  int reserved;
+} byteps_bucket_desc;
+
+/* Library version (BYTEPS_REDUCE_ABI_VERSION). */
+int byteps_reduce_version(void);
+
+/* Optional eager initialisation for `device` (hipSetDevice + kernel warm-up);
+ * every other call initialises lazily on the current device. */
+int byteps_reduce_init(int device);
+int byteps_reduce_shutdown(void);
+
+/* CpuReducer::sum(dst, src, len, dtype), cpu_reducer.cc:57-83. */
+int byteps_reduce_sum(void* dst, const void* src, size_t len, int dtype, void* stream);
+
+/* CpuReducer::sum(dst, src1, src2, len, dtype), cpu_reducer.cc:130-162. */
+int byteps_reduce_sum3(void* dst, const void* src1, const void* src2, size_t len,
+                       int dtype, void* stream);
+
+/* Fused N-way left fold: dst = ((srcs[0] + srcs[1]) + ...) + srcs[n-1].
+ * dst may alias srcs[0] exactly (the server's zero-copy accumulator,
+ * server.cc:216-218); partial overlaps are rejected.  Trailing bytes
+ * (len % sizeof(T)) of dst are copied from srcs[0]. */
+int byteps_reduce_sum_n(void* dst, const void* const* srcs, int n, size_t len,
+                        int dtype, int mode, void* stream);
+
+/* One launch for a whole block of buckets (all of one dtype). */
+int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets,
+                              int dtype, int mode, void* stream);
+
+/* CpuReducer::copy(dst, src, len), cpu_reducer.cc:209-220 (device to device). */
+int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream);
+
+/* Block the calling thread until all work queued on `stream` has finished. */
+int byteps_reduce_sync(void* stream);
+
+/* Size in bytes of one element of `dtype` (getDataTypeLength, common.cc:126-143),
+ * or BYTEPS_REDUCE_EDTYPE. */
+int byteps_reduce_dtype_size(int dtype);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* byteps_reduce_last_error(void);
+
+/* Launch tuning (process-wide; defaults chosen from rocprof measurements, see
+ * DESIGN.md).  vpt: 16-B vectors per thread per source per step (1, 2 or 4);
+ * nt: non-temporal input loads (0/1); max_grid: grid cap in 256-thread blocks.
+ * A value <= 0 (nt: < 0) keeps the current setting.  Also settable through
+ * the environment: BPSR_VPT, BPSR_NT, BPSR_MAX_GRID. */
+int byteps_reduce_set_tuning(int vpt, int nt, int max_grid);
+int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPSR_REDUCE_H */

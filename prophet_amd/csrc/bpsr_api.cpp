@@ -1,0 +1,364 @@
+// C ABI of libbpsr.so (include/bpsr/reduce.h): argument checking, geometry,
+// descriptor staging and dispatch to the gfx950 kernels.  Never aborts: every
+// failure is a negative status plus a thread-local message.
+#include "bpsr/reduce.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "bpsr_internal.h"
+
+namespace bpsr {
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+static int hip_fail(hipError_t e, const char* what) {
+  return fail(BYTEPS_REDUCE_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+int elem_size(int dtype) {
+  switch (dtype) {
+    case kInt8: case kUInt8: return 1;
+    case kFloat16: case kBFloat16: return 2;
+    case kInt32: case kFloat32: return 4;
+    case kInt64: case kFloat64: return 8;
+    default: return 0;
+  }
+}
+
+void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, int n,
+               bool copy_trailing, FoldGeom* g, int* aligned) {
+  const uint64_t es = (uint64_t)elem_size(dtype);
+  std::memset(g, 0, sizeof(*g));
+  g->n_elems = len / es;
+  g->trailing_bytes = len % es;
+  g->copy_trailing = (copy_trailing && g->trailing_bytes) ? 1u : 0u;
+  const uintptr_t d = (uintptr_t)dst;
+  bool elem_al = (d % es) == 0, co = true;
+  for (int k = 0; k < n; ++k) {
+    const uintptr_t s = (uintptr_t)srcs[k];
+    elem_al = elem_al && (s % es) == 0;
+    co = co && ((s & 15u) == (d & 15u));
+  }
+  *aligned = elem_al ? 1 : 0;
+  // fp16: elements >= floor(n/8)*8 are the reference's scalar tail
+  // (cpu_reducer.cc:103 vs :118) and must not enter the vector path.
+  const uint64_t vec_end = dtype == kFloat16 ? (g->n_elems / 8) * 8 : g->n_elems;
+  g->tail_sem_from = dtype == kFloat16 ? vec_end : g->n_elems;
+  if (elem_al && co) {
+    uint64_t head = ((16u - (d & 15u)) & 15u) / es;
+    if (head > g->n_elems) head = g->n_elems;
+    g->head_elems = head;
+    g->vec_off = head * es;
+    g->nvec = vec_end > head ? ((vec_end - head) * es) / 16 : 0;
+    g->tail_begin = head + g->nvec * 16 / es;
+  } else {
+    g->head_elems = 0;
+    g->vec_off = 0;
+    g->nvec = 0;
+    g->tail_begin = 0;
+  }
+}
+
+static Tuning& tuning() {
+  static Tuning tu = [] {
+    Tuning t{4, 0, 2048};
+    if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
+    if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
+    if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
+    if (t.vpt != 1 && t.vpt != 2) t.vpt = 4;
+    if (t.max_grid < 1) t.max_grid = 2048;
+    t.nt = t.nt ? 1 : 0;
+    return t;
+  }();
+  return tu;
+}
+
+static inline hipStream_t to_stream(void* s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : hipStreamPerThread;
+}
+
+static bool overlaps_partially(const void* a, const void* b, size_t len) {
+  if (a == b || len == 0) return false;
+  const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+  return x < y + len && y < x + len;
+}
+
+// One fold launch over at most kMaxSrcs sources.
+static int fold_once(void* dst, const void* const* srcs, int n, size_t len, int dtype,
+                     int mode, bool copy_trailing, hipStream_t s) {
+  FoldArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int k = 0; k < n; ++k) a.srcs[k] = static_cast<const unsigned char*>(srcs[k]);
+  a.dst = static_cast<unsigned char*>(dst);
+  a.n = n;
+  make_geom(dtype, len, dst, srcs, n, copy_trailing, &a.g, &a.aligned);
+  hipError_t e = launch_fold(a, dtype, mode, tuning(), s);
+  if (e != hipSuccess) return hip_fail(e, "fold kernel launch");
+  return BYTEPS_REDUCE_OK;
+}
+
+static int check_common(int dtype, int mode) {
+  if (elem_size(dtype) == 0) return fail(BYTEPS_REDUCE_EDTYPE, "Unsupported data type: %d", dtype);
+  if (mode != kModeReference && mode != kModeAccumF32)
+    return fail(BYTEPS_REDUCE_EARGS, "unknown mode %d", mode);
+  return BYTEPS_REDUCE_OK;
+}
+
+// ------------------------------------------------ batched descriptor staging --
+// Per-thread ring of pinned host + device tables.  A slot is reused only after
+// the event recorded behind the kernel that read it has completed.
+struct StageSlot {
+  int device = -1;
+  size_t cap = 0;
+  void* host = nullptr;
+  void* dev = nullptr;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+};
+constexpr int kRing = 8;
+
+struct StageRing {
+  StageSlot slots[kRing];
+  int next = 0;
+  ~StageRing() {
+    for (auto& s : slots) {
+      if (s.pending && s.done) (void)hipEventSynchronize(s.done);
+      if (s.done) (void)hipEventDestroy(s.done);
+      if (s.host) (void)hipHostFree(s.host);
+      if (s.dev) (void)hipFree(s.dev);
+    }
+  }
+};
+static thread_local StageRing g_ring;
+
+static int stage_acquire(size_t bytes, StageSlot** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  StageSlot& s = g_ring.slots[g_ring.next];
+  g_ring.next = (g_ring.next + 1) % kRing;
+  if (s.pending) {
+    e = hipEventSynchronize(s.done);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(stage)");
+    s.pending = false;
+  }
+  if (s.device != dev || s.cap < bytes) {
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.dev) (void)hipFree(s.dev);
+    if (s.done) (void)hipEventDestroy(s.done);
+    s.host = s.dev = nullptr;
+    s.done = nullptr;
+    size_t cap = std::max<size_t>(bytes, 64 * 1024);
+    if ((e = hipHostMalloc(&s.host, cap, hipHostMallocDefault)) != hipSuccess)
+      return hip_fail(e, "hipHostMalloc(stage)");
+    if ((e = hipMalloc(&s.dev, cap)) != hipSuccess) return hip_fail(e, "hipMalloc(stage)");
+    if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hipEventCreate(stage)");
+    s.cap = cap;
+    s.device = dev;
+  }
+  *out = &s;
+  return BYTEPS_REDUCE_OK;
+}
+
+}  // namespace bpsr
+
+using namespace bpsr;
+
+extern "C" {
+
+int byteps_reduce_version(void) { return BYTEPS_REDUCE_ABI_VERSION; }
+
+int byteps_reduce_dtype_size(int dtype) {
+  const int es = elem_size(dtype);
+  return es ? es : fail(BYTEPS_REDUCE_EDTYPE, "Unsupported data type: %d", dtype);
+}
+
+const char* byteps_reduce_last_error(void) { return g_last_error.c_str(); }
+
+int byteps_reduce_set_tuning(int vpt, int nt, int max_grid) {
+  Tuning& t = tuning();
+  if (vpt > 0) {
+    if (vpt != 1 && vpt != 2 && vpt != 4) return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2 or 4");
+    t.vpt = vpt;
+  }
+  if (nt >= 0) t.nt = nt ? 1 : 0;
+  if (max_grid > 0) t.max_grid = max_grid;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid) {
+  const Tuning& t = tuning();
+  if (vpt) *vpt = t.vpt;
+  if (nt) *nt = t.nt;
+  if (max_grid) *max_grid = t.max_grid;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_init(int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  (void)tuning();
+  e = hipFree(nullptr);  // forces context creation
+  if (e != hipSuccess) return hip_fail(e, "hip runtime init");
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_shutdown(void) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_sum(void* dst, const void* src, size_t len, int dtype, void* stream) {
+  int rc = check_common(dtype, kModeReference);
+  if (rc) return rc;
+  if (len == 0) return BYTEPS_REDUCE_OK;
+  if (!dst || !src) return fail(BYTEPS_REDUCE_EARGS, "null pointer");
+  if (overlaps_partially(dst, src, len))
+    return fail(BYTEPS_REDUCE_EARGS, "dst and src partially overlap");
+  const void* srcs[2] = {dst, src};
+  return fold_once(dst, srcs, 2, len, dtype, kModeReference, false, to_stream(stream));
+}
+
+int byteps_reduce_sum3(void* dst, const void* src1, const void* src2, size_t len, int dtype,
+                       void* stream) {
+  int rc = check_common(dtype, kModeReference);
+  if (rc) return rc;
+  if (len == 0) return BYTEPS_REDUCE_OK;
+  if (!dst || !src1 || !src2) return fail(BYTEPS_REDUCE_EARGS, "null pointer");
+  if (overlaps_partially(dst, src1, len) || overlaps_partially(dst, src2, len))
+    return fail(BYTEPS_REDUCE_EARGS, "dst partially overlaps a source");
+  const void* srcs[2] = {src1, src2};
+  return fold_once(dst, srcs, 2, len, dtype, kModeReference, false, to_stream(stream));
+}
+
+int byteps_reduce_sum_n(void* dst, const void* const* srcs, int n, size_t len, int dtype,
+                        int mode, void* stream) {
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (n < 1 || !srcs) return fail(BYTEPS_REDUCE_EARGS, "need n >= 1 sources (n=%d)", n);
+  if (len == 0) return BYTEPS_REDUCE_OK;
+  if (!dst) return fail(BYTEPS_REDUCE_EARGS, "null dst");
+  for (int k = 0; k < n; ++k) {
+    if (!srcs[k]) return fail(BYTEPS_REDUCE_EARGS, "null srcs[%d]", k);
+    if (overlaps_partially(dst, srcs[k], len))
+      return fail(BYTEPS_REDUCE_EARGS, "dst partially overlaps srcs[%d]", k);
+    if (k > 0 && srcs[k] == dst)
+      return fail(BYTEPS_REDUCE_EARGS, "dst may alias only srcs[0] (srcs[%d] == dst)", k);
+  }
+  hipStream_t s = to_stream(stream);
+  if (n == 1) {
+    if (dst == srcs[0]) return BYTEPS_REDUCE_OK;
+    hipError_t e = launch_copy(dst, srcs[0], len, tuning(), s);
+    return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "copy kernel launch");
+  }
+  // First launch folds up to kMaxSrcs sources; each further launch folds the
+  // running result (as its srcs[0]) with the next kMaxSrcs-1: still a strict
+  // left fold, bit-exact in reference mode.
+  int take = std::min(n, kMaxSrcs);
+  rc = fold_once(dst, srcs, take, len, dtype, mode, dst != srcs[0], s);
+  const void* chunk[kMaxSrcs];
+  for (int k = take; rc == 0 && k < n;) {
+    int m = std::min(n - k, kMaxSrcs - 1);
+    chunk[0] = dst;
+    for (int j = 0; j < m; ++j) chunk[1 + j] = srcs[k + j];
+    rc = fold_once(dst, chunk, m + 1, len, dtype, mode, false, s);
+    k += m;
+  }
+  return rc;
+}
+
+int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
+                              int mode, void* stream) {
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (nbuckets < 0 || (nbuckets > 0 && !buckets))
+    return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
+  if (nbuckets == 0) return BYTEPS_REDUCE_OK;
+  // Validate; count tiles (each bucket >= 1 tile so its element work runs).
+  const uint64_t tile_vecs = (uint64_t)kBlock * kBatchVPT;
+  const size_t tab_bytes = sizeof(BatchEntry) * (size_t)nbuckets;
+  const size_t ts_off = (tab_bytes + 255) & ~(size_t)255;
+  const size_t bytes = ts_off + sizeof(uint32_t) * (size_t)(nbuckets + 1);
+  StageSlot* slot = nullptr;
+  if ((rc = stage_acquire(bytes, &slot))) return rc;
+  BatchEntry* tab = static_cast<BatchEntry*>(slot->host);
+  uint32_t* ts = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->host) + ts_off);
+  uint64_t tiles = 0;
+  int live = 0;
+  for (int i = 0; i < nbuckets; ++i) {
+    const byteps_bucket_desc& b = buckets[i];
+    if (b.n < 1 || b.n > kMaxSrcs)
+      return fail(BYTEPS_REDUCE_EARGS, "bucket %d: n=%d outside [1, %d]", i, b.n, kMaxSrcs);
+    if (b.len == 0) continue;
+    if (!b.dst) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null dst", i);
+    for (int k = 0; k < b.n; ++k) {
+      if (!b.srcs[k]) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null srcs[%d]", i, k);
+      if (overlaps_partially(b.dst, b.srcs[k], b.len) || (k > 0 && b.srcs[k] == b.dst))
+        return fail(BYTEPS_REDUCE_EARGS, "bucket %d: dst overlaps srcs[%d]", i, k);
+    }
+    BatchEntry& e = tab[live];
+    std::memset(&e, 0, sizeof(e));
+    for (int k = 0; k < b.n; ++k) e.srcs[k] = static_cast<const unsigned char*>(b.srcs[k]);
+    e.dst = static_cast<unsigned char*>(b.dst);
+    e.n = b.n;
+    make_geom(dtype, b.len, b.dst, b.srcs, b.n, b.dst != b.srcs[0], &e.g, &e.aligned);
+    ts[live] = (uint32_t)tiles;
+    uint64_t t = (e.g.nvec + tile_vecs - 1) / tile_vecs;
+    tiles += t ? t : 1;
+    if (tiles > 0xffffffffull) return fail(BYTEPS_REDUCE_EARGS, "batch too large");
+    ++live;
+  }
+  if (live == 0) return BYTEPS_REDUCE_OK;
+  ts[live] = (uint32_t)tiles;
+  // Pack tile_start right behind the live entries' slot region.
+  hipStream_t s = to_stream(stream);
+  hipError_t e = hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
+  e = launch_batched(static_cast<const BatchEntry*>(slot->dev),
+                     reinterpret_cast<const uint32_t*>(static_cast<char*>(slot->dev) + ts_off),
+                     live, (uint32_t)tiles, dtype, mode, tuning(), s);
+  if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
+  e = hipEventRecord(slot->done, s);
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
+  slot->pending = true;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream) {
+  if (len == 0 || dst == src) return BYTEPS_REDUCE_OK;
+  if (!dst || !src) return fail(BYTEPS_REDUCE_EARGS, "null pointer");
+  if (overlaps_partially(dst, src, len))
+    return fail(BYTEPS_REDUCE_EARGS, "dst and src overlap");
+  hipError_t e = launch_copy(dst, src, len, tuning(), to_stream(stream));
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "copy kernel launch");
+}
+
+int byteps_reduce_sync(void* stream) {
+  hipError_t e = hipStreamSynchronize(to_stream(stream));
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// Internal (non-ABI) declarations shared by the kernels and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bpsr {
+
+// dtype ids: byteps/common/common.h:52-65 + bf16 extension (include/bpsr/reduce.h)
+enum : int {
+  kFloat32 = 0, kFloat64 = 1, kFloat16 = 2, kUInt8 = 3,
+  kInt32 = 4, kInt8 = 5, kInt64 = 6, kBFloat16 = 11
+};
+enum : int { kModeReference = 0, kModeAccumF32 = 1 };
+
+constexpr int kBlock = 256;     // 4 waves of 64
+constexpr int kMaxSrcs = 32;    // BYTEPS_REDUCE_MAX_SRCS
+constexpr int kBatchVPT = 4;    // vectors per thread per tile in the batched kernel
+
+// Byte/element geometry of one fold, identical for every operand (the vector
+// path needs all operands co-aligned mod 16).
+struct FoldGeom {
+  uint64_t n_elems;        // len / sizeof(T)
+  uint64_t head_elems;     // elements before the 16-B vector range
+  uint64_t vec_off;        // byte offset of the vector range
+  uint64_t nvec;           // 16-B vectors in the vector range
+  uint64_t tail_begin;     // first element after the vector range
+  uint64_t tail_sem_from;  // fp16: first element with F16C-tail semantics
+  uint64_t trailing_bytes; // len % sizeof(T)
+  uint32_t copy_trailing;  // fold into a separate dst: trailing bytes from srcs[0]
+  uint32_t pad;
+};
+
+struct FoldArgs {
+  const unsigned char* srcs[kMaxSrcs];
+  unsigned char* dst;
+  int n;
+  int aligned;  // every operand element-aligned
+  FoldGeom g;
+};
+
+struct BatchEntry {
+  const unsigned char* srcs[kMaxSrcs];
+  unsigned char* dst;
+  int n;
+  int aligned;
+  FoldGeom g;
+};
+
+struct Tuning {
+  int vpt;       // 16-B vectors per thread per source per step (1, 2, 4)
+  int nt;        // non-temporal loads
+  int max_grid;  // grid cap (grid-stride beyond)
+};
+
+int elem_size(int dtype);  // 0 if unsupported
+
+// Host-side geometry: vector range, head/tail split (fp16 body/tail rule of
+// cpu_reducer.cc:103,118), co-alignment test.
+void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, int n,
+               bool copy_trailing, FoldGeom* g, int* aligned);
+
+inline int fold_grid(const FoldGeom& g, const Tuning& tu) {
+  const uint64_t scalar = g.head_elems + (g.n_elems - g.tail_begin) + g.trailing_bytes;
+  uint64_t work = (g.nvec + tu.vpt - 1) / tu.vpt;
+  if (scalar > work) work = scalar;
+  uint64_t blocks = (work + kBlock - 1) / kBlock;
+  if (blocks > (uint64_t)tu.max_grid) blocks = tu.max_grid;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
+                       hipStream_t s);
+hipError_t launch_batched(const BatchEntry* tab, const uint32_t* tile_start, int nbuckets,
+                          uint32_t ntiles, int dtype, int mode, const Tuning& tu,
+                          hipStream_t s);
+hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
+                       hipStream_t s);
+
+}  // namespace bpsr

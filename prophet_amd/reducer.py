@@ -1,0 +1,205 @@
+"""Host-side mirror of the reference reducer surface, over the C ABI.
+
+:class:`GpuReducer` keeps ``CpuReducer``'s method names and argument meaning
+(byteps/common/cpu_reducer.h:41-58):
+
+=====================================  =========================================
+reference                              here
+=====================================  =========================================
+``sum(dst, src, len, dtype)``          ``GpuReducer.sum`` -> ``byteps_reduce_sum``
+``sum(dst, src1, src2, len, dtype)``   ``GpuReducer.sum3`` -> ``byteps_reduce_sum3``
+``copy(dst, src, len)``                ``GpuReducer.copy`` -> ``byteps_reduce_copy``
+``GetDataType(int)``                   ``GpuReducer.GetDataType``
+server fold, server.cc:216-273         ``GpuReducer.sum_n`` -> ``byteps_reduce_sum_n``
+one Prophet block                      ``GpuReducer.sum_batched``
+=====================================  =========================================
+
+``len`` is in BYTES as in the reference.  Operands are device pointers (ints)
+or torch CUDA tensors (their ``data_ptr()``); ``stream`` defaults to torch's
+current stream on the operand's device so the calls order with the caller's
+torch work.  Errors raise :class:`ReduceError` carrying the negative status
+(the reference aborts via BPS_CHECK instead, cpu_reducer.cc:79-80).
+
+There is no fallback: if ``libbpsr.so`` is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Sequence
+
+from .dtypes import DType, elem_size
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libbpsr.so")
+MAX_SRCS = 32
+
+MODE_REFERENCE = 0
+MODE_ACCUM_F32 = 1
+
+OK, EDTYPE, EARGS, EHIP, ERCCL = 0, -1, -2, -3, -4
+
+_vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+
+# Every symbol include/bpsr/reduce.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "byteps_reduce_version", "byteps_reduce_init", "byteps_reduce_shutdown",
+    "byteps_reduce_sum", "byteps_reduce_sum3", "byteps_reduce_sum_n",
+    "byteps_reduce_sum_batched", "byteps_reduce_copy", "byteps_reduce_sync",
+    "byteps_reduce_dtype_size", "byteps_reduce_last_error",
+    "byteps_reduce_set_tuning", "byteps_reduce_get_tuning",
+)
+
+
+class BucketDesc(ctypes.Structure):
+    """``byteps_bucket_desc`` (include/bpsr/reduce.h)."""
+    _fields_ = [("dst", _vp), ("srcs", _vp * MAX_SRCS), ("len", _sz), ("n", _int),
+                ("reserved", _int)]
+
+
+class ReduceError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"byteps_reduce error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libbpsr.so (once).  Raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `make -C prophet_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(path)
+    L.byteps_reduce_version.restype = _int
+    L.byteps_reduce_init.argtypes = [_int]
+    L.byteps_reduce_sum.argtypes = [_vp, _vp, _sz, _int, _vp]
+    L.byteps_reduce_sum3.argtypes = [_vp, _vp, _vp, _sz, _int, _vp]
+    L.byteps_reduce_sum_n.argtypes = [_vp, ctypes.POINTER(_vp), _int, _sz, _int, _int, _vp]
+    L.byteps_reduce_sum_batched.argtypes = [ctypes.POINTER(BucketDesc), _int, _int, _int, _vp]
+    L.byteps_reduce_copy.argtypes = [_vp, _vp, _sz, _vp]
+    L.byteps_reduce_sync.argtypes = [_vp]
+    L.byteps_reduce_dtype_size.argtypes = [_int]
+    L.byteps_reduce_last_error.restype = ctypes.c_char_p
+    L.byteps_reduce_set_tuning.argtypes = [_int, _int, _int]
+    L.byteps_reduce_get_tuning.argtypes = [ctypes.POINTER(_int)] * 3
+    _LIB = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != OK:
+        msg = (_LIB.byteps_reduce_last_error() or b"").decode(errors="replace")
+        raise ReduceError(rc, msg)
+
+
+def _ptr(x) -> int:
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    if x is None:
+        return 0
+    raise TypeError(f"expected a device pointer or tensor, got {type(x)!r}")
+
+
+def _stream_of(x, stream):
+    if stream is not None:
+        return int(getattr(stream, "cuda_stream", stream))
+    if hasattr(x, "device") and getattr(x.device, "type", "") == "cuda":
+        import torch
+        return int(torch.cuda.current_stream(x.device).cuda_stream)
+    return 0  # library default: hipStreamPerThread
+
+
+class GpuReducer:
+    """Drop-in for ``byteps::common::CpuReducer`` on device memory."""
+
+    def __init__(self, device: int | None = None):
+        self.lib = load_library()
+        if device is not None:
+            _check(self.lib.byteps_reduce_init(int(device)))
+
+    # cpu_reducer.h:58
+    @staticmethod
+    def GetDataType(dtype: int) -> DType:
+        return DType(dtype)
+
+    def sum(self, dst, src, length: int, dtype: int, stream=None) -> int:
+        """In place ``dst += src`` over ``length`` bytes (cpu_reducer.cc:57-83)."""
+        _check(self.lib.byteps_reduce_sum(_ptr(dst), _ptr(src), int(length), int(dtype),
+                                          _stream_of(dst, stream)))
+        return 0
+
+    def sum3(self, dst, src1, src2, length: int, dtype: int, stream=None) -> int:
+        """``dst = src1 + src2`` (cpu_reducer.cc:130-162)."""
+        _check(self.lib.byteps_reduce_sum3(_ptr(dst), _ptr(src1), _ptr(src2), int(length),
+                                           int(dtype), _stream_of(dst, stream)))
+        return 0
+
+    def copy(self, dst, src, length: int, stream=None) -> int:
+        """``length``-byte device copy (cpu_reducer.cc:209-220)."""
+        _check(self.lib.byteps_reduce_copy(_ptr(dst), _ptr(src), int(length),
+                                           _stream_of(dst, stream)))
+        return 0
+
+    def sum_n(self, dst, srcs: Sequence, length: int, dtype: int,
+              mode: int = MODE_REFERENCE, stream=None) -> int:
+        """Left fold ``dst = ((srcs[0] + srcs[1]) + ...)`` in the given order."""
+        arr = (_vp * len(srcs))(*[_ptr(s) for s in srcs])
+        _check(self.lib.byteps_reduce_sum_n(_ptr(dst), arr, len(srcs), int(length),
+                                            int(dtype), int(mode), _stream_of(dst, stream)))
+        return 0
+
+    def sum_batched(self, buckets: Sequence[tuple], dtype: int, mode: int = MODE_REFERENCE,
+                    stream=None) -> int:
+        """One launch for a block of buckets; each item is ``(dst, srcs, length)``."""
+        descs = (BucketDesc * max(1, len(buckets)))()
+        for i, (dst, srcs, length) in enumerate(buckets):
+            if len(srcs) > MAX_SRCS:
+                raise ReduceError(EARGS, f"bucket {i}: more than {MAX_SRCS} sources")
+            descs[i].dst = _ptr(dst)
+            for k, s in enumerate(srcs):
+                descs[i].srcs[k] = _ptr(s)
+            descs[i].len = int(length)
+            descs[i].n = len(srcs)
+        first = buckets[0][0] if buckets else None
+        _check(self.lib.byteps_reduce_sum_batched(descs, len(buckets), int(dtype), int(mode),
+                                                  _stream_of(first, stream)))
+        return 0
+
+    def sync(self, stream=None) -> None:
+        _check(self.lib.byteps_reduce_sync(_stream_of(None, stream)))
+
+    def set_tuning(self, vpt: int = 0, nt: int = -1, max_grid: int = 0) -> None:
+        _check(self.lib.byteps_reduce_set_tuning(vpt, nt, max_grid))
+
+    def get_tuning(self) -> tuple[int, int, int]:
+        a, b, c = _int(), _int(), _int()
+        _check(self.lib.byteps_reduce_get_tuning(ctypes.byref(a), ctypes.byref(b),
+                                                 ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    @staticmethod
+    def dtype_size(dtype: int) -> int:
+        return elem_size(dtype)
+
+
+# torch-tensor convenience: whole-tensor ops with dtype taken from the tensor
+def tensor_sum_n(dst, srcs, mode: int = MODE_REFERENCE, reducer: GpuReducer | None = None):
+    from .dtypes import from_torch
+    r = reducer or GpuReducer()
+    nbytes = dst.numel() * dst.element_size()
+    for s in srcs:
+        if s.numel() * s.element_size() != nbytes or s.dtype != dst.dtype:
+            raise ReduceError(EARGS, "sources must match dst in dtype and size")
+        if not s.is_contiguous():
+            raise ReduceError(EARGS, "sources must be contiguous")
+    if not dst.is_contiguous():
+        raise ReduceError(EARGS, "dst must be contiguous")
+    r.sum_n(dst, srcs, nbytes, from_torch(dst.dtype), mode)
+    return dst

@@ -1,0 +1,264 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+vectors and the CPU oracle, on a real MI355X.
+
+Bar: bit-exact for every dtype in reference mode (fp32/fp64 NaN+NaN payloads
+compared by class against the reference fixtures, whose choice is
+schedule-dependent, but bit-exact against the oracle restatement); ACCUM_F32
+mode within 1 ulp of the exactly rounded sum.
+"""
+import numpy as np
+import pytest
+
+from golden_util import assert_bytes_match, case_id, expected, inputs, manifest
+from oracle.oracle import PortReducer
+from prophet_amd import synth
+from prophet_amd.dtypes import ALL_DTYPES, DType, elem_size
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+CASES = manifest()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def red(dev):
+    from prophet_amd.reducer import GpuReducer
+    return GpuReducer(device=0)
+
+
+@pytest.fixture(scope="module")
+def port():
+    return PortReducer(nthreads=8)
+
+
+def to_dev(a: np.ndarray, dev, pad: int = 0, offset: int = 0):
+    """Device copy of host bytes at byte `offset` inside a larger buffer."""
+    buf = torch.full((len(a) + offset + pad + 16,), 0xEE, dtype=torch.uint8, device=dev)
+    if len(a):
+        buf[offset: offset + len(a)] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return buf, buf[offset: offset + len(a)] if len(a) else buf[offset:offset]
+
+
+def ptr(buf, offset=0):
+    return buf.data_ptr() + offset
+
+
+def run_gpu(red, dev, case, ins, offset=0):
+    L = case["len_bytes"]
+    if case["op"] == "copy":
+        dbuf, _ = to_dev(np.full(L, 0xA5, np.uint8), dev, offset=offset)
+        sbuf, _ = to_dev(ins[0], dev, offset=offset)
+        red.copy(ptr(dbuf, offset), ptr(sbuf, offset), L)
+    elif case["op"] == "sum3":
+        dbuf, _ = to_dev(np.full(L, 0xA5, np.uint8), dev, offset=offset)
+        a, _ = to_dev(ins[0], dev, offset=offset)
+        b, _ = to_dev(ins[1], dev, offset=offset)
+        red.sum3(ptr(dbuf, offset), ptr(a, offset), ptr(b, offset), L, case["dtype"])
+    else:
+        bufs = [to_dev(x, dev, offset=offset)[0] for x in ins]
+        dbuf, _ = to_dev(np.full(L, 0x5A, np.uint8), dev, offset=offset)
+        red.sum_n(ptr(dbuf, offset), [ptr(b, offset) for b in bufs], L, case["dtype"])
+    torch.cuda.synchronize()
+    return dbuf[offset: offset + L].cpu().numpy()
+
+
+@pytest.mark.parametrize("case", CASES, ids=case_id)
+def test_golden(red, dev, port, case):
+    ins = inputs(case)
+    got = run_gpu(red, dev, case, ins)
+    assert_bytes_match(case["dtype"], got, expected(case), what=case_id(case))
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["op"] == "fold" and
+                                  c["value_class"] in ("special", "bits")], ids=case_id)
+def test_golden_vs_port_bit_exact(red, dev, port, case):
+    """Against the restatement the NaN rule is deterministic: every bit must match."""
+    ins = inputs(case)
+    got = run_gpu(red, dev, case, ins)
+    L = case["len_bytes"]
+    want = np.zeros(L, np.uint8)
+    port.sum_n(want, ins, L, case["dtype"])
+    assert_bytes_match(case["dtype"], got, want, nan_class_f32_f64=False, what=case_id(case))
+
+
+@pytest.mark.parametrize("dt", list(ALL_DTYPES), ids=lambda d: DType(d).name)
+@pytest.mark.parametrize("offset", [0, 2, 4, 8, 12])
+def test_misaligned_coaligned(red, dev, port, dt, offset):
+    """Sub-bucket views (e.g. a shard inside a partition) start anywhere."""
+    es = elem_size(dt)
+    if offset % es:
+        pytest.skip("not element aligned")
+    n = 4099 + 13
+    L = n * es
+    ins = [np.ascontiguousarray(synth.bucket(dt, n, k, "special" if dt in
+           (DType.FLOAT16, DType.FLOAT32) else "normal", 321)).view(np.uint8) for k in range(3)]
+    case = {"op": "fold", "len_bytes": L, "dtype": int(dt)}
+    got = run_gpu(red, dev, case, ins, offset=offset)
+    want = np.zeros(L, np.uint8)
+    port.sum_n(want, ins, L, dt)
+    assert_bytes_match(dt, got, want, nan_class_f32_f64=False, what=f"off={offset}")
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.INT64, DType.UINT8],
+                         ids=lambda d: DType(d).name)
+def test_not_coaligned_and_unaligned(red, dev, port, dt):
+    """Operands with different (or no) element alignment take the element path."""
+    es = elem_size(dt)
+    n = 1000 + 7
+    L = n * es
+    ins = [np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 55)).view(np.uint8)
+           for k in range(4)]
+    offs = [0, es, 3 * es, 1]  # last source not even element-aligned
+    bufs = [to_dev(x, dev, offset=o)[0] for x, o in zip(ins, offs)]
+    dbuf, _ = to_dev(np.zeros(L, np.uint8), dev, offset=5)
+    red.sum_n(ptr(dbuf, 5), [ptr(b, o) for b, o in zip(bufs, offs)], L, dt)
+    torch.cuda.synchronize()
+    want = np.zeros(L, np.uint8)
+    port.sum_n(want, ins, L, dt)
+    assert_bytes_match(dt, dbuf[5:5 + L].cpu().numpy(), want, nan_class_f32_f64=False)
+
+
+@pytest.mark.parametrize("dt", list(ALL_DTYPES), ids=lambda d: DType(d).name)
+def test_engine_pattern_equals_fused(red, dev, dt):
+    """N-1 in-place sum() calls (server.cc:127-130 engine loop) == one sum_n()."""
+    es = elem_size(dt)
+    n = 65536 + 5
+    L = n * es
+    ins = [torch.from_numpy(np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 9))
+                            .view(np.uint8)).to(dev) for k in range(8)]
+    acc = ins[0].clone()
+    for s in ins[1:]:
+        red.sum(acc, s, L, dt)
+    fused = torch.empty_like(acc)
+    red.sum_n(fused, ins, L, dt)
+    inplace = ins[0].clone()
+    red.sum_n(inplace, [inplace] + ins[1:], L, dt)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, fused)
+    assert torch.equal(acc, inplace)
+
+
+def test_more_than_32_sources_chains_left_fold(red, dev, port):
+    dt, n = DType.FLOAT16, 3001
+    ins = [np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 4)).view(np.uint8)
+           for k in range(40)]
+    bufs = [torch.from_numpy(x).to(dev) for x in ins]
+    out = torch.empty_like(bufs[0])
+    red.sum_n(out, bufs, n * 2, dt)
+    torch.cuda.synchronize()
+    want = np.zeros(n * 2, np.uint8)
+    port.sum_n(want, ins, n * 2, dt)
+    assert_bytes_match(dt, out.cpu().numpy(), want, nan_class_f32_f64=False)
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.BFLOAT16, DType.INT32],
+                         ids=lambda d: DType(d).name)
+def test_batched_block_matches_oracle(red, dev, port, dt):
+    """One Prophet block (many buckets of ResNet-like sizes, 128 B .. 1 MiB) in one launch."""
+    from prophet_amd.buckets import resnet50_param_sizes
+    es = elem_size(dt)
+    sizes = resnet50_param_sizes()[:40]          # ragged, many < 1 KiB
+    N = 8
+    buckets, wants = [], []
+    keep = []
+    for i, ne in enumerate(sizes):
+        L = ne * es
+        ins = [np.ascontiguousarray(synth.bucket(dt, ne, k, "normal", 100 + i)).view(np.uint8)
+               for k in range(N)]
+        srcs = [torch.from_numpy(x).to(dev) for x in ins]
+        dst = srcs[0] if i % 2 == 0 else torch.empty_like(srcs[0])   # alias or not
+        keep += srcs + [dst]
+        buckets.append((dst, srcs, L))
+        w = np.zeros(L, np.uint8)
+        port.sum_n(w, ins, L, dt)
+        wants.append(w)
+    red.sum_batched(buckets, dt)
+    torch.cuda.synchronize()
+    for (dst, _, L), w in zip(buckets, wants):
+        assert_bytes_match(dt, dst.cpu().numpy(), w, nan_class_f32_f64=False)
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT16, DType.BFLOAT16], ids=lambda d: DType(d).name)
+def test_accum_f32_mode_within_one_ulp(red, dev, dt):
+    from prophet_amd.reducer import MODE_ACCUM_F32
+    n, N = 200_003, 16
+    ins = [torch.from_numpy(np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 3))
+                            .view(np.uint8)).to(dev) for k in range(N)]
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, n * 2, dt, mode=MODE_ACCUM_F32)
+    td = torch.float16 if dt == DType.FLOAT16 else torch.bfloat16
+    exact = sum(x.view(td).double() for x in ins)
+    rounded = exact.to(td)
+    got = out.view(td)
+    # ulp of the correctly rounded result
+    nxt = torch.nextafter(rounded.float(), torch.full_like(rounded.float(), float("inf"))).to(td)
+    ulp = (nxt.double() - rounded.double()).abs().clamp_min(2.0 ** -24)
+    err = (got.double() - exact).abs()
+    assert bool((err <= 1.0 * ulp + 1e-30).all())
+
+
+def test_full_size_config2_properties(red, dev):
+    """BASELINE config 2 at full size: 8 x 256 MiB fp32.  The fused fold must
+    equal torch's own pairwise left fold bit for bit (IEEE fp32 adds, finite
+    inputs), and a sampled window must match the oracle."""
+    n = (256 << 20) // 4
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234)
+    ins = [torch.randn(n, device=dev, generator=gen) for _ in range(8)]
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, n * 4, DType.FLOAT32)
+    ref = ins[0].clone()
+    for s in ins[1:]:
+        ref.add_(s)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    # sampled oracle window
+    port = PortReducer(nthreads=8)
+    lo = 12_345_678
+    win = [x[lo: lo + 1_000_003].cpu().numpy().view(np.uint8) for x in ins]
+    want = np.zeros_like(win[0])
+    port.sum_n(want, win, want.nbytes, DType.FLOAT32)
+    assert np.array_equal(out[lo: lo + 1_000_003].cpu().numpy().view(np.uint8), want)
+
+
+def test_full_size_fp16_left_fold_equals_torch(red, dev):
+    """fp16 at 98 MiB: per-step RNE left fold == torch half add chain."""
+    n = 51_114_064  # ResNet-50 element count
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    ins = [torch.randn(n, device=dev, generator=gen).half() for _ in range(8)]
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, n * 2, DType.FLOAT16)
+    ref = ins[0].clone()
+    for s in ins[1:]:
+        ref.add_(s)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+
+
+def test_stream_ordering_on_side_stream(red, dev):
+    s = torch.cuda.Stream()
+    n = 1 << 22
+    a = torch.ones(n, device=dev)
+    b = torch.full((n,), 2.0, device=dev)
+    with torch.cuda.stream(s):
+        a.mul_(3.0)                       # must complete before the reduce
+        red.sum(a, b, n * 4, DType.FLOAT32)  # picks up torch's current stream = s
+        a.add_(1.0)
+    s.synchronize()
+    assert bool((a == 6.0).all())
+
+
+def test_bad_dtype_raises(red, dev):
+    from prophet_amd.reducer import EDTYPE, ReduceError
+    a = torch.zeros(64, dtype=torch.uint8, device=dev)
+    with pytest.raises(ReduceError) as e:
+        red.sum(a, a.clone(), 64, 10)
+    assert e.value.code == EDTYPE

@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, tuning sweep, rocprof kernel
+# trace.  Each GPU step has its own time limit; the script stops at the first
+# step that ends in anything other than success or an ordinary test failure
+# (fault, abort, segfault, timeout).  Output: gpurun_out/<tag>/...
+#   usage: tools/gpu_round.sh <tag> [steps...]   steps: test smoke bench sweep prof pmc
+set -u
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"test smoke bench sweep prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a "$OUT/steps.log"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    sweep) run sweep 600 python tools/sweep.py ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+    pmc)   run pmc 900 python tools/pmc_traffic.py --out "$OUT/pmc" ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "done"
