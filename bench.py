@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--bucket-mib", type=float, default=256.0)
     p.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
     p.add_argument("--sets", type=int, default=3, help="rotated input sets")
+    p.add_argument("--layout", default="arena", choices=["arena", "separate"],
+                   help="worker slots in one skewed HBM arena, or separate allocations")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-mib", type=float, default=64.0,
                    help="bucket size of the CPU baseline sample")
@@ -146,7 +148,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from prophet_amd import synth
+    from prophet_amd.arena import BucketArena
     from prophet_amd.dtypes import DType
     from prophet_amd.reducer import GpuReducer
 
@@ -157,20 +159,22 @@ def main():
     n_elems = B // es
     red = GpuReducer(device=local_rank)
 
-    # Input sets: worker k's bucket of GPU `rank`'s key-space slice.  Seeded
-    # per (rank, set, worker); generated on device from the synthetic stream of
-    # one 1 MiB tile to keep setup fast, then perturbed per copy so buckets differ.
+    # Input sets: the server's per-worker receive slots for this GPU's bucket,
+    # carved from one HBM arena (prophet_amd/arena.py: skewed slots avoid the
+    # channel aliasing of power-of-two-spaced buffers), plus the output slot.
+    # Seeded N(0,1) gradients per (rank, set, worker), generated on device.
     torch.manual_seed(1000 + rank)
+    tdt = {DType.FLOAT32: torch.float32, DType.FLOAT16: torch.float16,
+           DType.BFLOAT16: torch.bfloat16}[dtype_id]
     sets = []
     for s in range(args.sets):
-        srcs = []
-        for k in range(N):
-            t = torch.empty(n_elems, dtype=torch.float32, device=dev)
-            t.normal_()
-            srcs.append(t.to({DType.FLOAT32: torch.float32, DType.FLOAT16: torch.float16,
-                              DType.BFLOAT16: torch.bfloat16}[dtype_id]).view(torch.uint8))
-        dst = torch.empty(B, dtype=torch.uint8, device=dev)
-        sets.append((dst, srcs))
+        if args.layout == "arena":
+            slots = BucketArena(N + 1, B, dev).slots()
+        else:
+            slots = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(N + 1)]
+        for t in slots[:N]:
+            t.view(tdt).copy_(torch.randn(n_elems, device=dev))
+        sets.append((slots[N], slots[:N]))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
@@ -205,8 +209,6 @@ def main():
 
     # Correctness spot check of the last set against torch's own left fold.
     dst, srcs = sets[(args.steps + args.warmup - 1) % len(sets)]
-    tdt = {DType.FLOAT32: torch.float32, DType.FLOAT16: torch.float16,
-           DType.BFLOAT16: torch.bfloat16}[dtype_id]
     chk = srcs[0].view(tdt)[: 1 << 20].clone()
     for s in srcs[1:]:
         chk.add_(s.view(tdt)[: 1 << 20])
@@ -233,7 +235,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (torch.randn on device, seeded per rank), resident in HBM, "
-                f"{args.sets} rotated input sets",
+                f"{args.sets} rotated input sets, layout={args.layout}",
         "config": {"workload": workload, "n_workers": N, "bucket_bytes": B,
                    "parallelism": f"key-space shard x{world}", "kernel": "byteps_reduce_sum_n",
                    "tuning": {"vpt": tv, "nt": tnt, "max_grid": tgrid}},

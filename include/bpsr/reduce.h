@@ -136,8 +136,9 @@ int byteps_reduce_dtype_size(int dtype);
 const char* byteps_reduce_last_error(void);
 
 /* Launch tuning (process-wide; defaults chosen from rocprof measurements, see
- * DESIGN.md).  vpt: 16-B vectors per thread per source per step (1, 2 or 4);
- * nt: non-temporal input loads (0/1); max_grid: grid cap in 256-thread blocks.
+ * DESIGN.md).  vpt: 16-B vectors per thread per tile (2, 4 or 8);
+ * nt: non-temporal loads and stores (0/1); max_grid: grid cap in 256-thread
+ * workgroups (tile-stride beyond).
  * A value <= 0 (nt: < 0) keeps the current setting.  Also settable through
  * the environment: BPSR_VPT, BPSR_NT, BPSR_MAX_GRID. */
 int byteps_reduce_set_tuning(int vpt, int nt, int max_grid);

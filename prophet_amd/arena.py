@@ -1,0 +1,33 @@
+"""HBM layout of per-worker bucket slots.
+
+The server keeps one receive slot per pushing worker for each bucket (the
+ps-lite receive buffers of byteps/server/server.cc:174,216-218, here resident
+in HBM).  Slots are carved from one device slab with a small skew between
+consecutive workers: with slots exactly a power of two apart (e.g. 256 MiB
+buckets from separate allocations), the N concurrent read streams of the fold
+alias onto the same HBM channel/bank pattern; a skew of a few KiB spreads
+them (measured on MI355X: +2-5 % on the 8-way 256 MiB fold over separate
+allocations, tools/sweep.py; DESIGN.md "HBM layout").
+"""
+from __future__ import annotations
+
+DEFAULT_SKEW = 16 * 1024   # bytes between consecutive slots beyond the (4 KiB-rounded) bucket
+ALIGN = 4096
+
+
+class BucketArena:
+    """``n_slots`` buckets of ``bucket_bytes`` in one uint8 device tensor."""
+
+    def __init__(self, n_slots: int, bucket_bytes: int, device, skew: int = DEFAULT_SKEW):
+        import torch
+        self.bucket_bytes = int(bucket_bytes)
+        self.stride = (self.bucket_bytes + ALIGN - 1) // ALIGN * ALIGN + int(skew)
+        self.n_slots = n_slots
+        self.slab = torch.empty(self.stride * n_slots, dtype=torch.uint8, device=device)
+
+    def slot(self, k: int):
+        o = k * self.stride
+        return self.slab[o: o + self.bucket_bytes]
+
+    def slots(self):
+        return [self.slot(k) for k in range(self.n_slots)]

@@ -82,12 +82,12 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 
 static Tuning& tuning() {
   static Tuning tu = [] {
-    Tuning t{4, 0, 2048};
+    Tuning t{4, 1, 1 << 20};
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
-    if (t.vpt != 1 && t.vpt != 2) t.vpt = 4;
-    if (t.max_grid < 1) t.max_grid = 2048;
+    if (t.vpt != 2 && t.vpt != 8) t.vpt = 4;
+    if (t.max_grid < 1) t.max_grid = 1 << 20;
     t.nt = t.nt ? 1 : 0;
     return t;
   }();
@@ -200,7 +200,8 @@ const char* byteps_reduce_last_error(void) { return g_last_error.c_str(); }
 int byteps_reduce_set_tuning(int vpt, int nt, int max_grid) {
   Tuning& t = tuning();
   if (vpt > 0) {
-    if (vpt != 1 && vpt != 2 && vpt != 4) return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2 or 4");
+    if (vpt != 2 && vpt != 4 && vpt != 8)
+      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 2, 4 or 8");
     t.vpt = vpt;
   }
   if (nt >= 0) t.nt = nt ? 1 : 0;

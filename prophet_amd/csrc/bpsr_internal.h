@@ -49,9 +49,9 @@ struct BatchEntry {
 };
 
 struct Tuning {
-  int vpt;       // 16-B vectors per thread per source per step (1, 2, 4)
-  int nt;        // non-temporal loads
-  int max_grid;  // grid cap (grid-stride beyond)
+  int vpt;       // 16-B vectors per thread per tile (2, 4, 8)
+  int nt;        // non-temporal loads and stores
+  int max_grid;  // grid cap in workgroups (tile-stride beyond)
 };
 
 int elem_size(int dtype);  // 0 if unsupported
@@ -61,15 +61,32 @@ int elem_size(int dtype);  // 0 if unsupported
 void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, int n,
                bool copy_trailing, FoldGeom* g, int* aligned);
 
-inline int fold_grid(const FoldGeom& g, const Tuning& tu) {
+// Tiles of kBlock*vpt vectors; one workgroup per tile up to max_grid, then
+// tile-stride.  The element path reuses the same threads (grid-stride).
+inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
+  const uint64_t tile = (uint64_t)kBlock * vpt;
+  uint64_t blocks = (g.nvec + tile - 1) / tile;
   const uint64_t scalar = g.head_elems + (g.n_elems - g.tail_begin) + g.trailing_bytes;
-  uint64_t work = (g.nvec + tu.vpt - 1) / tu.vpt;
-  if (scalar > work) work = scalar;
-  uint64_t blocks = (work + kBlock - 1) / kBlock;
+  const uint64_t sblocks = (scalar + kBlock - 1) / kBlock;
+  if (sblocks > blocks) blocks = sblocks;
   if (blocks > (uint64_t)tu.max_grid) blocks = tu.max_grid;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
 }
+
+#define BPSR_DECLARE_LAUNCHERS(NAME)                                                      \
+  hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s);      \
+  hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
+                                   uint32_t nt, const Tuning& tu, hipStream_t s);
+BPSR_DECLARE_LAUNCHERS(f32)
+BPSR_DECLARE_LAUNCHERS(f64)
+BPSR_DECLARE_LAUNCHERS(f16)
+BPSR_DECLARE_LAUNCHERS(f16acc)
+BPSR_DECLARE_LAUNCHERS(bf16)
+BPSR_DECLARE_LAUNCHERS(bf16acc)
+BPSR_DECLARE_LAUNCHERS(i8)
+BPSR_DECLARE_LAUNCHERS(i32)
+BPSR_DECLARE_LAUNCHERS(i64)
 
 hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);

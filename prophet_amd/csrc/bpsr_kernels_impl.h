@@ -1,0 +1,275 @@
+// CDNA4 (gfx950) kernels of the gradient-bucket reduce path — templates.
+// Instantiated per dtype in bpsr_k_*.hip (parallel compilation).
+//
+//   fold_kernel     dst = ((s0 + s1) + ...) + s_{n-1}, one bucket, one launch.
+//                   Replaces the (N-1) CpuReducer::sum calls of one server
+//                   round (server.cc:216-250, cpu_reducer.cc:86-91) with a
+//                   single pass: (N+1)*B HBM bytes instead of (3N-1)*B.
+//   batched_kernel  the same over a table of buckets (one Prophet block,
+//                   scheduled_queue.cc:244-296) in one launch.
+//
+// Design (pure HBM streaming, no reuse, no LDS, no MFMA):
+//   * the vector range is cut into tiles of kBlock*VPT 16-byte vectors; a
+//     workgroup owns a whole tile (contiguous 4*VPT KiB of every operand), lane
+//     i of a wave reads base + 16*i, so every wave-instruction moves 1 KiB;
+//   * per source, the VPT loads of a thread are issued back to back, all before
+//     the dependent adds; the tile's stores leave as one burst at the end
+//     (measured: tiles of 8-16 vectors per thread stream 5-10 % faster than a
+//     grid-stride interleave, tools/hbm_probe.hip);
+//   * non-temporal loads and stores (`nt`): inputs are read once, the output is
+//     not re-read by this kernel;
+//   * strict left fold in registers, no reassociation (bit-exact with the
+//     reference order);
+//   * elements outside the 16-B vector range (unaligned head, tail, and the
+//     fp16 F16C-tail region, cpu_reducer.cc:118-125) go through the element
+//     path with the reference's tail semantics.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bpsr_internal.h"
+#include "bpsr_ops.h"
+
+namespace bpsr {
+
+template <bool NT>
+__device__ __forceinline__ vec16 ld16(const unsigned char* p) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  if constexpr (NT) {
+    return bitcast<vec16>(__builtin_nontemporal_load(reinterpret_cast<const u4*>(p)));
+  } else {
+    return bitcast<vec16>(*reinterpret_cast<const u4*>(p));
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(unsigned char* p, const vec16& v) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  if constexpr (NT) {
+    __builtin_nontemporal_store(bitcast<u4>(v), reinterpret_cast<u4*>(p));
+  } else {
+    *reinterpret_cast<u4*>(p) = bitcast<u4>(v);
+  }
+}
+
+template <class E>
+__device__ __forceinline__ E ld_e(const unsigned char* p, bool aligned) {
+  if (aligned) return *reinterpret_cast<const E*>(p);
+  E v;
+  __builtin_memcpy(&v, p, sizeof(E));
+  return v;
+}
+
+template <class E>
+__device__ __forceinline__ void st_e(unsigned char* p, E v, bool aligned) {
+  if (aligned) {
+    *reinterpret_cast<E*>(p) = v;
+  } else {
+    __builtin_memcpy(p, &v, sizeof(E));
+  }
+}
+
+constexpr int cmin(int a, int b) { return a < b ? a : b; }
+
+// Exact replay of one vector's fold (NaN payload rules), re-reading memory.
+// Only runs for vectors whose fast-path result holds a NaN.
+template <class Op, bool NT>
+__device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* srcs, int n,
+                                                uint64_t off) {
+  typename Op::Acc acc = Op::init(ld16<NT>(srcs[0] + off));
+  for (int k = 1; k < n; ++k) Op::accum(acc, ld16<NT>(srcs[k] + off));
+  return Op::finish(acc);
+}
+
+// One tile: vectors [v0, v0 + kBlock*VPT) clipped to nvec, of the vector
+// range starting at byte `vec_off` of every operand.  Thread `lane` handles
+// v0 + j*kBlock + lane, j < VPT.
+//
+// Full tiles: the loads of G sources x VPT vectors are issued back to back
+// (G*VPT <= 32 16-B loads in flight per lane), then folded with plain adds
+// (Op::fast); a NaN anywhere in a chain survives to its result, so one
+// has_nan test per vector decides whether the exact NaN-payload rule must be
+// replayed (fold_vector_exact) — a wave-uniform branch that is never taken on
+// finite data.
+template <class Op, int VPT, bool NT, int NS>
+__device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int n,
+                                          unsigned char* dst, uint64_t vec_off, uint64_t v0,
+                                          uint64_t nvec, int lane) {
+  const int ns = NS > 0 ? NS : n;
+  const uint64_t off0 = vec_off + (v0 + lane) * 16;
+  constexpr uint64_t kStep = (uint64_t)kBlock * 16;
+  if (v0 + (uint64_t)kBlock * VPT <= nvec) {
+    constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
+    typename Op::Acc acc[VPT];
+    auto group = [&](int k0) __attribute__((always_inline)) {
+      vec16 x[G][VPT];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (NS > 0 || k0 + g < ns) {
+          const unsigned char* base = srcs[k0 + g] + off0;
+#pragma unroll
+          for (int j = 0; j < VPT; ++j) x[g][j] = ld16<NT>(base + j * kStep);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (NS > 0 || k0 + g < ns) {
+#pragma unroll
+          for (int j = 0; j < VPT; ++j) {
+            if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
+            else Op::fast(acc[j], x[g][j]);
+          }
+        }
+      }
+    };
+    if constexpr (NS > 0) {
+#pragma unroll
+      for (int k0 = 0; k0 < NS; k0 += G) group(k0);
+    } else {
+      for (int k0 = 0; k0 < ns; k0 += G) group(k0);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) bad |= Op::has_nan(acc[j]);
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      vec16 out = Op::finish(acc[j]);
+      if (__builtin_expect(bad, 0)) {
+        if (Op::has_nan(acc[j])) out = fold_vector_exact<Op, NT>(srcs, ns, off0 + j * kStep);
+      }
+      st16<NT>(dst + off0 + j * kStep, out);
+    }
+  } else {
+    // Partial (last) tile: exact fold per vector.
+    for (uint64_t v = v0 + lane; v < nvec; v += kBlock) {
+      const uint64_t off = vec_off + v * 16;
+      typename Op::Acc acc = Op::init(ld16<NT>(srcs[0] + off));
+      for (int k = 1; k < ns; ++k) Op::accum(acc, ld16<NT>(srcs[k] + off));
+      st16<NT>(dst + off, Op::finish(acc));
+    }
+  }
+}
+
+// Element part: elements [0, head) and [tail_begin, n_elems) plus trailing
+// bytes; elements >= tail_sem_from get the F16C-tail NaN rule (fp16 only).
+template <class Op>
+__device__ __forceinline__ void fold_elements(const unsigned char* const* srcs, int n,
+                                              unsigned char* dst, const FoldGeom& g,
+                                              bool aligned, uint64_t t, uint64_t stride) {
+  using E = typename Op::E;
+  const uint64_t n_head = g.head_elems;
+  const uint64_t n_tail = g.n_elems - g.tail_begin;
+  const uint64_t n_scalar = n_head + n_tail;
+  for (uint64_t s = t; s < n_scalar; s += stride) {
+    const uint64_t e = s < n_head ? s : g.tail_begin + (s - n_head);
+    const bool tail = e >= g.tail_sem_from;
+    const uint64_t off = e * sizeof(E);
+    typename Op::EAcc acc = Op::init_e(ld_e<E>(srcs[0] + off, aligned), tail);
+    for (int k = 1; k < n; ++k) Op::accum_e(acc, ld_e<E>(srcs[k] + off, aligned), tail);
+    st_e<E>(dst + off, Op::finish_e(acc, tail), aligned);
+  }
+  // Trailing len % sizeof(T) bytes of a fold into a separate dst: the fold's
+  // accumulator is the first arrival (server.cc:216-218), so they come from
+  // srcs[0].
+  if (g.copy_trailing) {
+    const uint64_t tb = g.n_elems * sizeof(E);
+    for (uint64_t b = t; b < g.trailing_bytes; b += stride) dst[tb + b] = srcs[0][tb + b];
+  }
+}
+
+template <class Op, int VPT, bool NT, int NS>
+__global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
+  const uint64_t tile_vecs = (uint64_t)kBlock * VPT;
+  const uint64_t ntiles = (a.g.nvec + tile_vecs - 1) / tile_vecs;
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    fold_tile<Op, VPT, NT, NS>(a.srcs, a.n, a.dst, a.g.vec_off, tile * tile_vecs, a.g.nvec,
+                               threadIdx.x);
+  fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0,
+                    (uint64_t)blockIdx.x * kBlock + threadIdx.x, (uint64_t)gridDim.x * kBlock);
+}
+
+// Batched: block b works on tile b of the concatenated tile space; a bucket's
+// tiles are [tile_start[i], tile_start[i+1]).  The element work of a bucket is
+// done by its first tile.
+template <class Op, int VPT, bool NT>
+__global__ __launch_bounds__(kBlock) void batched_kernel(const BatchEntry* __restrict__ tab,
+                                                         const uint32_t* __restrict__ tile_start,
+                                                         int nbuckets, uint32_t ntiles) {
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    int lo = 0, hi = nbuckets - 1;  // last i with tile_start[i] <= tile
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tile_start[mid] <= tile) lo = mid; else hi = mid - 1;
+    }
+    const BatchEntry& e = tab[lo];
+    const uint32_t local = tile - tile_start[lo];
+    fold_tile<Op, VPT, NT, 0>(e.srcs, e.n, e.dst, e.g.vec_off,
+                              (uint64_t)local * kBlock * VPT, e.g.nvec, threadIdx.x);
+    if (local == 0)
+      fold_elements<Op>(e.srcs, e.n, e.dst, e.g, e.aligned != 0, threadIdx.x, kBlock);
+  }
+}
+
+// ------------------------------------------------------------- launchers ----
+
+template <class Op, int VPT, bool NT, int NS>
+static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
+  hipLaunchKernelGGL((fold_kernel<Op, VPT, NT, NS>), dim3(fold_grid(a.g, tu, VPT)),
+                     dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+template <class Op, int VPT, bool NT>
+static hipError_t launch_fold_vpt(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
+  switch (a.n) {  // compile-time source counts for the common worker counts
+    case 2: return launch_fold_ns<Op, VPT, NT, 2>(a, tu, s);
+    case 8: return launch_fold_ns<Op, VPT, NT, 8>(a, tu, s);
+    case 16: return launch_fold_ns<Op, VPT, NT, 16>(a, tu, s);
+    default: return launch_fold_ns<Op, VPT, NT, 0>(a, tu, s);
+  }
+}
+
+template <class Op>
+static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
+  if (tu.nt) {
+    switch (tu.vpt) {
+      case 2: return launch_fold_vpt<Op, 2, true>(a, tu, s);
+      case 8: return launch_fold_vpt<Op, 8, true>(a, tu, s);
+      default: return launch_fold_vpt<Op, 4, true>(a, tu, s);
+    }
+  }
+  switch (tu.vpt) {
+    case 2: return launch_fold_vpt<Op, 2, false>(a, tu, s);
+    case 8: return launch_fold_vpt<Op, 8, false>(a, tu, s);
+    default: return launch_fold_vpt<Op, 4, false>(a, tu, s);
+  }
+}
+
+template <class Op>
+static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_start,
+                                    int nbuckets, uint32_t ntiles, const Tuning& tu,
+                                    hipStream_t s) {
+  const uint32_t grid = ntiles < (uint32_t)tu.max_grid ? ntiles : (uint32_t)tu.max_grid;
+  if (tu.nt)
+    hipLaunchKernelGGL((batched_kernel<Op, kBatchVPT, true>), dim3(grid), dim3(kBlock), 0, s,
+                       tab, tile_start, nbuckets, ntiles);
+  else
+    hipLaunchKernelGGL((batched_kernel<Op, kBatchVPT, false>), dim3(grid), dim3(kBlock), 0, s,
+                       tab, tile_start, nbuckets, ntiles);
+  return hipGetLastError();
+}
+
+}  // namespace bpsr
+
+// One translation unit per dtype family defines its entry points with this.
+#define BPSR_DEFINE_LAUNCHERS(NAME, OP)                                                   \
+  namespace bpsr {                                                                        \
+  hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s) {     \
+    return launch_fold_op<OP>(a, tu, s);                                                  \
+  }                                                                                       \
+  hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
+                                   uint32_t nt, const Tuning& tu, hipStream_t s) {        \
+    return launch_batched_op<OP>(tab, ts, nb, nt, tu, s);                                 \
+  }                                                                                       \
+  }

@@ -61,6 +61,17 @@ struct OpF32 {
       for (int i = 0; i < 4; ++i) a.w[i] = bitcast<uint32_t>(r[i]);
     }
   }
+  // Fast path: plain adds; a NaN anywhere in the chain leaves a NaN in the
+  // result (NaN + x = NaN, inf + -inf = NaN), so checking the result once
+  // decides whether the exact NaN-payload rule must be replayed (has_nan).
+  __device__ static void fast(Acc& a, const vec16& b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a.w[i] = bitcast<uint32_t>(bitcast<float>(a.w[i]) + bitcast<float>(b.w[i]));
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    return f32_nan(a.w[0]) || f32_nan(a.w[1]) || f32_nan(a.w[2]) || f32_nan(a.w[3]);
+  }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = f32_add(a, b); }
@@ -93,6 +104,13 @@ struct OpF64 {
     a1 = f64_add(a1, b1);
     a.w[0] = (uint32_t)a0; a.w[1] = (uint32_t)(a0 >> 32);
     a.w[2] = (uint32_t)a1; a.w[3] = (uint32_t)(a1 >> 32);
+  }
+  __device__ static void fast(Acc& a, const vec16& b) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    a = bitcast<vec16>(bitcast<d2>(a) + bitcast<d2>(b));
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    return f64_nan(((uint64_t)a.w[1] << 32) | a.w[0]) || f64_nan(((uint64_t)a.w[3] << 32) | a.w[2]);
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
@@ -139,6 +157,18 @@ struct OpF16 {
 #pragma unroll
     for (int i = 0; i < 4; ++i) a.w[i] = f16x2_add_body(a.w[i], b.w[i]);
   }
+  __device__ static void fast(Acc& a, const vec16& b) {  // v_pk_add_f16 x4
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a.w[i] = bitcast<uint32_t>(bitcast<h2_t>(a.w[i]) + bitcast<h2_t>(b.w[i]));
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    // (h & 0x7fff) + 0x03ff sets bit 15 of its lane iff h is a NaN
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t |= (a.w[i] & 0x7fff7fffu) + 0x03ff03ffu;
+    return (t & 0x80008000u) != 0;
+  }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool tail) { a = (E)f16_add_elem(a, b, tail); }
@@ -167,6 +197,20 @@ struct OpBF16 {
       uint32_t hi = bf16_add(a.w[i] >> 16, b.w[i] >> 16);
       a.w[i] = lo | (hi << 16);
     }
+  }
+  __device__ static void fast(Acc& a, const vec16& b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float lo = bitcast<float>(a.w[i] << 16) + bitcast<float>(b.w[i] << 16);
+      float hi = bitcast<float>(a.w[i] & 0xffff0000u) + bitcast<float>(b.w[i] & 0xffff0000u);
+      a.w[i] = f32_to_bf16_rne(bitcast<uint32_t>(lo)) | (f32_to_bf16_rne(bitcast<uint32_t>(hi)) << 16);
+    }
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    uint32_t t = 0;  // (h & 0x7fff) + 0x007f sets bit 15 iff h is a bf16 NaN
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t |= (a.w[i] & 0x7fff7fffu) + 0x007f007fu;
+    return (t & 0x80008000u) != 0;
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
@@ -207,6 +251,19 @@ struct OpAcc16 {
       a.f[2 * i + 1] = f32_add(a.f[2 * i + 1], up(b.w[i] >> 16));
     }
   }
+  __device__ static void fast(Acc& a, const vec16& b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a.f[2 * i] = bitcast<uint32_t>(bitcast<float>(a.f[2 * i]) + bitcast<float>(up(b.w[i] & 0xffffu)));
+      a.f[2 * i + 1] = bitcast<uint32_t>(bitcast<float>(a.f[2 * i + 1]) + bitcast<float>(up(b.w[i] >> 16)));
+    }
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    bool r = false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r |= f32_nan(a.f[i]);
+    return r;
+  }
   __device__ static vec16 finish(const Acc& a) {
     vec16 v;
 #pragma unroll
@@ -232,6 +289,8 @@ struct OpI8 {  // uint8 and int8: identical two's-complement bits
       a.w[i] = ((x & 0x7f7f7f7fu) + (y & 0x7f7f7f7fu)) ^ ((x ^ y) & 0x80808080u);
     }
   }
+  __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
+  __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = (E)(a + b); }
@@ -248,6 +307,8 @@ struct OpI32 {
 #pragma unroll
     for (int i = 0; i < 4; ++i) a.w[i] += b.w[i];
   }
+  __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
+  __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a += b; }
@@ -269,6 +330,8 @@ struct OpI64 {
       a.w[2 * i] = (uint32_t)x; a.w[2 * i + 1] = (uint32_t)(x >> 32);
     }
   }
+  __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
+  __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a += b; }

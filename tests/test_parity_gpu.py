@@ -197,9 +197,10 @@ def test_accum_f32_mode_within_one_ulp(red, dev, dt):
     exact = sum(x.view(td).double() for x in ins)
     rounded = exact.to(td)
     got = out.view(td)
-    # ulp of the correctly rounded result
-    nxt = torch.nextafter(rounded.float(), torch.full_like(rounded.float(), float("inf"))).to(td)
-    ulp = (nxt.double() - rounded.double()).abs().clamp_min(2.0 ** -24)
+    # ulp of the correctly rounded result (10 / 7 stored mantissa bits)
+    mbits, emin = (10, -14) if dt == DType.FLOAT16 else (7, -126)
+    mag = rounded.double().abs().clamp_min(2.0 ** emin)
+    ulp = torch.pow(2.0, torch.floor(torch.log2(mag)) - mbits)
     err = (got.double() - exact).abs()
     assert bool((err <= 1.0 * ulp + 1e-30).all())
 
