@@ -122,6 +122,18 @@ int byteps_reduce_sum_n(void* dst, const void* const* srcs, int n, size_t len,
 int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets,
                               int dtype, int mode, void* stream);
 
+/* A reusable batched reduction: the bucket table of one Prophet block is
+ * validated and uploaded to the device once (at plan creation, on the current
+ * device); every launch is then ONE kernel with no host work, no allocation
+ * and no synchronisation, so it can be captured into a hipGraph.  The reference
+ * keys, partitions and server receive buffers are fixed after InitTensor
+ * (operations.cc:219-316), so a block's table is fixed across iterations. */
+typedef struct byteps_reduce_plan byteps_reduce_plan;
+int byteps_reduce_plan_create(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
+                              int mode, byteps_reduce_plan** plan);
+int byteps_reduce_plan_launch(byteps_reduce_plan* plan, void* stream);
+int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
+
 /* CpuReducer::copy(dst, src, len), cpu_reducer.cc:209-220 (device to device). */
 int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream);
 

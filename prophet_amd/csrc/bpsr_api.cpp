@@ -82,7 +82,7 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 
 static Tuning& tuning() {
   static Tuning tu = [] {
-    Tuning t{4, 1, 1 << 20};
+    Tuning t{4, 1, 1 << 20};  // tools/sweep.py, profiles/r01_sweep_*.jsonl
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
@@ -181,6 +181,71 @@ static int stage_acquire(size_t bytes, StageSlot** out) {
   *out = &s;
   return BYTEPS_REDUCE_OK;
 }
+
+// ------------------------------------------------------- batch table build --
+struct TableInfo {
+  int vpt = kBatchVPT;   // tile size of the batched kernel for this table
+  int live = 0;          // buckets with len > 0
+  uint32_t tiles = 0;    // total tiles
+  size_t map_off = 0;    // byte offset of tile_bucket[] in the table
+  size_t bytes = 0;      // bytes to upload
+};
+
+// Validate buckets and write [BatchEntry x live][pad to 256][tile_bucket x tiles]
+// into `out`.  Every live bucket gets >= 1 tile so its element work runs.
+static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
+                       std::vector<char>& out, TableInfo* ti) {
+  std::vector<BatchEntry> tab;
+  tab.reserve(nbuckets);
+  uint64_t vecs = 0;
+  for (int i = 0; i < nbuckets; ++i) {
+    const byteps_bucket_desc& b = buckets[i];
+    if (b.n < 1 || b.n > kMaxSrcs)
+      return fail(BYTEPS_REDUCE_EARGS, "bucket %d: n=%d outside [1, %d]", i, b.n, kMaxSrcs);
+    if (b.len == 0) continue;
+    if (!b.dst) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null dst", i);
+    for (int k = 0; k < b.n; ++k) {
+      if (!b.srcs[k]) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null srcs[%d]", i, k);
+      if (overlaps_partially(b.dst, b.srcs[k], b.len) || (k > 0 && b.srcs[k] == b.dst))
+        return fail(BYTEPS_REDUCE_EARGS, "bucket %d: dst overlaps srcs[%d]", i, k);
+    }
+    BatchEntry e;
+    std::memset(&e, 0, sizeof(e));
+    for (int k = 0; k < b.n; ++k) e.srcs[k] = static_cast<const unsigned char*>(b.srcs[k]);
+    e.dst = static_cast<unsigned char*>(b.dst);
+    e.n = b.n;
+    make_geom(dtype, b.len, b.dst, b.srcs, b.n, b.dst != b.srcs[0], &e.g, &e.aligned);
+    vecs += e.g.nvec;
+    tab.push_back(e);
+  }
+  // Small batches (a Prophet block of a few MiB) get 256-vector tiles so the
+  // launch still has >= kMinTiles workgroups to spread over 256 CUs.
+  const int vpt = vecs / ((uint64_t)kBlock * kBatchVPT) >= kMinTiles ? kBatchVPT : 1;
+  const uint64_t tile_vecs = (uint64_t)kBlock * vpt;
+  uint64_t tiles = 0;
+  for (auto& e : tab) {
+    e.first_tile = (uint32_t)tiles;
+    const uint64_t t = (e.g.nvec + tile_vecs - 1) / tile_vecs;
+    tiles += t ? t : 1;
+    if (tiles > 0xffffffffull) return fail(BYTEPS_REDUCE_EARGS, "batch too large");
+  }
+  const size_t map_off = ((sizeof(BatchEntry) * tab.size()) + 255) & ~(size_t)255;
+  out.assign(map_off + sizeof(uint32_t) * (size_t)tiles, 0);
+  if (!tab.empty()) std::memcpy(out.data(), tab.data(), sizeof(BatchEntry) * tab.size());
+  uint32_t* map = reinterpret_cast<uint32_t*>(out.data() + map_off);
+  for (size_t b = 0; b < tab.size(); ++b) {
+    const uint32_t end = b + 1 < tab.size() ? tab[b + 1].first_tile : (uint32_t)tiles;
+    for (uint32_t t = tab[b].first_tile; t < end; ++t) map[t] = (uint32_t)b;
+  }
+  ti->vpt = vpt;
+  ti->live = (int)tab.size();
+  ti->tiles = (uint32_t)tiles;
+  ti->map_off = map_off;
+  ti->bytes = out.size();
+  return BYTEPS_REDUCE_OK;
+}
+
+static thread_local std::vector<char> g_table;
 
 }  // namespace bpsr
 
@@ -298,54 +363,80 @@ int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets, i
   if (nbuckets < 0 || (nbuckets > 0 && !buckets))
     return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
   if (nbuckets == 0) return BYTEPS_REDUCE_OK;
-  // Validate; count tiles (each bucket >= 1 tile so its element work runs).
-  const uint64_t tile_vecs = (uint64_t)kBlock * kBatchVPT;
-  const size_t tab_bytes = sizeof(BatchEntry) * (size_t)nbuckets;
-  const size_t ts_off = (tab_bytes + 255) & ~(size_t)255;
-  const size_t bytes = ts_off + sizeof(uint32_t) * (size_t)(nbuckets + 1);
+  TableInfo ti;
+  if ((rc = build_table(buckets, nbuckets, dtype, g_table, &ti))) return rc;
+  if (ti.live == 0) return BYTEPS_REDUCE_OK;
   StageSlot* slot = nullptr;
-  if ((rc = stage_acquire(bytes, &slot))) return rc;
-  BatchEntry* tab = static_cast<BatchEntry*>(slot->host);
-  uint32_t* ts = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->host) + ts_off);
-  uint64_t tiles = 0;
-  int live = 0;
-  for (int i = 0; i < nbuckets; ++i) {
-    const byteps_bucket_desc& b = buckets[i];
-    if (b.n < 1 || b.n > kMaxSrcs)
-      return fail(BYTEPS_REDUCE_EARGS, "bucket %d: n=%d outside [1, %d]", i, b.n, kMaxSrcs);
-    if (b.len == 0) continue;
-    if (!b.dst) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null dst", i);
-    for (int k = 0; k < b.n; ++k) {
-      if (!b.srcs[k]) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null srcs[%d]", i, k);
-      if (overlaps_partially(b.dst, b.srcs[k], b.len) || (k > 0 && b.srcs[k] == b.dst))
-        return fail(BYTEPS_REDUCE_EARGS, "bucket %d: dst overlaps srcs[%d]", i, k);
-    }
-    BatchEntry& e = tab[live];
-    std::memset(&e, 0, sizeof(e));
-    for (int k = 0; k < b.n; ++k) e.srcs[k] = static_cast<const unsigned char*>(b.srcs[k]);
-    e.dst = static_cast<unsigned char*>(b.dst);
-    e.n = b.n;
-    make_geom(dtype, b.len, b.dst, b.srcs, b.n, b.dst != b.srcs[0], &e.g, &e.aligned);
-    ts[live] = (uint32_t)tiles;
-    uint64_t t = (e.g.nvec + tile_vecs - 1) / tile_vecs;
-    tiles += t ? t : 1;
-    if (tiles > 0xffffffffull) return fail(BYTEPS_REDUCE_EARGS, "batch too large");
-    ++live;
-  }
-  if (live == 0) return BYTEPS_REDUCE_OK;
-  ts[live] = (uint32_t)tiles;
-  // Pack tile_start right behind the live entries' slot region.
+  if ((rc = stage_acquire(ti.bytes, &slot))) return rc;
+  std::memcpy(slot->host, g_table.data(), ti.bytes);
   hipStream_t s = to_stream(stream);
-  hipError_t e = hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, s);
+  hipError_t e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
   e = launch_batched(static_cast<const BatchEntry*>(slot->dev),
-                     reinterpret_cast<const uint32_t*>(static_cast<char*>(slot->dev) + ts_off),
-                     live, (uint32_t)tiles, dtype, mode, tuning(), s);
+                     reinterpret_cast<const uint32_t*>(static_cast<char*>(slot->dev) + ti.map_off),
+                     ti.live, ti.tiles, ti.vpt, dtype, mode, tuning(), s);
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
   e = hipEventRecord(slot->done, s);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
   slot->pending = true;
   return BYTEPS_REDUCE_OK;
+}
+
+struct byteps_reduce_plan {
+  int device;
+  int dtype;
+  int mode;
+  void* dev_table;
+  TableInfo ti;
+};
+
+int byteps_reduce_plan_create(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
+                              int mode, byteps_reduce_plan** out) {
+  if (!out) return fail(BYTEPS_REDUCE_EARGS, "null plan out-pointer");
+  *out = nullptr;
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (nbuckets < 0 || (nbuckets > 0 && !buckets))
+    return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
+  std::vector<char> host;
+  TableInfo ti;
+  if ((rc = build_table(buckets, nbuckets, dtype, host, &ti))) return rc;
+  auto* p = new byteps_reduce_plan();
+  p->dtype = dtype;
+  p->mode = mode;
+  p->ti = ti;
+  p->dev_table = nullptr;
+  hipError_t e = hipGetDevice(&p->device);
+  if (e == hipSuccess && ti.live > 0) {
+    e = hipMalloc(&p->dev_table, ti.bytes);
+    if (e == hipSuccess)
+      e = hipMemcpy(p->dev_table, host.data(), ti.bytes, hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    if (p->dev_table) (void)hipFree(p->dev_table);
+    delete p;
+    return hip_fail(e, "plan table upload");
+  }
+  *out = p;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_plan_launch(byteps_reduce_plan* p, void* stream) {
+  if (!p) return fail(BYTEPS_REDUCE_EARGS, "null plan");
+  if (p->ti.live == 0) return BYTEPS_REDUCE_OK;
+  hipError_t e = launch_batched(
+      static_cast<const BatchEntry*>(p->dev_table),
+      reinterpret_cast<const uint32_t*>(static_cast<char*>(p->dev_table) + p->ti.map_off),
+      p->ti.live, p->ti.tiles, p->ti.vpt, p->dtype, p->mode, tuning(), to_stream(stream));
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "plan kernel launch");
+}
+
+int byteps_reduce_plan_destroy(byteps_reduce_plan* p) {
+  if (!p) return BYTEPS_REDUCE_OK;
+  hipError_t e = hipSuccess;
+  if (p->dev_table) e = hipFree(p->dev_table);
+  delete p;
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "plan free");
 }
 
 int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream) {

@@ -16,7 +16,10 @@ enum : int { kModeReference = 0, kModeAccumF32 = 1 };
 
 constexpr int kBlock = 256;     // 4 waves of 64
 constexpr int kMaxSrcs = 32;    // BYTEPS_REDUCE_MAX_SRCS
-constexpr int kBatchVPT = 4;    // vectors per thread per tile in the batched kernel
+constexpr int kBatchVPT = 4;    // vectors per thread per tile in the batched kernel (large batches)
+// Fewer tiles than this leave CUs idle (256 CUs, several workgroups each):
+// launches that would get fewer fall back to smaller tiles.
+constexpr uint64_t kMinTiles = 2048;
 
 // Byte/element geometry of one fold, identical for every operand (the vector
 // path needs all operands co-aligned mod 16).
@@ -46,6 +49,8 @@ struct BatchEntry {
   int n;
   int aligned;
   FoldGeom g;
+  uint32_t first_tile;  // index of the bucket's first tile in the launch
+  uint32_t pad;
 };
 
 struct Tuning {
@@ -77,7 +82,7 @@ inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
 #define BPSR_DECLARE_LAUNCHERS(NAME)                                                      \
   hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s);      \
   hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
-                                   uint32_t nt, const Tuning& tu, hipStream_t s);
+                                   uint32_t nt, int vpt, const Tuning& tu, hipStream_t s);
 BPSR_DECLARE_LAUNCHERS(f32)
 BPSR_DECLARE_LAUNCHERS(f64)
 BPSR_DECLARE_LAUNCHERS(f16)
@@ -90,9 +95,17 @@ BPSR_DECLARE_LAUNCHERS(i64)
 
 hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);
-hipError_t launch_batched(const BatchEntry* tab, const uint32_t* tile_start, int nbuckets,
-                          uint32_t ntiles, int dtype, int mode, const Tuning& tu,
+hipError_t launch_batched(const BatchEntry* tab, const uint32_t* tile_bucket, int nbuckets,
+                          uint32_t ntiles, int vpt, int dtype, int mode, const Tuning& tu,
                           hipStream_t s);
+
+// Tile size actually used for a single fold: the tuned vpt, halved while the
+// launch would have fewer than kMinTiles tiles.
+inline int fold_vpt(uint64_t nvec, int vpt) {
+  while (vpt > 1 && (nvec + (uint64_t)kBlock * vpt - 1) / ((uint64_t)kBlock * vpt) < kMinTiles)
+    vpt >>= 1;
+  return vpt;
+}
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s);
 

@@ -86,73 +86,79 @@ __device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* s
 // range starting at byte `vec_off` of every operand.  Thread `lane` handles
 // v0 + j*kBlock + lane, j < VPT.
 //
-// Full tiles: the loads of G sources x VPT vectors are issued back to back
-// (G*VPT <= 32 16-B loads in flight per lane), then folded with plain adds
-// (Op::fast); a NaN anywhere in a chain survives to its result, so one
-// has_nan test per vector decides whether the exact NaN-payload rule must be
-// replayed (fold_vector_exact) — a wave-uniform branch that is never taken on
-// finite data.
+// The loads of G sources x VPT vectors are issued back to back (G*VPT <= 32
+// 16-B loads in flight per lane), then folded with plain adds (Op::fast); a
+// NaN anywhere in a chain survives to its result, so one has_nan test per
+// vector decides whether the exact NaN-payload rule must be replayed
+// (fold_vector_exact) — a wave-uniform branch never taken on finite data.
+// GUARD: the last, partial tile (vectors past nvec are neither read nor written).
+template <class Op, int VPT, bool NT, int NS, bool GUARD>
+__device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs, int n,
+                                               unsigned char* dst, uint64_t vec_off,
+                                               uint64_t v0, uint64_t nvec, int lane) {
+  const int ns = NS > 0 ? NS : n;
+  const uint64_t off0 = vec_off + (v0 + lane) * 16;
+  constexpr uint64_t kStep = (uint64_t)kBlock * 16;
+  constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
+  bool valid[VPT];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) valid[j] = !GUARD || (v0 + lane + (uint64_t)j * kBlock < nvec);
+  typename Op::Acc acc[VPT];
+  auto group = [&](int k0) __attribute__((always_inline)) {
+    vec16 x[G][VPT];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (NS > 0 || k0 + g < ns) {
+        const unsigned char* base = srcs[k0 + g] + off0;
+#pragma unroll
+        for (int j = 0; j < VPT; ++j)
+          x[g][j] = valid[j] ? ld16<NT>(base + j * kStep) : vec16{{0, 0, 0, 0}};
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (NS > 0 || k0 + g < ns) {
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+          if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
+          else Op::fast(acc[j], x[g][j]);
+        }
+      }
+    }
+  };
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int k0 = 0; k0 < NS; k0 += G) group(k0);
+  } else {
+    for (int k0 = 0; k0 < ns; k0 += G) group(k0);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) bad |= valid[j] && Op::has_nan(acc[j]);
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    vec16 out = Op::finish(acc[j]);
+    if (__builtin_expect(bad, 0)) {
+      if (valid[j] && Op::has_nan(acc[j]))
+        out = fold_vector_exact<Op, NT>(srcs, ns, off0 + j * kStep);
+    }
+    if (valid[j]) st16<NT>(dst + off0 + j * kStep, out);
+  }
+}
+
 template <class Op, int VPT, bool NT, int NS>
 __device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int n,
                                           unsigned char* dst, uint64_t vec_off, uint64_t v0,
                                           uint64_t nvec, int lane) {
-  const int ns = NS > 0 ? NS : n;
-  const uint64_t off0 = vec_off + (v0 + lane) * 16;
-  constexpr uint64_t kStep = (uint64_t)kBlock * 16;
-  if (v0 + (uint64_t)kBlock * VPT <= nvec) {
-    constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
-    typename Op::Acc acc[VPT];
-    auto group = [&](int k0) __attribute__((always_inline)) {
-      vec16 x[G][VPT];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if (NS > 0 || k0 + g < ns) {
-          const unsigned char* base = srcs[k0 + g] + off0;
-#pragma unroll
-          for (int j = 0; j < VPT; ++j) x[g][j] = ld16<NT>(base + j * kStep);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if (NS > 0 || k0 + g < ns) {
-#pragma unroll
-          for (int j = 0; j < VPT; ++j) {
-            if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
-            else Op::fast(acc[j], x[g][j]);
-          }
-        }
-      }
-    };
-    if constexpr (NS > 0) {
-#pragma unroll
-      for (int k0 = 0; k0 < NS; k0 += G) group(k0);
-    } else {
-      for (int k0 = 0; k0 < ns; k0 += G) group(k0);
-    }
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) bad |= Op::has_nan(acc[j]);
-#pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      vec16 out = Op::finish(acc[j]);
-      if (__builtin_expect(bad, 0)) {
-        if (Op::has_nan(acc[j])) out = fold_vector_exact<Op, NT>(srcs, ns, off0 + j * kStep);
-      }
-      st16<NT>(dst + off0 + j * kStep, out);
-    }
-  } else {
-    // Partial (last) tile: exact fold per vector.
-    for (uint64_t v = v0 + lane; v < nvec; v += kBlock) {
-      const uint64_t off = vec_off + v * 16;
-      typename Op::Acc acc = Op::init(ld16<NT>(srcs[0] + off));
-      for (int k = 1; k < ns; ++k) Op::accum(acc, ld16<NT>(srcs[k] + off));
-      st16<NT>(dst + off, Op::finish(acc));
-    }
-  }
+  if (v0 + (uint64_t)kBlock * VPT <= nvec)
+    fold_tile_body<Op, VPT, NT, NS, false>(srcs, n, dst, vec_off, v0, nvec, lane);
+  else
+    fold_tile_body<Op, VPT, NT, NS, true>(srcs, n, dst, vec_off, v0, nvec, lane);
 }
 
 // Element part: elements [0, head) and [tail_begin, n_elems) plus trailing
 // bytes; elements >= tail_sem_from get the F16C-tail NaN rule (fp16 only).
+// Each element's N loads are issued together (groups of 8) before the fold.
 template <class Op>
 __device__ __forceinline__ void fold_elements(const unsigned char* const* srcs, int n,
                                               unsigned char* dst, const FoldGeom& g,
@@ -165,8 +171,20 @@ __device__ __forceinline__ void fold_elements(const unsigned char* const* srcs, 
     const uint64_t e = s < n_head ? s : g.tail_begin + (s - n_head);
     const bool tail = e >= g.tail_sem_from;
     const uint64_t off = e * sizeof(E);
-    typename Op::EAcc acc = Op::init_e(ld_e<E>(srcs[0] + off, aligned), tail);
-    for (int k = 1; k < n; ++k) Op::accum_e(acc, ld_e<E>(srcs[k] + off, aligned), tail);
+    typename Op::EAcc acc{};
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      E x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (k0 + q < n) x[q] = ld_e<E>(srcs[k0 + q] + off, aligned);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (k0 + q < n) {
+          if (k0 + q == 0) acc = Op::init_e(x[q], tail);
+          else Op::accum_e(acc, x[q], tail);
+        }
+      }
+    }
     st_e<E>(dst + off, Op::finish_e(acc, tail), aligned);
   }
   // Trailing len % sizeof(T) bytes of a fold into a separate dst: the fold's
@@ -189,21 +207,19 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
                     (uint64_t)blockIdx.x * kBlock + threadIdx.x, (uint64_t)gridDim.x * kBlock);
 }
 
-// Batched: block b works on tile b of the concatenated tile space; a bucket's
-// tiles are [tile_start[i], tile_start[i+1]).  The element work of a bucket is
-// done by its first tile.
+// Batched: block b works on tile b of the concatenated tile space;
+// tile_bucket[tile] names the bucket (one load instead of a binary search:
+// the dependent-load chain is what a small block's launch waits on), and
+// tile - first_tile is the tile's index inside it.  The element work of a
+// bucket is done by its first tile.
 template <class Op, int VPT, bool NT>
 __global__ __launch_bounds__(kBlock) void batched_kernel(const BatchEntry* __restrict__ tab,
-                                                         const uint32_t* __restrict__ tile_start,
+                                                         const uint32_t* __restrict__ tile_bucket,
                                                          int nbuckets, uint32_t ntiles) {
+  (void)nbuckets;
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    int lo = 0, hi = nbuckets - 1;  // last i with tile_start[i] <= tile
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tile_start[mid] <= tile) lo = mid; else hi = mid - 1;
-    }
-    const BatchEntry& e = tab[lo];
-    const uint32_t local = tile - tile_start[lo];
+    const BatchEntry& e = tab[tile_bucket[tile]];
+    const uint32_t local = tile - e.first_tile;
     fold_tile<Op, VPT, NT, 0>(e.srcs, e.n, e.dst, e.g.vec_off,
                               (uint64_t)local * kBlock * VPT, e.g.nvec, threadIdx.x);
     if (local == 0)
@@ -232,32 +248,43 @@ static hipError_t launch_fold_vpt(const FoldArgs& a, const Tuning& tu, hipStream
 
 template <class Op>
 static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
+  const int vpt = fold_vpt(a.g.nvec, tu.vpt);
   if (tu.nt) {
-    switch (tu.vpt) {
+    switch (vpt) {
+      case 1: return launch_fold_vpt<Op, 1, true>(a, tu, s);
       case 2: return launch_fold_vpt<Op, 2, true>(a, tu, s);
       case 8: return launch_fold_vpt<Op, 8, true>(a, tu, s);
       default: return launch_fold_vpt<Op, 4, true>(a, tu, s);
     }
   }
-  switch (tu.vpt) {
+  switch (vpt) {
+    case 1: return launch_fold_vpt<Op, 1, false>(a, tu, s);
     case 2: return launch_fold_vpt<Op, 2, false>(a, tu, s);
     case 8: return launch_fold_vpt<Op, 8, false>(a, tu, s);
     default: return launch_fold_vpt<Op, 4, false>(a, tu, s);
   }
 }
 
-template <class Op>
-static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_start,
-                                    int nbuckets, uint32_t ntiles, const Tuning& tu,
-                                    hipStream_t s) {
+template <class Op, int VPT>
+static hipError_t launch_batched_vpt(const BatchEntry* tab, const uint32_t* tile_bucket,
+                                     int nbuckets, uint32_t ntiles, const Tuning& tu,
+                                     hipStream_t s) {
   const uint32_t grid = ntiles < (uint32_t)tu.max_grid ? ntiles : (uint32_t)tu.max_grid;
   if (tu.nt)
-    hipLaunchKernelGGL((batched_kernel<Op, kBatchVPT, true>), dim3(grid), dim3(kBlock), 0, s,
-                       tab, tile_start, nbuckets, ntiles);
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(grid), dim3(kBlock), 0, s, tab,
+                       tile_bucket, nbuckets, ntiles);
   else
-    hipLaunchKernelGGL((batched_kernel<Op, kBatchVPT, false>), dim3(grid), dim3(kBlock), 0, s,
-                       tab, tile_start, nbuckets, ntiles);
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(grid), dim3(kBlock), 0, s, tab,
+                       tile_bucket, nbuckets, ntiles);
   return hipGetLastError();
+}
+
+template <class Op>
+static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_bucket,
+                                    int nbuckets, uint32_t ntiles, int vpt, const Tuning& tu,
+                                    hipStream_t s) {
+  return vpt == 1 ? launch_batched_vpt<Op, 1>(tab, tile_bucket, nbuckets, ntiles, tu, s)
+                  : launch_batched_vpt<Op, kBatchVPT>(tab, tile_bucket, nbuckets, ntiles, tu, s);
 }
 
 }  // namespace bpsr
@@ -269,7 +296,7 @@ static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_
     return launch_fold_op<OP>(a, tu, s);                                                  \
   }                                                                                       \
   hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
-                                   uint32_t nt, const Tuning& tu, hipStream_t s) {        \
-    return launch_batched_op<OP>(tab, ts, nb, nt, tu, s);                                 \
+                                   uint32_t nt, int vpt, const Tuning& tu, hipStream_t s) { \
+    return launch_batched_op<OP>(tab, ts, nb, nt, vpt, tu, s);                            \
   }                                                                                       \
   }

@@ -47,6 +47,7 @@ EXPORTS = (
     "byteps_reduce_sum_batched", "byteps_reduce_copy", "byteps_reduce_sync",
     "byteps_reduce_dtype_size", "byteps_reduce_last_error",
     "byteps_reduce_set_tuning", "byteps_reduce_get_tuning",
+    "byteps_reduce_plan_create", "byteps_reduce_plan_launch", "byteps_reduce_plan_destroy",
 )
 
 
@@ -87,6 +88,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_last_error.restype = ctypes.c_char_p
     L.byteps_reduce_set_tuning.argtypes = [_int, _int, _int]
     L.byteps_reduce_get_tuning.argtypes = [ctypes.POINTER(_int)] * 3
+    L.byteps_reduce_plan_create.argtypes = [ctypes.POINTER(BucketDesc), _int, _int, _int,
+                                            ctypes.POINTER(_vp)]
+    L.byteps_reduce_plan_launch.argtypes = [_vp, _vp]
+    L.byteps_reduce_plan_destroy.argtypes = [_vp]
     _LIB = L
     return L
 
@@ -158,19 +163,18 @@ class GpuReducer:
     def sum_batched(self, buckets: Sequence[tuple], dtype: int, mode: int = MODE_REFERENCE,
                     stream=None) -> int:
         """One launch for a block of buckets; each item is ``(dst, srcs, length)``."""
-        descs = (BucketDesc * max(1, len(buckets)))()
-        for i, (dst, srcs, length) in enumerate(buckets):
-            if len(srcs) > MAX_SRCS:
-                raise ReduceError(EARGS, f"bucket {i}: more than {MAX_SRCS} sources")
-            descs[i].dst = _ptr(dst)
-            for k, s in enumerate(srcs):
-                descs[i].srcs[k] = _ptr(s)
-            descs[i].len = int(length)
-            descs[i].n = len(srcs)
+        descs = _descs(buckets)
         first = buckets[0][0] if buckets else None
         _check(self.lib.byteps_reduce_sum_batched(descs, len(buckets), int(dtype), int(mode),
                                                   _stream_of(first, stream)))
         return 0
+
+    def make_plan(self, buckets: Sequence[tuple], dtype: int,
+                  mode: int = MODE_REFERENCE) -> "Plan":
+        """Upload a block's bucket table once; ``Plan.launch`` is then one
+        kernel launch (graph-capturable).  Tensors in ``buckets`` must stay
+        alive (and at the same addresses) for the plan's lifetime."""
+        return Plan(self.lib, buckets, dtype, mode)
 
     def sync(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_sync(_stream_of(None, stream)))
@@ -187,6 +191,45 @@ class GpuReducer:
     @staticmethod
     def dtype_size(dtype: int) -> int:
         return elem_size(dtype)
+
+
+def _descs(buckets):
+    descs = (BucketDesc * max(1, len(buckets)))()
+    for i, (dst, srcs, length) in enumerate(buckets):
+        if len(srcs) > MAX_SRCS:
+            raise ReduceError(EARGS, f"bucket {i}: more than {MAX_SRCS} sources")
+        descs[i].dst = _ptr(dst)
+        for k, s in enumerate(srcs):
+            descs[i].srcs[k] = _ptr(s)
+        descs[i].len = int(length)
+        descs[i].n = len(srcs)
+    return descs
+
+
+class Plan:
+    """``byteps_reduce_plan``: a Prophet block's bucket table resident on the device."""
+
+    def __init__(self, lib, buckets, dtype, mode):
+        self.lib = lib
+        self.handle = _vp()
+        self._keep = buckets          # keep the tensors alive
+        self.first = buckets[0][0] if buckets else None
+        _check(lib.byteps_reduce_plan_create(_descs(buckets), len(buckets), int(dtype),
+                                             int(mode), ctypes.byref(self.handle)))
+
+    def launch(self, stream=None) -> None:
+        _check(self.lib.byteps_reduce_plan_launch(self.handle, _stream_of(self.first, stream)))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.byteps_reduce_plan_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # torch-tensor convenience: whole-tensor ops with dtype taken from the tensor

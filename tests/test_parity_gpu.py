@@ -263,3 +263,47 @@ def test_bad_dtype_raises(red, dev):
     with pytest.raises(ReduceError) as e:
         red.sum(a, a.clone(), 64, 10)
     assert e.value.code == EDTYPE
+
+
+def test_plan_launch_and_graph_replay(red, dev, port):
+    """A block plan (table uploaded once) equals the oracle, also when its
+    launch is captured into a hipGraph and replayed with new data in place."""
+    from prophet_amd.buckets import resnet50_param_sizes
+    dt = DType.FLOAT16
+    sizes = resnet50_param_sizes()[100:130]
+    N = 8
+    bufs, buckets = [], []
+    for i, ne in enumerate(sizes):
+        srcs = [torch.empty(ne * 2, dtype=torch.uint8, device=dev) for _ in range(N)]
+        dst = torch.empty_like(srcs[0])
+        bufs.append((dst, srcs))
+        buckets.append((dst, srcs, ne * 2))
+    plan = red.make_plan(buckets, dt)
+
+    def fill(seed):
+        wants = []
+        for i, ((dst, srcs), ne) in enumerate(zip(bufs, sizes)):
+            ins = [np.ascontiguousarray(synth.bucket(dt, ne, k, "normal", seed + i)).view(np.uint8)
+                   for k in range(N)]
+            for s, x in zip(srcs, ins):
+                s.copy_(torch.from_numpy(x))
+            w = np.zeros(ne * 2, np.uint8)
+            port.sum_n(w, ins, ne * 2, dt)
+            wants.append(w)
+        return wants
+
+    wants = fill(10)
+    plan.launch()
+    torch.cuda.synchronize()
+    for (dst, _), w in zip(bufs, wants):
+        assert np.array_equal(dst.cpu().numpy(), w)
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        plan.launch(side)
+    wants = fill(20)
+    g.replay()
+    torch.cuda.synchronize()
+    for (dst, _), w in zip(bufs, wants):
+        assert np.array_equal(dst.cpu().numpy(), w)
+    plan.close()

@@ -1,0 +1,73 @@
+"""GPU tests of the paths around the kernel: host-streamed reduction (cfg5
+shape, small), the sharded reducer on one rank, the HBM slot arena."""
+import numpy as np
+import pytest
+
+from golden_util import assert_bytes_match
+from oracle.oracle import PortReducer
+from prophet_amd import synth
+from prophet_amd.dtypes import DType, elem_size
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def red():
+    assert torch.cuda.is_available()
+    from prophet_amd.reducer import GpuReducer
+    return GpuReducer(device=0)
+
+
+@pytest.mark.parametrize("dt", [DType.BFLOAT16, DType.FLOAT16, DType.FLOAT32, DType.INT8],
+                         ids=lambda d: DType(d).name)
+@pytest.mark.parametrize("extra", [0, 1, 7])
+def test_streaming_reducer_bit_exact(red, dt, extra):
+    from prophet_amd.stream import StreamingReducer
+    es = elem_size(dt)
+    n = 300_007
+    L = n * es + (extra % es if es > 1 else 0)
+    N = 5
+    ins = [np.ascontiguousarray(synth.bucket(dt, n + 1, k, "special" if dt in (DType.FLOAT16, DType.BFLOAT16, DType.FLOAT32) else "normal", 31))
+           .view(np.uint8)[:L].copy() for k in range(N)]
+    host = [torch.from_numpy(x).pin_memory() for x in ins]
+    out = torch.zeros(L, dtype=torch.uint8).pin_memory()
+    sr = StreamingReducer(N, chunk_bytes=64 * 1024 + 48, depth=3, reducer=red)
+    sr.reduce(host, out, L, dt)
+    want = np.zeros(L, np.uint8)
+    PortReducer(nthreads=4).sum_n(want, ins, L, dt)
+    assert_bytes_match(dt, out.numpy(), want, nan_class_f32_f64=False)
+
+
+def test_sharded_reducer_single_rank(red):
+    import torch.distributed as dist
+    from prophet_amd.shard import ShardedReducer
+    if not dist.is_initialized():
+        import os
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    n = 100_003
+    sr = ShardedReducer(n)            # default fold = HIP via the C ABI
+    dev = torch.device("cuda:0")
+    pushes = [torch.randn(n, device=dev) for _ in range(4)]
+    slots = [torch.empty(n, device=dev) for _ in range(4)]
+    owned = torch.empty(n, device=dev)
+    sr.scatter_reduce(0, pushes, slots, owned)
+    ref = pushes[0].clone()
+    for p in pushes[1:]:
+        ref.add_(p)
+    torch.cuda.synchronize()
+    assert torch.equal(owned, ref)
+    full = torch.empty(n, device=dev)
+    sr.allgather(owned, full)
+    assert torch.equal(full, ref)
+
+
+def test_arena_slots_are_skewed_and_disjoint():
+    from prophet_amd.arena import BucketArena
+    a = BucketArena(9, 1 << 20, torch.device("cuda:0"))
+    ptrs = [s.data_ptr() for s in a.slots()]
+    assert all(b - a_ == a.stride for a_, b in zip(ptrs, ptrs[1:]))
+    assert a.stride % (1 << 20) != 0
+    assert all(s.numel() == 1 << 20 for s in a.slots())

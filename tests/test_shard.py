@@ -1,0 +1,114 @@
+"""Key-space sharding: ownership math (core_loops.cc:208-247) and the
+multi-process data path over gloo (world_size 2 and 3, CPU).
+
+The local fold in these CPU tests is the oracle (test infrastructure), injected
+into ShardedReducer; the product default is the HIP fold (tests/test_parity_gpu.py
+covers it on the GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from prophet_amd.buckets import partition_all, vgg16_param_sizes
+from prophet_amd.shard import owner_of, owner_ranges, split_buckets
+
+
+def test_owner_ranges_match_reference_split():
+    # core_loops.cc:210-211: per = len/nccl_size/unit; tail to the root (last)
+    assert owner_ranges(10, 4) == [(0, 2), (2, 4), (4, 6), (6, 10)]
+    assert owner_ranges(8, 8) == [(i, i + 1) for i in range(8)]
+    assert owner_ranges(3, 4) == [(0, 0), (0, 0), (0, 0), (0, 3)]
+    vgg = sum(vgg16_param_sizes())
+    r = owner_ranges(vgg, 8)
+    assert all(hi - lo == 17_294_693 for lo, hi in r)
+    for e in (0, 1, 17_294_692, 17_294_693, vgg - 1):
+        g = owner_of(e, vgg, 8)
+        assert r[g][0] <= e < r[g][1]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_split_buckets_covers_exactly(world):
+    sizes = [p.len // 4 for p in partition_all([n * 4 for n in vgg16_param_sizes()])]
+    pieces = split_buckets(sizes, world)
+    total = sum(sizes)
+    cover = np.zeros(total, dtype=np.int8)
+    ranges = owner_ranges(total, world)
+    starts = np.cumsum([0] + sizes)
+    for p in pieces:
+        assert ranges[p.owner][0] <= p.start and p.start + p.length <= ranges[p.owner][1]
+        assert starts[p.bucket] + p.bucket_offset == p.start
+        cover[p.start: p.start + p.length] += 1
+    assert (cover == 1).all()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_fold():
+    from oracle.oracle import PortReducer
+    from prophet_amd.dtypes import from_torch
+    port = PortReducer(nthreads=1)
+
+    def fold(dst, srcs):
+        a = dst.numpy().view(np.uint8)
+        ins = [s.contiguous().numpy().view(np.uint8) for s in srcs]
+        assert port.sum_n(a, ins, a.nbytes, from_torch(dst.dtype)) == 0
+    return fold
+
+
+def _worker(rank, world, port, n_elems, n_workers, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from prophet_amd import synth
+        from prophet_amd.dtypes import DType
+        from prophet_amd.shard import ShardedReducer
+        sr = ShardedReducer(n_elems, fold=_oracle_fold())
+        root = 0
+        pushes = None
+        if rank == root:
+            pushes = [torch.from_numpy(synth.bucket(DType.FLOAT32, n_elems, k, "normal", 77))
+                      for k in range(n_workers)]
+        slots = [torch.empty(sr.owned, dtype=torch.float32) for _ in range(n_workers)]
+        owned = torch.empty(sr.owned, dtype=torch.float32)
+        sr.scatter_reduce(root, pushes, slots, owned)
+        full = torch.empty(n_elems, dtype=torch.float32)
+        sr.allgather(owned, full)
+        q.put((rank, full.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_reduce_allgather_gloo(world):
+    n_elems, n_workers = 10_007, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_elems, n_workers, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # unsharded left fold by the oracle
+    from oracle.oracle import PortReducer
+    from prophet_amd import synth
+    from prophet_amd.dtypes import DType
+    ins = [np.ascontiguousarray(synth.bucket(DType.FLOAT32, n_elems, k, "normal", 77)).view(np.uint8)
+           for k in range(n_workers)]
+    want = np.zeros(n_elems * 4, np.uint8)
+    PortReducer().sum_n(want, ins, want.nbytes, DType.FLOAT32)
+    for r in range(world):
+        assert results[r] == want.tobytes(), f"rank {r}"

@@ -1,0 +1,291 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE.json configs on one MI355X (bench.py measures config 2).
+
+  cfg3   8-way fp16 over ResNet-50's 161 gradient tensors (165 BytePS partitions
+         of <= 4,096,000 B), Prophet block grouping: one batched launch per
+         block (12 blocks) vs one launch per partition vs one launch for all.
+  sweep  8-way fp16 single-bucket sum, bucket 1 KiB .. 64 MiB and 97.49 MiB.
+  cfg4   8-way fp32 over VGG-16 (553,430,176 B): whole set on one GPU, and the
+         per-GPU shard of a G-way key-space split (G = 2, 4, 8) timed alone —
+         the device-resident sum-only scaling of SURVEY.md §8d cfg4.
+  cfg5   16-way bf16, 4 GiB of pinned host gradients, streamed H2D -> fold ->
+         D2H on side streams (prophet_amd.stream.StreamingReducer), plus the
+         bare H2D rate of the same bytes for reference.
+
+Every result is checked against torch's own left fold (bit-exact) before it is
+reported.  Prints one JSON line per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GIB = float(1 << 30)
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def timed(fn, reps, stream):
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(0)
+    torch.cuda.synchronize()
+    ts = []
+    for r in range(3):
+        e0.record(stream)
+        for i in range(reps):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / reps)
+    return statistics.median(ts), min(ts)
+
+
+def torch_fold(srcs, tdt):
+    acc = srcs[0].view(tdt).clone()
+    for s in srcs[1:]:
+        acc.add_(s.view(tdt))
+    return acc.view(__import__("torch").uint8)
+
+
+def cfg3(red, dev, N=8, sets=3):
+    import torch
+    from prophet_amd.buckets import partition_all, prophet_blocks, resnet50_param_sizes
+    from prophet_amd.dtypes import DType
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    parts = partition_all(sizes)
+    blocks = prophet_blocks(len(sizes))
+    total = sum(sizes)
+    s = torch.cuda.current_stream()
+    # per set: each worker's whole gradient vector in one buffer (partitions are views)
+    data = []
+    for _ in range(sets):
+        w = [torch.randn(total // 2, device=dev).half().view(torch.uint8) for _ in range(N)]
+        out = torch.empty(total, dtype=torch.uint8, device=dev)
+        toff = [0]
+        for n in sizes:
+            toff.append(toff[-1] + n)
+        data.append((w, out, toff))
+
+    def views(i, p):
+        w, out, toff = data[i % sets]
+        o = toff[p.tensor] + p.offset
+        return out[o:o + p.len], [x[o:o + p.len] for x in w]
+
+    by_block = []
+    for blk in blocks:
+        tset = set(blk)
+        by_block.append([p for p in parts if p.tensor in tset])
+
+    def per_partition(i):
+        for p in parts:
+            d, ss = views(i, p)
+            red.sum_n(d, ss, p.len, DType.FLOAT16, stream=s)
+
+    def per_block(i):
+        for bp in by_block:
+            red.sum_batched([(*views(i, p), p.len) for p in bp], DType.FLOAT16, stream=s)
+
+    def all_in_one(i):
+        red.sum_batched([(*views(i, p), p.len) for p in parts], DType.FLOAT16, stream=s)
+
+    plans = [[red.make_plan([(*views(i, p), p.len) for p in bp], DType.FLOAT16)
+              for bp in by_block] for i in range(sets)]
+
+    def per_block_plan(i):
+        for pl in plans[i % sets]:
+            pl.launch(s)
+
+    graphs = []
+    for i in range(sets):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(s)
+        with torch.cuda.stream(side):
+            per_block_plan(i)          # warm the capture stream
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            for pl in plans[i]:
+                pl.launch(side)
+        graphs.append(g)
+
+    def per_block_graph(i):
+        graphs[i % sets].replay()
+
+    # Engine streams: independent keys/blocks run concurrently, like the
+    # reference's BYTEPS_SERVER_ENGINE_THREAD engine threads (server.cc:363-370).
+    eng = [torch.cuda.Stream() for _ in range(4)]
+
+    def per_block_plans_4streams(i, cur=None):
+        cur = cur or torch.cuda.current_stream()
+        for e in eng:
+            e.wait_stream(cur)
+        for b, pl in enumerate(plans[i % sets]):
+            pl.launch(eng[b % len(eng)])
+        for e in eng:
+            cur.wait_stream(e)
+
+    graphs4 = []
+    for i in range(sets):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(s)
+        with torch.cuda.stream(side):
+            per_block_plans_4streams(i, side)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            per_block_plans_4streams(i, side)
+        graphs4.append(g)
+
+    def per_block_graph4(i):
+        graphs4[i % sets].replay()
+
+    for name, fn in (("per_partition_launch", per_partition), ("prophet_block_batched", per_block),
+                     ("single_batched_launch", all_in_one),
+                     ("prophet_block_plans", per_block_plan),
+                     ("prophet_block_plans_hipgraph", per_block_graph),
+                     ("prophet_block_plans_4streams", per_block_plans_4streams),
+                     ("prophet_block_plans_4streams_hipgraph", per_block_graph4)):
+        med, mn = timed(fn, 10, s)
+        w, out, _ = data[0]
+        fn(0)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(out, torch_fold(w, torch.float16)))
+        emit(config="cfg3", variant=name, n_workers=N, tensors=len(sizes), partitions=len(parts),
+             blocks=len(blocks), bytes_per_worker=total, ms=round(med, 4), min_ms=round(mn, 4),
+             gibps=round(N * total / (med * 1e-3) / GIB, 1),
+             hbm_frac=round((N + 1) * total / (med * 1e-3) / 8e12, 4), exact=ok)
+
+
+def size_sweep(red, dev, N=8):
+    import torch
+    from prophet_amd.dtypes import DType
+    s = torch.cuda.current_stream()
+    sizes = [1 << k for k in range(10, 27)] + [102_228_128]
+    for B in sizes:
+        n = B // 2
+        sets = 3 if B >= (8 << 20) else 1
+        data = [([torch.randn(n, device=dev).half().view(torch.uint8) for _ in range(N)],
+                 torch.empty(B, dtype=torch.uint8, device=dev)) for _ in range(sets)]
+
+        def fn(i):
+            w, o = data[i % sets]
+            red.sum_n(o, w, B, DType.FLOAT16, stream=s)
+        med, mn = timed(fn, 50 if B < (16 << 20) else 10, s)
+        w, o = data[0]
+        fn(0)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(o, torch_fold(w, torch.float16)))
+        emit(config="sweep_fp16", bucket_bytes=B, n_workers=N, us=round(med * 1e3, 2),
+             gibps=round(N * B / (med * 1e-3) / GIB, 1),
+             hbm_frac=round((N + 1) * B / (med * 1e-3) / 8e12, 4), exact=ok)
+
+
+def cfg4(red, dev, N=8):
+    import torch
+    from prophet_amd.arena import BucketArena
+    from prophet_amd.buckets import vgg16_param_sizes
+    from prophet_amd.dtypes import DType
+    from prophet_amd.shard import owner_ranges
+    s = torch.cuda.current_stream()
+    E = sum(vgg16_param_sizes())
+    for G in (1, 2, 4, 8):
+        lo, hi = owner_ranges(E, G)[G - 1]
+        n = hi - lo
+        B = n * 4
+        sets = 3 if (N + 1) * B * 3 < (40 << 30) else 2
+        data = []
+        for _ in range(sets):
+            slots = BucketArena(N + 1, B, dev).slots()
+            for t in slots[:N]:
+                t.view(torch.float32).copy_(torch.randn(n, device=dev))
+            data.append((slots[N], slots[:N]))
+
+        def fn(i):
+            o, w = data[i % sets]
+            red.sum_n(o, w, B, DType.FLOAT32, stream=s)
+        med, mn = timed(fn, 10, s)
+        o, w = data[0]
+        fn(0)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(o, torch_fold(w, torch.float32)))
+        emit(config="cfg4", gpus_in_split=G, shard_elems=n, ms=round(med, 4),
+             per_gpu_gibps=round(N * B / (med * 1e-3) / GIB, 1),
+             node_gibps_if_parallel=round(G * N * B / (med * 1e-3) / GIB, 1),
+             whole_set_time_ms_if_parallel=round(med, 4),
+             hbm_frac=round((N + 1) * B / (med * 1e-3) / 8e12, 4), exact=ok)
+        del data
+        torch.cuda.empty_cache()
+
+
+def cfg5(red, dev, N=16, B=256 << 20, chunk=32 << 20):
+    import torch
+    from prophet_amd.dtypes import DType
+    from prophet_amd.stream import StreamingReducer
+    n = B // 2
+    t0 = time.perf_counter()
+    host = [torch.empty(B, dtype=torch.uint8, pin_memory=True) for _ in range(N)]
+    g = torch.Generator()
+    for k, h in enumerate(host):
+        g.manual_seed(1000 + k)
+        h.view(torch.bfloat16).copy_(torch.randn(n, generator=g))
+    out = torch.empty(B, dtype=torch.uint8, pin_memory=True)
+    setup_s = time.perf_counter() - t0
+    sr = StreamingReducer(N, chunk_bytes=chunk, depth=3, device=dev, reducer=red)
+    sr.reduce(host, out, B, DType.BFLOAT16)          # warm-up
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        sr.reduce(host, out, B, DType.BFLOAT16)
+        ts.append(time.perf_counter() - t)
+    med = statistics.median(ts)
+    # check a 16 MiB window against torch's bf16 left fold on the device
+    w = 8 << 20
+    acc = host[0][:w].to(dev).view(torch.bfloat16).clone()
+    for h in host[1:]:
+        acc.add_(h[:w].to(dev).view(torch.bfloat16))
+    ok = bool(torch.equal(acc.view(torch.uint8).cpu(), out[:w]))
+    # bare H2D of the same N*B bytes into one device buffer (reference rate)
+    dbuf = torch.empty(chunk, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for h in host:
+        for o in range(0, B, chunk):
+            dbuf.copy_(h[o:o + chunk], non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = time.perf_counter() - t
+    emit(config="cfg5", n_workers=N, bucket_bytes=B, total_bytes=N * B, chunk_bytes=chunk,
+         e2e_s=round(med, 4), e2e_gibps=round(N * B / med / GIB, 2),
+         h2d_only_gibps=round(N * B / h2d / GIB, 2), e2e_over_h2d=round(h2d / med, 3),
+         host_setup_s=round(setup_s, 1), exact_window=ok)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--only", default="cfg3,sweep,cfg4,cfg5")
+    a = p.parse_args()
+    import torch
+    from prophet_amd.reducer import GpuReducer
+    dev = torch.device("cuda:0")
+    red = GpuReducer(device=0)
+    todo = a.only.split(",")
+    if "cfg3" in todo:
+        cfg3(red, dev)
+    if "sweep" in todo:
+        size_sweep(red, dev)
+    if "cfg4" in todo:
+        cfg4(red, dev)
+    if "cfg5" in todo:
+        cfg5(red, dev)
+
+
+if __name__ == "__main__":
+    main()
