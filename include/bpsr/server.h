@@ -1,0 +1,91 @@
+/*
+ * bpsr/server.h — GPU-resident parameter-server aggregation (C ABI of
+ * libbpsr.so), the device counterpart of byteps/server/server.cc.
+ *
+ * Reference behaviour reproduced (server.cc:147-308, 70-145; server.h:138-162):
+ *   - round 0 (store not initialised): collect one init push per worker; the
+ *     store is initialised by a copy of the LAST arriving init push
+ *     (server.cc:175-199);
+ *   - every later round, sync mode: the first arrival is the accumulator, the
+ *     others are summed into it in ARRIVAL order, and when all NumWorkers pushes
+ *     have arrived the merged result becomes the store (server.cc:200-273); a
+ *     pull is answered once the round's push is finished and after NumWorkers
+ *     pulls the key re-arms (server.cc:280-306, 100-114);
+ *   - async mode: every push is summed straight into the store
+ *     (server.cc:220-230) and pulls are answered immediately;
+ *   - keys are pinned to engine lanes by least accumulated bytes, sticky per key
+ *     (GetThreadID, server.h:138-162) — a lane here is a pair of HIP streams,
+ *     not a CPU thread.
+ *
+ * Device-native differences:
+ *   - receive slots, the store and (incremental policy) the accumulator live in
+ *     HBM, one skewed arena per key; data reaches a slot by H2D/D2D copy
+ *     (byteps_server_push) or is written there directly by a transport
+ *     (byteps_server_recv_slot + byteps_server_push_ready, the analogue of
+ *     ps-lite's zero-copy SArray);
+ *   - policy FUSED folds all N slots into the store with ONE kernel at the last
+ *     arrival ((N+1)*B HBM bytes); policy INCREMENTAL mirrors SUM_RECV /
+ *     COPY_MERGED (an in-place add per arrival, then a copy).  Both give the
+ *     same bits: a strict left fold in arrival order.
+ */
+#ifndef BPSR_SERVER_H
+#define BPSR_SERVER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "bpsr/reduce.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum byteps_server_policy { BYTEPS_SERVER_FUSED = 0, BYTEPS_SERVER_INCREMENTAL = 1 };
+enum byteps_server_location { BYTEPS_SERVER_HOST = 0, BYTEPS_SERVER_DEVICE = 1 };
+
+typedef struct byteps_server_config {
+  int num_workers;     /* ps::NumWorkers() / DMLC_NUM_WORKER                 */
+  int engine_lanes;    /* BYTEPS_SERVER_ENGINE_THREAD (default 4)            */
+  int policy;          /* byteps_server_policy                               */
+  int async_mode;      /* 1 = asynchronous training (sum into the store)     */
+  int device;          /* HIP device ordinal                                 */
+} byteps_server_config;
+
+typedef struct byteps_server byteps_server;
+
+/* Defaults from the environment, as init_global_env (server.cc:310-337) reads
+ * them: DMLC_NUM_WORKER, BYTEPS_SERVER_ENGINE_THREAD, BYTEPS_ENABLE_ASYNC
+ * (here "1" means asynchronous; the reference reads the flag inverted,
+ * server.cc:315), BPSR_SERVER_POLICY (fused|incremental), device 0. */
+int byteps_server_config_from_env(byteps_server_config* cfg);
+
+int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
+int byteps_server_destroy(byteps_server* s);
+
+/* Optional: allocate a key's slots and store before its first push. */
+int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype);
+
+/* A worker's push of `len` bytes for `key` (round 0 = init push).  The data is
+ * copied into the worker's receive slot before the call returns (the caller may
+ * reuse `data`); the fold is queued on the key's engine lane. */
+int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data,
+                       size_t len, int dtype, int location);
+
+/* Zero-copy transport path: where worker `worker`'s push for `key` must land,
+ * then the arrival notice once the bytes are there (visible to the device). */
+int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot);
+int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
+
+/* A worker's pull: blocks until the key's current round is finished (sync mode),
+ * then copies the store (len bytes) to `out`. */
+int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
+
+/* Introspection for tests/debug (BYTEPS_SERVER_DEBUG analogue): completed
+ * rounds, engine lane, and the arrival order of the last completed round. */
+int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
+                           int* last_order, int max_order);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPSR_SERVER_H */

@@ -21,8 +21,7 @@ namespace bpsr {
 
 static thread_local std::string g_last_error;
 
-static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static int fail(int code, const char* fmt, ...) {
+int fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -32,7 +31,7 @@ static int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-static int hip_fail(hipError_t e, const char* what) {
+int hip_fail(hipError_t e, const char* what) {
   return fail(BYTEPS_REDUCE_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 

@@ -61,6 +61,11 @@ struct Tuning {
 
 int elem_size(int dtype);  // 0 if unsupported
 
+// Thread-local error reporting shared by every C-ABI entry point
+// (byteps_reduce_last_error): returns `code`.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_fail(hipError_t e, const char* what);
+
 // Host-side geometry: vector range, head/tail split (fp16 body/tail rule of
 // cpu_reducer.cc:103,118), co-alignment test.
 void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, int n,

@@ -1,0 +1,421 @@
+// GPU-resident parameter-server aggregation (include/bpsr/server.h): the
+// per-key state machine of byteps/server/server.cc:147-308 with the engine
+// threads (server.cc:70-145) replaced by HIP stream lanes and the CpuReducer
+// calls replaced by the gfx950 fold kernels.
+#include "bpsr/server.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "bpsr_internal.h"
+
+namespace bpsr {
+namespace {
+
+constexpr size_t kSlotAlign = 4096;
+constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots
+
+struct Lane {
+  hipStream_t fold = nullptr;  // folds, in round order per key
+  hipStream_t copy = nullptr;  // push/pull copies
+};
+
+struct KeyState {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool allocated = false;
+  bool inited = false;        // store initialised (round 0 done)
+  size_t len = 0;
+  int dtype = 0;
+  int lane = 0;
+  char* arena = nullptr;      // N receive slots + store
+  size_t stride = 0;
+  std::vector<char*> slot;
+  char* store = nullptr;
+  // current round
+  std::vector<char> got;      // worker pushed this round
+  std::vector<int> order;     // arrival order this round
+  int arrived = 0;
+  int init_count = 0;
+  // completion / pull gating (server.cc:100-114, 280-306)
+  uint64_t rounds = 0;
+  bool push_finished = false;
+  int pull_cnt = 0;
+  std::vector<int> last_order;
+  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the round
+  hipEvent_t copied = nullptr;
+  bool has_done = false;
+};
+
+}  // namespace
+}  // namespace bpsr
+
+struct byteps_server {
+  byteps_server_config cfg;
+  std::vector<bpsr::Lane> lanes;
+  std::mutex map_mu;
+  std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
+  std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
+};
+
+namespace bpsr {
+namespace {
+
+int set_device(const byteps_server* s) {
+  hipError_t e = hipSetDevice(s->cfg.device);
+  return e == hipSuccess ? 0 : hip_fail(e, "hipSetDevice");
+}
+
+// server.h:138-162 GetThreadID: least accumulated bytes, sticky per key.
+int pick_lane(byteps_server* s, size_t len) {
+  int best = 0;
+  uint64_t best_load = std::numeric_limits<uint64_t>::max();
+  for (int i = 0; i < (int)s->acc_load.size(); ++i) {
+    if (s->acc_load[i] < best_load) {
+      best_load = s->acc_load[i];
+      best = i;
+    }
+  }
+  s->acc_load[best] += len;
+  return best;
+}
+
+KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
+  std::lock_guard<std::mutex> g(s->map_mu);
+  auto it = s->keys.find(key);
+  if (it != s->keys.end()) return it->second.get();
+  if (!create) return nullptr;
+  auto ks = std::make_unique<KeyState>();
+  KeyState* p = ks.get();
+  s->keys.emplace(key, std::move(ks));
+  return p;
+}
+
+// Allocate slots + store for a key (caller holds ks->mu).
+int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
+  if (ks->allocated) {
+    if (len != ks->len || dtype != ks->dtype)
+      return fail(BYTEPS_REDUCE_EARGS, "key re-declared with len %zu dtype %d (was %zu, %d)", len,
+                  dtype, ks->len, ks->dtype);
+    return 0;
+  }
+  if (elem_size(dtype) == 0) return fail(BYTEPS_REDUCE_EDTYPE, "Unsupported data type: %d", dtype);
+  if (len == 0) return fail(BYTEPS_REDUCE_EARGS, "init tensor size not larger than 0");
+  const int N = s->cfg.num_workers;
+  ks->stride = (len + kSlotAlign - 1) / kSlotAlign * kSlotAlign + kSlotSkew;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, ks->stride * (size_t)(N + 1));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(key arena)");
+  ks->arena = static_cast<char*>(p);
+  ks->slot.resize(N);
+  for (int k = 0; k < N; ++k) ks->slot[k] = ks->arena + ks->stride * k;
+  ks->store = ks->arena + ks->stride * N;
+  ks->got.assign(N, 0);
+  ks->order.clear();
+  if ((e = hipEventCreateWithFlags(&ks->done, hipEventDisableTiming)) != hipSuccess)
+    return hip_fail(e, "hipEventCreate");
+  if ((e = hipEventCreateWithFlags(&ks->copied, hipEventDisableTiming)) != hipSuccess)
+    return hip_fail(e, "hipEventCreate");
+  ks->len = len;
+  ks->dtype = dtype;
+  {
+    std::lock_guard<std::mutex> g(s->map_mu);
+    ks->lane = pick_lane(s, len);
+  }
+  ks->allocated = true;
+  return 0;
+}
+
+// Bring `len` bytes into worker `w`'s slot on the lane's copy stream, after
+// the previous round's fold has consumed the slot; wait for the copy.
+int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc) {
+  Lane& L = s->lanes[ks->lane];
+  hipError_t e = hipSuccess;
+  if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->done, 0);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ks->slot[w], data, len,
+                       loc == BYTEPS_SERVER_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                       L.copy);
+  if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
+  if (e == hipSuccess) e = hipEventSynchronize(ks->copied);
+  return e == hipSuccess ? 0 : hip_fail(e, "push copy");
+}
+
+// A push's bytes are in slot w: advance the state machine (caller holds ks->mu).
+int arrive(byteps_server* s, KeyState* ks, int w) {
+  const int N = s->cfg.num_workers;
+  Lane& L = s->lanes[ks->lane];
+  void* fold_stream = reinterpret_cast<void*>(L.fold);
+  int rc = 0;
+  if (!ks->inited) {
+    // Round 0: server.cc:175-199 — after all NumWorkers init pushes the store
+    // is initialised by copying the LAST arrived push.
+    if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d sent two init pushes", w);
+    ks->got[w] = 1;
+    if (++ks->init_count < N) return 0;
+    rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, fold_stream);
+    if (rc) return rc;
+    hipError_t e = hipEventRecord(ks->done, L.fold);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    ks->has_done = true;
+    ks->inited = true;
+    std::fill(ks->got.begin(), ks->got.end(), 0);
+    ks->cv.notify_all();
+    return 0;
+  }
+  if (s->cfg.async_mode) {
+    // server.cc:220-230: every push is summed straight into the store.
+    rc = byteps_reduce_sum(ks->store, ks->slot[w], ks->len, ks->dtype, fold_stream);
+    if (rc) return rc;
+    hipError_t e = hipEventRecord(ks->done, L.fold);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    ks->has_done = true;
+    ks->rounds++;
+    ks->cv.notify_all();
+    return 0;
+  }
+  if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d pushed twice in one round", w);
+  ks->got[w] = 1;
+  ks->order.push_back(w);
+  ks->arrived++;
+  if (s->cfg.policy == BYTEPS_SERVER_INCREMENTAL && ks->arrived > 1) {
+    // SUM_RECV (server.cc:117-139): merged (= first arrival's slot) += this push
+    rc = byteps_reduce_sum(ks->slot[ks->order[0]], ks->slot[w], ks->len, ks->dtype, fold_stream);
+    if (rc) return rc;
+  }
+  if (ks->arrived < N) return 0;
+  if (s->cfg.policy == BYTEPS_SERVER_INCREMENTAL) {
+    // COPY_MERGED (server.cc:82-115)
+    rc = byteps_reduce_copy(ks->store, ks->slot[ks->order[0]], ks->len, fold_stream);
+  } else {
+    // one fused left fold in arrival order straight into the store
+    std::vector<const void*> srcs(N);
+    for (int k = 0; k < N; ++k) srcs[k] = ks->slot[ks->order[k]];
+    rc = byteps_reduce_sum_n(ks->store, srcs.data(), N, ks->len, ks->dtype,
+                             BYTEPS_REDUCE_MODE_REFERENCE, fold_stream);
+  }
+  if (rc) return rc;
+  hipError_t e = hipEventRecord(ks->done, L.fold);
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  ks->has_done = true;
+  ks->last_order = ks->order;
+  ks->order.clear();
+  ks->arrived = 0;
+  std::fill(ks->got.begin(), ks->got.end(), 0);
+  ks->rounds++;
+  ks->push_finished = true;
+  ks->pull_cnt = 0;
+  ks->cv.notify_all();
+  return 0;
+}
+
+// Init pushes block until every worker's init push has arrived and the store
+// is initialised: the reference answers them only then (server.cc:184-198).
+int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock<std::mutex>& lk) {
+  const bool init_round = !ks->inited;
+  int rc = arrive(s, ks, w);
+  if (rc || !init_round) return rc;
+  ks->cv.wait(lk, [&] { return ks->inited; });
+  return 0;
+}
+
+// Per-thread stream for pull copies (a pull blocks only on its own copy).
+hipStream_t pull_stream(int device) {
+  thread_local hipStream_t st = nullptr;
+  thread_local int dev = -1;
+  if (st && dev == device) return st;
+  if (st) (void)hipStreamDestroy(st);
+  st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
+  dev = device;
+  return st;
+}
+
+}  // namespace
+}  // namespace bpsr
+
+using namespace bpsr;
+
+extern "C" {
+
+int byteps_server_config_from_env(byteps_server_config* cfg) {
+  if (!cfg) return fail(BYTEPS_REDUCE_EARGS, "null config");
+  cfg->num_workers = getenv("DMLC_NUM_WORKER") ? atoi(getenv("DMLC_NUM_WORKER")) : 1;
+  cfg->engine_lanes = getenv("BYTEPS_SERVER_ENGINE_THREAD")
+                          ? atoi(getenv("BYTEPS_SERVER_ENGINE_THREAD")) : 4;
+  const char* a = getenv("BYTEPS_ENABLE_ASYNC");
+  cfg->async_mode = (a && atoi(a) != 0) ? 1 : 0;
+  const char* p = getenv("BPSR_SERVER_POLICY");
+  cfg->policy = (p && std::string(p) == "incremental") ? BYTEPS_SERVER_INCREMENTAL
+                                                       : BYTEPS_SERVER_FUSED;
+  cfg->device = 0;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
+  if (!cfg || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  *out = nullptr;
+  if (cfg->num_workers < 1) return fail(BYTEPS_REDUCE_EARGS, "num_workers must be >= 1");
+  if (cfg->engine_lanes < 1)  // server.cc:332 CHECK_GE(engine_thread_num_, 1)
+    return fail(BYTEPS_REDUCE_EARGS, "engine_lanes must be >= 1");
+  if (cfg->policy != BYTEPS_SERVER_FUSED && cfg->policy != BYTEPS_SERVER_INCREMENTAL)
+    return fail(BYTEPS_REDUCE_EARGS, "unknown policy %d", cfg->policy);
+  auto s = std::make_unique<byteps_server>();
+  s->cfg = *cfg;
+  int rc = set_device(s.get());
+  if (rc) return rc;
+  s->lanes.resize(cfg->engine_lanes);
+  s->acc_load.assign(cfg->engine_lanes, 0);
+  for (auto& L : s->lanes) {
+    hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      byteps_server_destroy(s.release());
+      return hip_fail(e, "hipStreamCreate");
+    }
+  }
+  *out = s.release();
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_destroy(byteps_server* s) {
+  if (!s) return BYTEPS_REDUCE_OK;
+  (void)hipSetDevice(s->cfg.device);
+  for (auto& L : s->lanes) {
+    if (L.fold) (void)hipStreamSynchronize(L.fold);
+    if (L.copy) (void)hipStreamSynchronize(L.copy);
+  }
+  for (auto& kv : s->keys) {
+    KeyState* ks = kv.second.get();
+    if (ks->done) (void)hipEventDestroy(ks->done);
+    if (ks->copied) (void)hipEventDestroy(ks->copied);
+    if (ks->arena) (void)hipFree(ks->arena);
+  }
+  for (auto& L : s->lanes) {
+    if (L.fold) (void)hipStreamDestroy(L.fold);
+    if (L.copy) (void)hipStreamDestroy(L.copy);
+  }
+  delete s;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype) {
+  if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, true);
+  std::lock_guard<std::mutex> g(ks->mu);
+  return allocate(s, ks, len, dtype);
+}
+
+int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
+                       int dtype, int location) {
+  if (!s || !data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, true);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  if ((rc = allocate(s, ks, len, dtype))) return rc;
+  if (s->cfg.async_mode == 0 && ks->inited && ks->got[worker]) {
+    // A worker's next-round push may arrive while the key still waits for the
+    // other workers' pulls of this round; hold it until the key re-arms.
+    ks->cv.wait(lk, [&] { return !ks->got[worker]; });
+  }
+  if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
+  return arrive_and_wait_init(s, ks, worker, lk);
+}
+
+int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot) {
+  if (!s || !slot) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated)
+    return fail(BYTEPS_REDUCE_EARGS, "key %llu not initialised (byteps_server_init_key)",
+                (unsigned long long)key);
+  std::lock_guard<std::mutex> g(ks->mu);
+  if (ks->has_done) {  // the slot may be read by the last queued fold
+    hipError_t e = hipEventSynchronize(ks->done);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+  }
+  *slot = ks->slot[worker];
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
+  if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
+  std::unique_lock<std::mutex> lk(ks->mu);
+  return arrive_and_wait_init(s, ks, worker, lk);
+}
+
+int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location) {
+  if (!s || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated)  // server.cc:282-283
+    return fail(BYTEPS_REDUCE_EARGS,
+                "Processing pull request when the key %llu has not been inited yet",
+                (unsigned long long)key);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished; });
+  hipStream_t cs = pull_stream(s->cfg.device);
+  if (!cs) return fail(BYTEPS_REDUCE_EHIP, "cannot create the pull stream");
+  // Order the copy after the round's fold while still holding the key lock
+  // (async mode keeps adding into the store); the copy itself runs unlocked.
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(cs, ks->done, 0) : hipSuccess;
+  lk.unlock();
+  // In sync mode the store cannot change while this pull is outstanding: the
+  // next round needs this worker's next push, which follows the pull.
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out, ks->store, len,
+                       location == BYTEPS_SERVER_HOST ? hipMemcpyDeviceToHost
+                                                      : hipMemcpyDeviceToDevice, cs);
+  if (e == hipSuccess) e = hipStreamSynchronize(cs);
+  if (e != hipSuccess) return hip_fail(e, "pull copy");
+  lk.lock();
+  if (!s->cfg.async_mode) {
+    // server.cc:105-113: after NumWorkers pulls the key re-arms
+    if (++ks->pull_cnt == s->cfg.num_workers) {
+      ks->push_finished = false;
+      ks->pull_cnt = 0;
+    }
+    ks->cv.notify_all();
+  }
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
+                           int* last_order, int max_order) {
+  if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
+  KeyState* ks = get_key(s, key, false);
+  if (!ks) return fail(BYTEPS_REDUCE_EARGS, "unknown key");
+  std::lock_guard<std::mutex> g(ks->mu);
+  if (rounds) *rounds = ks->rounds;
+  if (lane) *lane = ks->lane;
+  if (last_order)
+    for (int i = 0; i < max_order && i < (int)ks->last_order.size(); ++i)
+      last_order[i] = ks->last_order[i];
+  return BYTEPS_REDUCE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+"""Python mirror of the GPU-resident PS server (include/bpsr/server.h).
+
+``PSServer`` keeps the request semantics of byteps/server/server.cc
+(``BytePSHandler`` for pushes and pulls, engine lanes chosen like
+``GetThreadID``) with an in-process transport: ``push(key, worker, data)`` /
+``pull(key, out)`` take numpy arrays (host) or torch tensors (host or device).
+Worker threads call them concurrently, as ps-lite's receive threads would.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .reducer import ReduceError, _check, load_library
+
+FUSED, INCREMENTAL = 0, 1
+HOST, DEVICE = 0, 1
+
+SERVER_EXPORTS = (
+    "byteps_server_config_from_env", "byteps_server_create", "byteps_server_destroy",
+    "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
+    "byteps_server_push_ready", "byteps_server_pull", "byteps_server_key_info",
+)
+
+_vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+
+
+class ServerConfig(ctypes.Structure):
+    _fields_ = [("num_workers", _int), ("engine_lanes", _int), ("policy", _int),
+                ("async_mode", _int), ("device", _int)]
+
+
+def _lib():
+    L = load_library()
+    if not getattr(L, "_server_bound", False):
+        L.byteps_server_config_from_env.argtypes = [ctypes.POINTER(ServerConfig)]
+        L.byteps_server_create.argtypes = [ctypes.POINTER(ServerConfig), ctypes.POINTER(_vp)]
+        L.byteps_server_destroy.argtypes = [_vp]
+        L.byteps_server_init_key.argtypes = [_vp, _u64, _sz, _int]
+        L.byteps_server_push.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int]
+        L.byteps_server_recv_slot.argtypes = [_vp, _u64, _int, ctypes.POINTER(_vp)]
+        L.byteps_server_push_ready.argtypes = [_vp, _u64, _int]
+        L.byteps_server_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
+        L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
+                                             ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
+        L._server_bound = True
+    return L
+
+
+def _buf(x):
+    """(pointer, nbytes, location) of a numpy array or torch tensor."""
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"]
+        return x.ctypes.data, x.nbytes, HOST
+    if hasattr(x, "data_ptr"):
+        loc = DEVICE if x.device.type == "cuda" else HOST
+        return int(x.data_ptr()), x.numel() * x.element_size(), loc
+    raise TypeError(f"unsupported buffer {type(x)!r}")
+
+
+def config_from_env() -> ServerConfig:
+    c = ServerConfig()
+    _check(_lib().byteps_server_config_from_env(ctypes.byref(c)))
+    return c
+
+
+class PSServer:
+    def __init__(self, num_workers: int, engine_lanes: int = 4, policy: int = FUSED,
+                 async_mode: bool = False, device: int = 0):
+        self.lib = _lib()
+        self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device)
+        self.handle = _vp()
+        _check(self.lib.byteps_server_create(ctypes.byref(self.cfg), ctypes.byref(self.handle)))
+
+    def init_key(self, key: int, nbytes: int, dtype: int) -> None:
+        _check(self.lib.byteps_server_init_key(self.handle, key, nbytes, int(dtype)))
+
+    def push(self, key: int, worker: int, data, dtype: int, nbytes: int | None = None) -> None:
+        p, n, loc = _buf(data)
+        _check(self.lib.byteps_server_push(self.handle, key, worker, p,
+                                           n if nbytes is None else nbytes, int(dtype), loc))
+
+    def recv_slot(self, key: int, worker: int) -> int:
+        out = _vp()
+        _check(self.lib.byteps_server_recv_slot(self.handle, key, worker, ctypes.byref(out)))
+        return int(out.value)
+
+    def push_ready(self, key: int, worker: int) -> None:
+        _check(self.lib.byteps_server_push_ready(self.handle, key, worker))
+
+    def pull(self, key: int, out, nbytes: int | None = None) -> None:
+        p, n, loc = _buf(out)
+        _check(self.lib.byteps_server_pull(self.handle, key, p, n if nbytes is None else nbytes,
+                                           loc))
+
+    def key_info(self, key: int):
+        rounds, lane = _u64(), _int()
+        order = (_int * self.cfg.num_workers)()
+        _check(self.lib.byteps_server_key_info(self.handle, key, ctypes.byref(rounds),
+                                               ctypes.byref(lane), order, self.cfg.num_workers))
+        return int(rounds.value), int(lane.value), list(order)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.byteps_server_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+__all__ = ["PSServer", "ServerConfig", "config_from_env", "FUSED", "INCREMENTAL", "HOST",
+           "DEVICE", "ReduceError", "SERVER_EXPORTS"]

@@ -11,17 +11,21 @@ from prophet_amd import reducer
 from prophet_amd.dtypes import ALL_DTYPES, elem_size
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "bpsr", "reduce.h")
+HEADERS = [os.path.join(ROOT, "include", "bpsr", h) for h in ("reduce.h", "server.h")]
 
 
-def header_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(byteps_\w+)\s*\(", text)))
+def header_functions(headers=HEADERS):
+    names = set()
+    for h in headers:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(byteps_\w+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_declares_expected_api():
-    assert header_functions() == sorted(reducer.EXPORTS)
+    from prophet_amd.server import SERVER_EXPORTS
+    assert header_functions(HEADERS[:1]) == sorted(reducer.EXPORTS)
+    assert header_functions(HEADERS[1:]) == sorted(SERVER_EXPORTS)
 
 
 def test_library_exports_every_header_symbol():
@@ -82,3 +86,34 @@ def test_tuning_roundtrip():
 def test_bucket_desc_layout_matches_header():
     # void* dst; const void* srcs[32]; size_t len; int n; int reserved;
     assert ctypes.sizeof(reducer.BucketDesc) == 8 + 32 * 8 + 8 + 4 + 4
+
+
+def test_cpp_wrapper_compiles_with_reference_flags(tmp_path):
+    """include/bpsr/gpu_reducer.hpp + reduce.h under the reference's own
+    compiler settings (g++ -std=c++11 -Wall, setup.py:171), linked to libbpsr.so."""
+    exe = tmp_path / "header_check"
+    src = os.path.join(ROOT, "tests", "cpp", "header_check.cpp")
+    libdir = os.path.dirname(reducer.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    src, "-L", libdir, "-lbpsr", f"-Wl,-rpath,{libdir}", "-o", str(exe)],
+                   check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "fails=0" in r.stdout
+
+
+def test_server_config_and_errors_without_gpu(monkeypatch):
+    from prophet_amd import server
+    monkeypatch.setenv("DMLC_NUM_WORKER", "8")
+    monkeypatch.setenv("BYTEPS_SERVER_ENGINE_THREAD", "3")
+    monkeypatch.setenv("BYTEPS_ENABLE_ASYNC", "0")
+    monkeypatch.setenv("BPSR_SERVER_POLICY", "incremental")
+    c = server.config_from_env()
+    assert (c.num_workers, c.engine_lanes, c.async_mode, c.policy) == (8, 3, 0, server.INCREMENTAL)
+    lib = server._lib()
+    bad = server.ServerConfig(0, 4, 0, 0, 0)
+    h = ctypes.c_void_p()
+    assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
+    bad = server.ServerConfig(2, 0, 0, 0, 0)      # server.cc:332 CHECK_GE(threads, 1)
+    assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
+    assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS

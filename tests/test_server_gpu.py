@@ -1,0 +1,208 @@
+"""GPU-resident PS server (include/bpsr/server.h) against the reference's
+server semantics (byteps/server/server.cc:147-308): concurrent worker threads,
+random arrival order, several rounds, both policies; results bit-exact with the
+oracle's left fold in the recorded arrival order."""
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from golden_util import assert_bytes_match
+from oracle.oracle import PortReducer
+from prophet_amd import synth
+from prophet_amd.dtypes import DType, elem_size
+
+torch = pytest.importorskip("torch")
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(180)]
+
+
+@pytest.fixture(scope="module")
+def port():
+    assert torch.cuda.is_available()
+    return PortReducer(nthreads=4)
+
+
+def data(dt, n, worker, rnd, key):
+    return np.ascontiguousarray(synth.bucket(dt, n, worker, "normal", 1000 * rnd + 37 * key)) \
+        .view(np.uint8)
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
+def test_sync_rounds_concurrent_workers(port, policy, dt):
+    from prophet_amd.server import PSServer
+    N, R = 8, 3
+    sizes = [1, 7, 1000, 65_536 + 3, 1_000_003]    # elements per key
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=4, policy=policy)
+    bar = threading.Barrier(N + 1)
+    errors = []
+    results = {}
+
+    def worker(w):
+        try:
+            rng = random.Random(w)
+            for rnd in range(R + 1):               # round 0 = init pushes
+                keys = list(range(len(sizes)))
+                if rnd > 0:
+                    # init pushes block until every worker's arrived, so they go
+                    # in declaration order like BytePS's InitTensor (operations.cc:219)
+                    rng.shuffle(keys)
+                for j in keys:
+                    time.sleep(rng.random() * 0.002)
+                    srv.push(j, w, data(dt, sizes[j], w, rnd, j), dt)
+                bar.wait()                          # main thread reads arrival orders
+                bar.wait()
+                if rnd == 0:
+                    continue
+                for j in keys:
+                    out = np.zeros(sizes[j] * es, np.uint8)
+                    srv.pull(j, out)
+                    results[(w, rnd, j)] = out
+        except Exception as e:  # surfaced below
+            errors.append(e)
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    orders = {}
+    for rnd in range(R + 1):
+        bar.wait()
+        for j in range(len(sizes)):
+            rounds, lane, order = srv.key_info(j)
+            assert rounds == rnd
+            orders[(rnd, j)] = order
+        bar.wait()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for rnd in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            order = orders[(rnd, j)]
+            assert sorted(order) == list(range(N))
+            ins = [data(dt, n, w, rnd, j) for w in order]
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, ins, n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, results[(w, rnd, j)], want, nan_class_f32_f64=False,
+                                   what=f"round {rnd} key {j} worker {w}")
+    srv.close()
+
+
+def test_fused_equals_incremental_in_same_order(port):
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT16, 5, 300_001
+    outs = []
+    for policy in (0, 1):
+        srv = PSServer(N, policy=policy)
+        init = [threading.Thread(target=srv.push, args=(0, w, data(dt, n, w, 0, 0), dt))
+                for w in range(N)]    # init round: each push blocks until all arrived
+        for t in init:
+            t.start()
+        for t in init:
+            t.join()
+        for w in (3, 0, 4, 1, 2):
+            srv.push(0, w, data(dt, n, w, 1, 0), dt)
+        out = np.zeros(n * 2, np.uint8)
+        srv.pull(0, out)
+        assert srv.key_info(0)[2] == [3, 0, 4, 1, 2]
+        outs.append(out)
+        srv.close()
+    assert np.array_equal(outs[0], outs[1])
+    want = np.zeros(n * 2, np.uint8)
+    port.sum_n(want, [data(dt, n, w, 1, 0) for w in (3, 0, 4, 1, 2)], n * 2, dt)
+    assert np.array_equal(outs[0], want)
+
+
+def test_pull_blocks_until_round_complete():
+    from prophet_amd.server import PSServer
+    N, n, dt = 3, 4096, DType.INT32
+    srv = PSServer(N)
+    init = [threading.Thread(target=srv.push, args=(7, w, np.zeros(n, np.int32), dt))
+            for w in range(N)]
+    for t in init:
+        t.start()
+    for t in init:
+        t.join()
+    got = {}
+
+    def puller():
+        out = np.zeros(n, np.int32)
+        srv.pull(7, out)
+        got["v"] = out
+
+    srv.push(7, 0, np.full(n, 1, np.int32), dt)
+    srv.push(7, 1, np.full(n, 2, np.int32), dt)
+    t = threading.Thread(target=puller)
+    t.start()
+    time.sleep(0.3)
+    assert "v" not in got                     # round not finished: pull queued
+    srv.push(7, 2, np.full(n, 4, np.int32), dt)
+    t.join(timeout=10)
+    assert (got["v"] == 7).all()
+    srv.close()
+
+
+def test_async_mode_sums_into_store():
+    from prophet_amd.server import PSServer
+    N, n, dt = 4, 10_001, DType.INT64
+    srv = PSServer(N, async_mode=True)
+    init = np.arange(n, dtype=np.int64)
+    ts = [threading.Thread(target=srv.push, args=(1, w, init, dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for w in range(N):
+        srv.push(1, w, np.full(n, w + 1, np.int64), dt)
+    out = np.zeros(n, np.int64)
+    srv.pull(1, out)                      # async: answered immediately
+    assert np.array_equal(out, init + 10)
+    srv.close()
+
+
+def test_zero_copy_slot_path(port):
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 4, 77_777
+    red = GpuReducer()
+    srv = PSServer(N)
+    srv.init_key(5, n * 4, dt)
+    for rnd in range(2):
+        ins = [data(dt, n, w, rnd, 5) for w in range(N)]
+        dev = [torch.from_numpy(x).cuda() for x in ins]
+        ths = []
+        for w in range(N):
+            slot = srv.recv_slot(5, w)
+            red.copy(slot, dev[w], n * 4)
+            red.sync()
+            ths.append(threading.Thread(target=srv.push_ready, args=(5, w)))
+            ths[-1].start()
+        for t in ths:
+            t.join()
+        if rnd == 0:
+            continue
+        out = torch.empty(n * 4, dtype=torch.uint8, device="cuda")
+        srv.pull(5, out)
+        order = srv.key_info(5)[2]
+        want = np.zeros(n * 4, np.uint8)
+        port.sum_n(want, [ins[w] for w in order], n * 4, dt)
+        assert np.array_equal(out.cpu().numpy(), want)
+    srv.close()
+
+
+def test_engine_lanes_least_loaded_sticky():
+    """server.h:138-162 GetThreadID: least accumulated bytes, sticky per key."""
+    from prophet_amd.server import PSServer
+    srv = PSServer(2, engine_lanes=3)
+    sizes = [4000, 1000, 1000, 500, 3000, 100]
+    load = [0, 0, 0]
+    for k, s in enumerate(sizes):
+        srv.init_key(k, s, DType.UINT8)
+        want = min(range(3), key=lambda i: (load[i], i))
+        load[want] += s
+        assert srv.key_info(k)[1] == want
+    srv.close()

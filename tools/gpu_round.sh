@@ -28,7 +28,7 @@ run() {  # name limit cmd...
 
 for s in $STEPS; do
   case $s in
-    test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     sweep) run sweep 600 python tools/sweep.py ;;
