@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Secondary BASELINE.json configs on one MI355X (bench.py measures config 2).
 
+  cfg1   2-worker fp32 64 MiB server rounds through the GPU-resident PS server
+         (host-resident and device-resident pushes, 1 key or 17 partitions).
   cfg3   8-way fp16 over ResNet-50's 161 gradient tensors (165 BytePS partitions
          of <= 4,096,000 B), Prophet block grouping: one batched launch per
          block (12 blocks) vs one launch per partition vs one launch for all.
@@ -268,15 +270,75 @@ def cfg5(red, dev, N=16, B=256 << 20, chunk=32 << 20):
          host_setup_s=round(setup_s, 1), exact_window=ok)
 
 
+def cfg1(dev, N=2, B=64 << 20):
+    """2-worker fp32 64 MiB server rounds through the GPU-resident PS server
+    (prophet_amd.server, in-process transport): pushes start in pinned host
+    memory (as ps-lite's receive buffers would be) or on the device; one round =
+    every worker pushes, then every worker pulls the merged bucket to host.
+    As one key, and as the 17 BytePS partitions of 4,096,000 B on 4 lanes."""
+    import threading
+    import torch
+    from prophet_amd.buckets import partition_tensor
+    from prophet_amd.dtypes import DType
+    from prophet_amd.server import PSServer
+    n = B // 4
+    host = [torch.randn(n).pin_memory() for _ in range(N)]
+    devd = [h.to(dev) for h in host]
+    for layout in ("1key", "17keys"):
+        parts = [(0, 0, B)] if layout == "1key" else \
+            [(p.key, p.offset, p.len) for p in partition_tensor(0, B)]
+        for src_loc, srcs in (("host", host), ("device", devd)):
+            for policy in (0, 1):
+                srv = PSServer(N, engine_lanes=4, policy=policy)
+                out = torch.empty(B, dtype=torch.uint8).pin_memory()
+
+                def rnd(init=False):
+                    def w(k):
+                        b = srcs[k].view(torch.uint8)
+                        for key, off, ln in parts:
+                            srv.push(key, k, b[off:off + ln], DType.FLOAT32)
+                        if not init:
+                            for key, off, ln in parts:
+                                if k == 0:
+                                    srv.pull(key, out[off:off + ln])
+                                else:
+                                    tmp = torch.empty(ln, dtype=torch.uint8).pin_memory() \
+                                        if not hasattr(rnd, "tmp") else rnd.tmp[:ln]
+                                    rnd.tmp = tmp if not hasattr(rnd, "tmp") else rnd.tmp
+                                    srv.pull(key, tmp[:ln])
+                    ts = [threading.Thread(target=w, args=(k,)) for k in range(N)]
+                    for t in ts:
+                        t.start()
+                    for t in ts:
+                        t.join()
+                rnd.tmp = torch.empty(B, dtype=torch.uint8).pin_memory()
+                rnd(init=True)
+                rnd()
+                ts_ = []
+                for _ in range(10):
+                    t0 = time.perf_counter()
+                    rnd()
+                    ts_.append(time.perf_counter() - t0)
+                med = statistics.median(ts_)
+                want = (host[0] + host[1]).view(torch.uint8)
+                ok = bool(torch.equal(out, want))
+                emit(config="cfg1", layout=layout, pushes_from=src_loc,
+                     policy=["fused", "incremental"][policy], n_workers=N, bucket_bytes=B,
+                     round_ms=round(med * 1e3, 3), gibps=round(N * B / med / GIB, 2), exact=ok)
+                srv.close()
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--only", default="cfg3,sweep,cfg4,cfg5")
+    p.add_argument("--only", default="cfg1,cfg3,sweep,cfg4,cfg5")
     a = p.parse_args()
     import torch
     from prophet_amd.reducer import GpuReducer
     dev = torch.device("cuda:0")
     red = GpuReducer(device=0)
     todo = a.only.split(",")
+    if "cfg1" in todo:
+        cfg1(dev)
     if "cfg3" in todo:
         cfg3(red, dev)
     if "sweep" in todo:
