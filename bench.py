@@ -221,7 +221,7 @@ def main():
     alg_bytes = (N + 1) * B
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload = f"{N}-way {args.dtype} left-fold sum of one {B / (1 << 20):.0f} MiB bucket per GPU"
-    tv, tnt, tgrid = red.get_tuning()
+    tv, tnt, tgrid, tocc = red.get_tuning()
     line = {
         "metric": "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs",
         "value": round(world * N * B / t_step / GIB, 2),
@@ -238,7 +238,8 @@ def main():
                 f"{args.sets} rotated input sets, layout={args.layout}",
         "config": {"workload": workload, "n_workers": N, "bucket_bytes": B,
                    "parallelism": f"key-space shard x{world}", "kernel": "byteps_reduce_sum_n",
-                   "tuning": {"vpt": tv, "nt": tnt, "max_grid": tgrid}},
+                   "tuning": {"vpt": tv, "nt": tnt, "max_grid": tgrid,
+                                                 "wg_per_cu": tocc}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": pmc_traffic(workload),

@@ -147,14 +147,15 @@ int byteps_reduce_dtype_size(int dtype);
 /* Thread-local description of the last error on this thread ("" if none). */
 const char* byteps_reduce_last_error(void);
 
-/* Launch tuning (process-wide; defaults chosen from rocprof measurements, see
- * DESIGN.md).  vpt: 16-B vectors per thread per tile (2, 4 or 8);
+/* Launch tuning (process-wide; defaults chosen from measurements, see
+ * DESIGN.md §4.1).  vpt: 16-B vectors per thread per tile (1, 2, 4 or 8);
  * nt: non-temporal loads and stores (0/1); max_grid: grid cap in 256-thread
- * workgroups (tile-stride beyond).
- * A value <= 0 (nt: < 0) keeps the current setting.  Also settable through
- * the environment: BPSR_VPT, BPSR_NT, BPSR_MAX_GRID. */
-int byteps_reduce_set_tuning(int vpt, int nt, int max_grid);
-int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid);
+ * workgroups (tile-stride beyond); occ: workgroups resident per CU, enforced
+ * through the dynamic LDS request (0 = hardware limit, 1..8).  A value <= 0
+ * (nt, occ: < 0) keeps the current setting.  Also settable through the
+ * environment: BPSR_VPT, BPSR_NT, BPSR_MAX_GRID, BPSR_OCC. */
+int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ);
+int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid, int* occ);
 
 #ifdef __cplusplus
 }

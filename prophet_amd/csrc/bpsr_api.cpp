@@ -81,11 +81,13 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 
 static Tuning& tuning() {
   static Tuning tu = [] {
-    Tuning t{4, 1, 1 << 20};  // tools/sweep.py, profiles/r01_sweep_*.jsonl
+    Tuning t{2, 1, 1 << 20, 1};  // tools/sweep.py, profiles/r01_sweep_*.jsonl
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
-    if (t.vpt != 2 && t.vpt != 8) t.vpt = 4;
+    if (const char* v = getenv("BPSR_OCC")) t.occ = atoi(v);
+    if (t.vpt != 1 && t.vpt != 4 && t.vpt != 8) t.vpt = 2;
+    if (t.occ < 0 || t.occ > 8) t.occ = 1;
     if (t.max_grid < 1) t.max_grid = 1 << 20;
     t.nt = t.nt ? 1 : 0;
     return t;
@@ -261,23 +263,26 @@ int byteps_reduce_dtype_size(int dtype) {
 
 const char* byteps_reduce_last_error(void) { return g_last_error.c_str(); }
 
-int byteps_reduce_set_tuning(int vpt, int nt, int max_grid) {
+int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ) {
   Tuning& t = tuning();
   if (vpt > 0) {
-    if (vpt != 2 && vpt != 4 && vpt != 8)
-      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 2, 4 or 8");
+    if (vpt != 1 && vpt != 2 && vpt != 4 && vpt != 8)
+      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2, 4 or 8");
     t.vpt = vpt;
   }
+  if (occ > 8) return fail(BYTEPS_REDUCE_EARGS, "occ must be 0..8");
   if (nt >= 0) t.nt = nt ? 1 : 0;
   if (max_grid > 0) t.max_grid = max_grid;
+  if (occ >= 0) t.occ = occ;
   return BYTEPS_REDUCE_OK;
 }
 
-int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid) {
+int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid, int* occ) {
   const Tuning& t = tuning();
   if (vpt) *vpt = t.vpt;
   if (nt) *nt = t.nt;
   if (max_grid) *max_grid = t.max_grid;
+  if (occ) *occ = t.occ;
   return BYTEPS_REDUCE_OK;
 }
 

@@ -54,10 +54,22 @@ struct BatchEntry {
 };
 
 struct Tuning {
-  int vpt;       // 16-B vectors per thread per tile (2, 4, 8)
+  int vpt;       // 16-B vectors per thread per tile (1, 2, 4, 8)
   int nt;        // non-temporal loads and stores
   int max_grid;  // grid cap in workgroups (tile-stride beyond)
+  int occ;       // workgroups resident per CU (0 = hardware limit), set through LDS
 };
+
+// Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so
+// asking for 160 KiB / occ per workgroup admits at most `occ` workgroups per
+// CU.  Fewer bytes in flight per CU stream HBM better for the 9-stream fold
+// (tools/hbm_probe2.hip).
+constexpr size_t kLdsPerCU = 160 * 1024;
+inline size_t occ_lds_bytes(int occ) {
+  return occ > 0 ? (kLdsPerCU / (size_t)occ) & ~(size_t)255 : 0;
+}
+// Allow `kernel` to request up to 160 KiB of dynamic LDS (once per kernel).
+hipError_t allow_full_lds(const void* kernel);
 
 int elem_size(int dtype);  // 0 if unsupported
 

@@ -47,6 +47,11 @@ __global__ __launch_bounds__(kBlock) void copy_kernel(unsigned char* __restrict_
   }
 }
 
+hipError_t allow_full_lds(const void* kernel) {
+  return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)kLdsPerCU);
+}
+
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s) {
   const uintptr_t d = (uintptr_t)dst, q = (uintptr_t)src;

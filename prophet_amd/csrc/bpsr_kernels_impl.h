@@ -73,12 +73,19 @@ __device__ __forceinline__ void st_e(unsigned char* p, E v, bool aligned) {
 constexpr int cmin(int a, int b) { return a < b ? a : b; }
 
 // Exact replay of one vector's fold (NaN payload rules), re-reading memory.
-// Only runs for vectors whose fast-path result holds a NaN.
+// Only runs for vectors whose fast-path result holds a NaN.  The addresses go
+// through an empty asm so the compiler cannot merge these loads with the fast
+// path's (merging drops the loads' non-temporal hint and reorders the fast
+// path's load stream around the first adds).
 template <class Op, bool NT>
 __device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* srcs, int n,
-                                                uint64_t off) {
-  typename Op::Acc acc = Op::init(ld16<NT>(srcs[0] + off));
-  for (int k = 1; k < n; ++k) Op::accum(acc, ld16<NT>(srcs[k] + off));
+                                                   uint64_t off) {
+  auto opaque = [](const unsigned char* p) {
+    asm volatile("" : "+v"(p));
+    return p;
+  };
+  typename Op::Acc acc = Op::init(ld16<NT>(opaque(srcs[0] + off)));
+  for (int k = 1; k < n; ++k) Op::accum(acc, ld16<NT>(opaque(srcs[k] + off)));
   return Op::finish(acc);
 }
 
@@ -231,8 +238,11 @@ __global__ __launch_bounds__(kBlock) void batched_kernel(const BatchEntry* __res
 
 template <class Op, int VPT, bool NT, int NS>
 static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
+  static const hipError_t lds_ok =
+      allow_full_lds(reinterpret_cast<const void*>(&fold_kernel<Op, VPT, NT, NS>));
+  if (lds_ok != hipSuccess) return lds_ok;
   hipLaunchKernelGGL((fold_kernel<Op, VPT, NT, NS>), dim3(fold_grid(a.g, tu, VPT)),
-                     dim3(kBlock), 0, s, a);
+                     dim3(kBlock), occ_lds_bytes(tu.occ), s, a);
   return hipGetLastError();
 }
 
@@ -252,16 +262,16 @@ static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_
   if (tu.nt) {
     switch (vpt) {
       case 1: return launch_fold_vpt<Op, 1, true>(a, tu, s);
-      case 2: return launch_fold_vpt<Op, 2, true>(a, tu, s);
+      case 4: return launch_fold_vpt<Op, 4, true>(a, tu, s);
       case 8: return launch_fold_vpt<Op, 8, true>(a, tu, s);
-      default: return launch_fold_vpt<Op, 4, true>(a, tu, s);
+      default: return launch_fold_vpt<Op, 2, true>(a, tu, s);
     }
   }
   switch (vpt) {
     case 1: return launch_fold_vpt<Op, 1, false>(a, tu, s);
-    case 2: return launch_fold_vpt<Op, 2, false>(a, tu, s);
+    case 4: return launch_fold_vpt<Op, 4, false>(a, tu, s);
     case 8: return launch_fold_vpt<Op, 8, false>(a, tu, s);
-    default: return launch_fold_vpt<Op, 4, false>(a, tu, s);
+    default: return launch_fold_vpt<Op, 2, false>(a, tu, s);
   }
 }
 
@@ -270,11 +280,18 @@ static hipError_t launch_batched_vpt(const BatchEntry* tab, const uint32_t* tile
                                      int nbuckets, uint32_t ntiles, const Tuning& tu,
                                      hipStream_t s) {
   const uint32_t grid = ntiles < (uint32_t)tu.max_grid ? ntiles : (uint32_t)tu.max_grid;
+  static const hipError_t ok_nt =
+      allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, true>));
+  static const hipError_t ok_t =
+      allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
+  if (ok_nt != hipSuccess) return ok_nt;
+  if (ok_t != hipSuccess) return ok_t;
+  const size_t lds = occ_lds_bytes(tu.occ);
   if (tu.nt)
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(grid), dim3(kBlock), 0, s, tab,
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(grid), dim3(kBlock), lds, s, tab,
                        tile_bucket, nbuckets, ntiles);
   else
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(grid), dim3(kBlock), 0, s, tab,
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(grid), dim3(kBlock), lds, s, tab,
                        tile_bucket, nbuckets, ntiles);
   return hipGetLastError();
 }

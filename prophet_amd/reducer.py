@@ -86,8 +86,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_sync.argtypes = [_vp]
     L.byteps_reduce_dtype_size.argtypes = [_int]
     L.byteps_reduce_last_error.restype = ctypes.c_char_p
-    L.byteps_reduce_set_tuning.argtypes = [_int, _int, _int]
-    L.byteps_reduce_get_tuning.argtypes = [ctypes.POINTER(_int)] * 3
+    L.byteps_reduce_set_tuning.argtypes = [_int, _int, _int, _int]
+    L.byteps_reduce_get_tuning.argtypes = [ctypes.POINTER(_int)] * 4
     L.byteps_reduce_plan_create.argtypes = [ctypes.POINTER(BucketDesc), _int, _int, _int,
                                             ctypes.POINTER(_vp)]
     L.byteps_reduce_plan_launch.argtypes = [_vp, _vp]
@@ -179,14 +179,14 @@ class GpuReducer:
     def sync(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_sync(_stream_of(None, stream)))
 
-    def set_tuning(self, vpt: int = 0, nt: int = -1, max_grid: int = 0) -> None:
-        _check(self.lib.byteps_reduce_set_tuning(vpt, nt, max_grid))
+    def set_tuning(self, vpt: int = 0, nt: int = -1, max_grid: int = 0, occ: int = -1) -> None:
+        _check(self.lib.byteps_reduce_set_tuning(vpt, nt, max_grid, occ))
 
-    def get_tuning(self) -> tuple[int, int, int]:
-        a, b, c = _int(), _int(), _int()
+    def get_tuning(self) -> tuple[int, int, int, int]:
+        a, b, c, d = _int(), _int(), _int(), _int()
         _check(self.lib.byteps_reduce_get_tuning(ctypes.byref(a), ctypes.byref(b),
-                                                 ctypes.byref(c)))
-        return a.value, b.value, c.value
+                                                 ctypes.byref(c), ctypes.byref(d)))
+        return a.value, b.value, c.value, d.value
 
     @staticmethod
     def dtype_size(dtype: int) -> int:

@@ -16,7 +16,11 @@ Data path (one process per GPU, torch.distributed over RCCL/xGMI):
     ``dist.batch_isend_irecv``), then the owner folds
     (``ShardedReducer.scatter_reduce``);
   * optional return leg: all-gather of the owned results
-    (``ShardedReducer.allgather``, mirrors core_loops.cc:249-254).
+    (``ShardedReducer.allgather``, mirrors core_loops.cc:249-254);
+  * worker local reduce: every GPU holds a full gradient; each owner receives
+    its slice from every GPU and folds them in rank order
+    (``ShardedReducer.reduce_scatter`` / ``allreduce``): a deterministic,
+    bit-reproducible replacement for ncclReduceScatter + ncclAllGather.
 """
 from __future__ import annotations
 
@@ -126,6 +130,41 @@ class ShardedReducer:
                 r.wait()
         if self.owned:
             self.fold(dst, list(recv_slots))
+
+    def reduce_scatter(self, local_full, recv_slots, dst) -> None:
+        """Worker local reduce (REDUCE stage, core_loops.cc:184-247): every rank
+        holds its own full gradient vector ``local_full`` (n_elems); rank g
+        receives slice g of every rank's vector into ``recv_slots[r]`` (grouped
+        point-to-point over RCCL/xGMI) and folds them in RANK order into ``dst``.
+        Unlike ncclReduceScatter, whose summation order follows the ring, the
+        result is a fixed left fold: bit-reproducible and equal to the oracle."""
+        dist = self.dist
+        ops = []
+        for g, (lo, hi) in enumerate(self.ranges):
+            if g != self.rank and hi > lo:
+                ops.append(dist.P2POp(dist.isend, local_full[lo:hi], g, self.group))
+        if self.owned:
+            for r in range(self.world):
+                if r != self.rank:
+                    ops.append(dist.P2POp(dist.irecv, recv_slots[r], r, self.group))
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        if self.owned:
+            recv_slots[self.rank].copy_(local_full[self.lo:self.hi])
+            self.fold(dst, list(recv_slots))
+
+    def allreduce(self, local_full, out_full, recv_slots=None, owned=None) -> None:
+        """Deterministic all-reduce = reduce_scatter (P2P + HIP fold in rank
+        order) + allgather (core_loops.cc:248-261 return leg)."""
+        import torch
+        if recv_slots is None:
+            recv_slots = [torch.empty(self.owned, dtype=local_full.dtype, device=local_full.device)
+                          for _ in range(self.world)]
+        if owned is None:
+            owned = torch.empty(self.owned, dtype=local_full.dtype, device=local_full.device)
+        self.reduce_scatter(local_full, recv_slots, owned)
+        self.allgather(owned, out_full)
 
     def allgather(self, owned_result, full_out) -> None:
         """Return leg: every rank gets the whole reduced vector (core_loops.cc:249-254).

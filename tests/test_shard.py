@@ -84,6 +84,9 @@ def _worker(rank, world, port, n_elems, n_workers, q):
         full = torch.empty(n_elems, dtype=torch.float32)
         sr.allgather(owned, full)
         q.put((rank, full.numpy().tobytes()))
+    except Exception as e:      # fail fast instead of a queue timeout
+        q.put((rank, repr(e)))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -110,5 +113,51 @@ def test_scatter_reduce_allgather_gloo(world):
            for k in range(n_workers)]
     want = np.zeros(n_elems * 4, np.uint8)
     PortReducer().sum_n(want, ins, want.nbytes, DType.FLOAT32)
+    for r in range(world):
+        assert results[r] == want.tobytes(), f"rank {r}"
+
+
+def _worker_allreduce(rank, world, port, n_elems, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from prophet_amd import synth
+        from prophet_amd.dtypes import DType
+        from prophet_amd.shard import ShardedReducer
+        sr = ShardedReducer(n_elems, fold=_oracle_fold())
+        mine = torch.from_numpy(synth.bucket(DType.FLOAT16, n_elems, rank, "bits", 91)).view(torch.float16)
+        out = torch.empty(n_elems, dtype=torch.float16)
+        sr.allreduce(mine, out)
+        q.put((rank, out.numpy().tobytes()))
+    except Exception as e:      # fail fast instead of a queue timeout
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_local_reduce_allreduce_rank_order_gloo(world):
+    """Worker local reduce (core_loops.cc:184-261) as P2P + fold + all-gather:
+    every rank ends with the oracle's left fold in rank order (fp16 per-step RNE)."""
+    n_elems = 9_999
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_allreduce, args=(r, world, port, n_elems, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from oracle.oracle import PortReducer
+    from prophet_amd import synth
+    from prophet_amd.dtypes import DType
+    ins = [np.ascontiguousarray(synth.bucket(DType.FLOAT16, n_elems, r, "bits", 91)).view(np.uint8)
+           for r in range(world)]
+    want = np.zeros(n_elems * 2, np.uint8)
+    PortReducer().sum_n(want, ins, want.nbytes, DType.FLOAT16)
     for r in range(world):
         assert results[r] == want.tobytes(), f"rank {r}"

@@ -22,21 +22,27 @@
   } while (0)
 
 typedef float f4 __attribute__((ext_vector_type(4)));
-struct Ops { char* p[9]; };
+struct Ops { char* p[17]; };
 
-template <int LAUX, int SAUX, int VPT, bool INPLACE>
+template <int LAUX, int SAUX, int VPT, bool INPLACE, int NSRC = 8, bool INDEP = false>
 __global__ __launch_bounds__(256) void fold8(Ops o, unsigned bytes_per_op) {
   const unsigned tile = blockIdx.x;
   const unsigned off0 = (tile * 256u * VPT + threadIdx.x) * 16u;
-  __amdgpu_buffer_rsrc_t r[9];
+  __amdgpu_buffer_rsrc_t r[NSRC + 1];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc(o.p[k], 0, bytes_per_op, 0x00020000);
+  for (int k = 0; k <= NSRC; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc(o.p[k], 0, bytes_per_op, 0x00020000);
   f4 acc[VPT];
+  if (INDEP) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)   // store first: no dependency on this tile's loads
+      __builtin_amdgcn_raw_buffer_store_b128(u4{1, 2, 3, tile}, r[NSRC], off0 + j * 4096u, 0, SAUX);
+  }
 #pragma unroll
   for (int j = 0; j < VPT; ++j)
     acc[j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r[0], off0 + j * 4096u, 0, LAUX));
 #pragma unroll
-  for (int k = 1; k < 8; ++k) {
+  for (int k = 1; k < NSRC; ++k) {
     f4 x[VPT];
 #pragma unroll
     for (int j = 0; j < VPT; ++j)
@@ -45,19 +51,76 @@ __global__ __launch_bounds__(256) void fold8(Ops o, unsigned bytes_per_op) {
     for (int j = 0; j < VPT; ++j) acc[j] += x[j];
   }
   typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  if (INDEP) {
+    if (acc[0].x == 12345.f) o.p[16][threadIdx.x] = 1;   // keep the loads alive
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < VPT; ++j)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[j]), INPLACE ? r[0] : r[8],
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[j]), INPLACE ? r[0] : r[NSRC],
                                            off0 + j * 4096u, 0, SAUX);
+}
+
+// Persistent variant: grid = CUs x k, each workgroup walks tiles with a stride
+// of gridDim.x and keeps the next tile's loads in flight while it folds and
+// stores the current one (software pipelining in registers).
+template <int VPT, int NSRC>
+__global__ __launch_bounds__(256) void fold_persist(Ops o, unsigned bytes_per_op, unsigned ntiles) {
+  __amdgpu_buffer_rsrc_t r[NSRC + 1];
+#pragma unroll
+  for (int k = 0; k <= NSRC; ++k) r[k] = __builtin_amdgcn_make_buffer_rsrc(o.p[k], 0, bytes_per_op, 0x00020000);
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  f4 a[NSRC][VPT], b[NSRC][VPT];
+  unsigned tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  auto issue = [&](f4 (&x)[NSRC][VPT], unsigned t) __attribute__((always_inline)) {
+    const unsigned off0 = (t * 256u * VPT + threadIdx.x) * 16u;
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k)
+#pragma unroll
+      for (int j = 0; j < VPT; ++j)
+        x[k][j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r[k], off0 + j * 4096u, 0, 2));
+  };
+  auto finish = [&](f4 (&x)[NSRC][VPT], unsigned t) __attribute__((always_inline)) {
+    const unsigned off0 = (t * 256u * VPT + threadIdx.x) * 16u;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      f4 acc = x[0][j];
+#pragma unroll
+      for (int k = 1; k < NSRC; ++k) acc += x[k][j];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc), r[NSRC], off0 + j * 4096u, 0, 2);
+    }
+  };
+  issue(a, tile);
+  for (;;) {
+    const unsigned nxt = tile + gridDim.x;
+    if (nxt < ntiles) issue(b, nxt);
+    finish(a, tile);
+    if (nxt >= ntiles) break;
+    tile = nxt;
+    const unsigned nx2 = tile + gridDim.x;
+    if (nx2 < ntiles) issue(a, nx2);
+    finish(b, tile);
+    if (nx2 >= ntiles) break;
+    tile = nx2;
+  }
 }
 
 struct V {
   const char* name;
   void (*fn)(Ops, unsigned, int, hipStream_t);
 };
-template <int LA, int SA, int VPT, bool IP>
+template <int LA, int SA, int VPT, bool IP, int NS = 8, bool IND = false, int LDS_KB = 0>
 static void L(Ops o, unsigned b, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((fold8<LA, SA, VPT, IP>), dim3(grid), dim3(256), 0, s, o, b);
+  // LDS_KB of dynamic LDS per workgroup caps residency (160 KiB per CU)
+  hipLaunchKernelGGL((fold8<LA, SA, VPT, IP, NS, IND>), dim3(grid), dim3(256), LDS_KB * 1024, s, o, b);
+}
+
+template <int VPT, int NS, int GRID_PER_CU, int LDS_KB>
+static void P(Ops o, unsigned b, int grid, hipStream_t s) {
+  const unsigned ntiles = (unsigned)grid;  // caller passes the tile count
+  hipLaunchKernelGGL((fold_persist<VPT, NS>), dim3(256 * GRID_PER_CU), dim3(256), LDS_KB * 1024, s,
+                     o, b, ntiles);
 }
 
 int main(int argc, char** argv) {
@@ -69,23 +132,28 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<V> vs = {
-      {"l0_s0", L<0, 0, 4, false>},       {"l2_s2", L<2, 2, 4, false>},
-      {"l2_s0", L<2, 0, 4, false>},       {"l0_s2", L<0, 2, 4, false>},
-      {"l2_s16", L<2, 16, 4, false>},     {"l2_s18", L<2, 18, 4, false>},
-      {"l2_s17", L<2, 17, 4, false>},     {"l3_s2", L<3, 2, 4, false>},
-      {"l16_s2", L<16, 2, 4, false>},     {"l18_s18", L<18, 18, 4, false>},
-      {"l2_s2_v2", L<2, 2, 2, false>},    {"l2_s2_v8", L<2, 2, 8, false>},
-      {"inpl_l2_s2", L<2, 2, 4, true>},   {"inpl_l0_s0", L<0, 0, 4, true>},
-      {"inpl_l2_s0", L<2, 0, 4, true>},   {"inpl_l2_s2_v8", L<2, 2, 8, true>},
+      {"n8", L<2, 2, 4, false, 8>},
+      {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
+      {"n8_v1_wg2cu", L<2, 2, 1, false, 8, false, 80>},
+      {"n8_persist_v2_g1", P<2, 8, 1, 160>},
+      {"n8_persist_v1_g1", P<1, 8, 1, 160>},
+      {"n8_persist_v4_g1", P<4, 8, 1, 160>},
+      {"n8_persist_v1_g2", P<1, 8, 2, 80>},
+      {"n8_persist_v2_g2", P<2, 8, 2, 80>},
+      {"n8_persist_v2_g1nolds", P<2, 8, 1, 0>},
+      {"n8_persist_v1_g4", P<1, 8, 4, 40>},
+      {"n16_persist_v1_g1", P<1, 16, 1, 160>},
+      {"n16_persist_v2_g1", P<2, 16, 1, 160>},
+      {"n16_v2_wg1cu", L<2, 2, 2, false, 16, false, 160>},
   };
-  const size_t skews[] = {0, 4096, 16384, 65536};
+  const size_t skews[] = {16384};
   for (int rep = 0; rep < 2; ++rep) {
     for (size_t skew : skews) {
       const size_t stride = B + skew;
       std::vector<char*> slab(sets);
       for (int s = 0; s < sets; ++s) {
-        CK(hipMalloc(&slab[s], 9 * stride));
-        CK(hipMemset(slab[s], 0, 9 * stride));
+        CK(hipMalloc(&slab[s], 17 * stride));
+        CK(hipMemset(slab[s], 0, 17 * stride));
       }
       for (const V& v : vs) {
         float best = 1e30f;
@@ -94,11 +162,13 @@ int main(int argc, char** argv) {
           CK(hipEventRecord(e0, st));
           for (int r = 0; r < reps; ++r) {
             Ops o;
-            for (int k = 0; k < 9; ++k) o.p[k] = slab[r % sets] + k * stride;
+            int ns = atoi(v.name + 1);
+            for (int k = 0; k <= ns; ++k) o.p[k] = slab[r % sets] + k * stride;
+            for (int k = ns + 1; k < 17; ++k) o.p[k] = slab[r % sets] + 16 * stride;
             // grid derived from the name's VPT suffix
             int VPT = 4;
             for (const char* c = v.name; *c; ++c)
-              if (c[0] == '_' && c[1] == 'v') VPT = atoi(c + 2);
+              if (c[0] == '_' && c[1] == 'v' && c[2] >= '0' && c[2] <= '9') VPT = atoi(c + 2);
             v.fn(o, (unsigned)B, (int)(B / 16 / (256 * VPT)), st);
           }
           CK(hipEventRecord(e1, st));
@@ -108,8 +178,9 @@ int main(int argc, char** argv) {
           ms /= reps;
           if (round > 0 && ms < best) best = ms;
         }
+        const int ns = atoi(v.name + 1);
         printf("{\"v\": \"%s\", \"skew\": %zu, \"rep\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
-               v.name, skew, rep, best, 9.0 * B / (best * 1e-3) / 1e9);
+               v.name, skew, rep, best, (ns + 1.0) * B / (best * 1e-3) / 1e9);
         fflush(stdout);
       }
       for (int s = 0; s < sets; ++s) CK(hipFree(slab[s]));

@@ -26,10 +26,11 @@ def main():
     p.add_argument("--dtype", default="f32")
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=10)
-    p.add_argument("--vpt", default="4,8,16")
-    p.add_argument("--nt", default="0,1")
-    p.add_argument("--grid", default="2048,1048576")
-    p.add_argument("--layouts", default="separate,skew0,skew4k,skew12k,skew68k,skew324k")
+    p.add_argument("--vpt", default="1,2,4")
+    p.add_argument("--nt", default="1")
+    p.add_argument("--grid", default="1048576")
+    p.add_argument("--occ", default="0,1,2")
+    p.add_argument("--layouts", default="separate,skew16k")
     a = p.parse_args()
 
     import torch
@@ -71,7 +72,8 @@ def main():
 
     variants = list(itertools.product([int(x) for x in a.vpt.split(",")],
                                       [int(x) for x in a.nt.split(",")],
-                                      [int(x) for x in a.grid.split(",")]))
+                                      [int(x) for x in a.grid.split(",")],
+                                      [int(x) for x in a.occ.split(",")]))
     alg = (N + 1) * B
     for layout in a.layouts.split(","):
         sets = make_sets(layout.split("@")[0])
@@ -90,7 +92,7 @@ def main():
             med, mn = statistics.median(ts), min(ts)
             gbps = (2 * B if k == "torch_copy" else alg) / (med * 1e-3) / 1e9
             print(json.dumps({"layout": layout, "variant": k if isinstance(k, str) else
-                              {"vpt": k[0], "nt": k[1], "max_grid": k[2]},
+                              {"vpt": k[0], "nt": k[1], "max_grid": k[2], "occ": k[3]},
                               "median_ms": round(med, 4), "min_ms": round(mn, 4),
                               "GBps": round(gbps, 1), "frac_8TBps": round(gbps / 8000, 4)}),
                   flush=True)
