@@ -41,6 +41,7 @@ struct FoldArgs {
   int n;
   int aligned;  // every operand element-aligned
   FoldGeom g;
+  uint64_t grid;  // launched workgroups (set by the launcher)
 };
 
 struct BatchEntry {
@@ -83,15 +84,16 @@ int hip_fail(hipError_t e, const char* what);
 void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, int n,
                bool copy_trailing, FoldGeom* g, int* aligned);
 
-// Tiles of kBlock*vpt vectors; one workgroup per tile up to max_grid, then
-// tile-stride.  The element path reuses the same threads (grid-stride).
+// One workgroup per tile of kBlock*vpt vectors (no cap: workgroups are
+// dispatched in tile order, which keeps the HBM sweep tight); the element path
+// reuses the same threads, grid-stride, when there is no vector range.
 inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
+  (void)tu;
   const uint64_t tile = (uint64_t)kBlock * vpt;
   uint64_t blocks = (g.nvec + tile - 1) / tile;
   const uint64_t scalar = g.head_elems + (g.n_elems - g.tail_begin) + g.trailing_bytes;
   const uint64_t sblocks = (scalar + kBlock - 1) / kBlock;
-  if (sblocks > blocks) blocks = sblocks;
-  if (blocks > (uint64_t)tu.max_grid) blocks = tu.max_grid;
+  if (blocks == 0) blocks = sblocks < 65536 ? sblocks : 65536;
   if (blocks < 1) blocks = 1;
   return (int)blocks;
 }

@@ -153,12 +153,74 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
   }
 }
 
+// Full tile through buffer instructions: one SGPR descriptor per operand
+// based at the tile's first byte (wave-uniform: kernel arguments + blockIdx),
+// 32-bit lane offsets, nt as the cache-policy operand.  Same load grouping,
+// fast fold and NaN replay as fold_tile_body.
+template <class Op, int VPT, bool NT, int NS>
+__device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs, int n,
+                                                   unsigned char* dst, uint64_t byte0, int lane) {
+  constexpr int kAux = NT ? 2 : 0;               // 2 = nt
+  constexpr int kTileBytes = kBlock * VPT * 16;
+  constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
+  const int ns = NS > 0 ? NS : n;
+  const int voff = lane * 16;
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  auto rsrc = [&](const unsigned char* base) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned char*>(base) + byte0, 0,
+                                             kTileBytes, 0x00020000);
+  };
+  typename Op::Acc acc[VPT];
+  auto group = [&](int k0) __attribute__((always_inline)) {
+    vec16 x[G][VPT];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (NS > 0 || k0 + g < ns) {
+        const auto r = rsrc(srcs[k0 + g]);
+#pragma unroll
+        for (int j = 0; j < VPT; ++j)
+          x[g][j] = bitcast<vec16>(__builtin_amdgcn_raw_buffer_load_b128(r, voff + j * kBlock * 16,
+                                                                         0, kAux));
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (NS > 0 || k0 + g < ns) {
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) {
+          if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
+          else Op::fast(acc[j], x[g][j]);
+        }
+      }
+    }
+  };
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int k0 = 0; k0 < NS; k0 += G) group(k0);
+  } else {
+    for (int k0 = 0; k0 < ns; k0 += G) group(k0);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) bad = bad || Op::has_nan(acc[j]);
+  const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + byte0, 0, kTileBytes, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    vec16 out = Op::finish(acc[j]);
+    if (__builtin_expect(bad, 0)) {
+      if (Op::has_nan(acc[j]))
+        out = fold_vector_exact<Op, NT>(srcs, ns, byte0 + voff + j * kBlock * 16);
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(bitcast<u4>(out), rd, voff + j * kBlock * 16, 0, kAux);
+  }
+}
+
 template <class Op, int VPT, bool NT, int NS>
 __device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int n,
                                           unsigned char* dst, uint64_t vec_off, uint64_t v0,
                                           uint64_t nvec, int lane) {
   if (v0 + (uint64_t)kBlock * VPT <= nvec)
-    fold_tile_body<Op, VPT, NT, NS, false>(srcs, n, dst, vec_off, v0, nvec, lane);
+    fold_tile_full_buf<Op, VPT, NT, NS>(srcs, n, dst, vec_off + v0 * 16, lane);
   else
     fold_tile_body<Op, VPT, NT, NS, true>(srcs, n, dst, vec_off, v0, nvec, lane);
 }
@@ -203,15 +265,55 @@ __device__ __forceinline__ void fold_elements(const unsigned char* const* srcs, 
   }
 }
 
+// Pin every kernel argument the tile loop needs in SGPRs at kernel entry (no
+// instruction emitted): ONE asm statement, so all the scalar loads issue
+// together behind one s_waitcnt instead of as a chain of dependent scalar
+// round trips.  With one resident workgroup per CU that chain would be paid
+// on every tile.
+template <int NS>
+__device__ __forceinline__ void pin_args(const FoldArgs& a) {
+  if constexpr (NS == 8) {
+    asm volatile("" ::"s"(a.srcs[0]), "s"(a.srcs[1]), "s"(a.srcs[2]), "s"(a.srcs[3]),
+                 "s"(a.srcs[4]), "s"(a.srcs[5]), "s"(a.srcs[6]), "s"(a.srcs[7]), "s"(a.dst),
+                 "s"(a.g.nvec), "s"(a.g.vec_off), "s"(a.grid));
+  } else if constexpr (NS == 2) {
+    asm volatile("" ::"s"(a.srcs[0]), "s"(a.srcs[1]), "s"(a.dst), "s"(a.g.nvec),
+                 "s"(a.g.vec_off), "s"(a.grid));
+  } else if constexpr (NS == 16) {
+    asm volatile("" ::"s"(a.srcs[0]), "s"(a.srcs[1]), "s"(a.srcs[2]), "s"(a.srcs[3]),
+                 "s"(a.srcs[4]), "s"(a.srcs[5]), "s"(a.srcs[6]), "s"(a.srcs[7]),
+                 "s"(a.srcs[8]), "s"(a.srcs[9]), "s"(a.srcs[10]), "s"(a.srcs[11]),
+                 "s"(a.srcs[12]), "s"(a.srcs[13]), "s"(a.srcs[14]), "s"(a.srcs[15]),
+                 "s"(a.dst), "s"(a.g.nvec), "s"(a.g.vec_off), "s"(a.grid));
+  } else {
+    asm volatile("" ::"s"(a.dst), "s"(a.g.nvec), "s"(a.g.vec_off), "s"(a.grid));
+  }
+}
+
 template <class Op, int VPT, bool NT, int NS>
 __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
+  pin_args<NS>(a);
+  // decided at entry, while the arguments are in SGPRs (no reload after the loop)
+  const int elem_mode = a.g.nvec == 0 ? 2 : (blockIdx.x == a.grid - 1 ? 1 : 0);
+  // One tile per workgroup (the launcher sizes the grid to the tile count):
+  // workgroups are dispatched in tile order, so the chip sweeps every operand
+  // as one tight window (a persistent tile-stride loop measured 10-20 % slower).
   const uint64_t tile_vecs = (uint64_t)kBlock * VPT;
-  const uint64_t ntiles = (a.g.nvec + tile_vecs - 1) / tile_vecs;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
-    fold_tile<Op, VPT, NT, NS>(a.srcs, a.n, a.dst, a.g.vec_off, tile * tile_vecs, a.g.nvec,
-                               threadIdx.x);
-  fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0,
-                    (uint64_t)blockIdx.x * kBlock + threadIdx.x, (uint64_t)gridDim.x * kBlock);
+  const uint64_t tile = blockIdx.x;
+  if ((tile + 1) * tile_vecs <= a.g.nvec)
+    fold_tile_full_buf<Op, VPT, NT, NS>(a.srcs, a.n, a.dst, a.g.vec_off + tile * tile_vecs * 16,
+                                        threadIdx.x);
+  else if (tile * tile_vecs < a.g.nvec)
+    fold_tile_body<Op, VPT, NT, NS, true>(a.srcs, a.n, a.dst, a.g.vec_off, tile * tile_vecs,
+                                          a.g.nvec, threadIdx.x);
+  // Element work (unaligned head, tail, fp16 F16C tail, trailing bytes) is a
+  // handful of elements unless there is no vector range at all: give it to the
+  // last workgroup only, so no other workgroup pays the extra argument loads.
+  if (elem_mode == 2)
+    fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0,
+                      (uint64_t)blockIdx.x * kBlock + threadIdx.x, (uint64_t)a.grid * kBlock);
+  else if (elem_mode == 1)
+    fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0, threadIdx.x, kBlock);
 }
 
 // Batched: block b works on tile b of the concatenated tile space;
@@ -241,8 +343,10 @@ static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_
   static const hipError_t lds_ok =
       allow_full_lds(reinterpret_cast<const void*>(&fold_kernel<Op, VPT, NT, NS>));
   if (lds_ok != hipSuccess) return lds_ok;
-  hipLaunchKernelGGL((fold_kernel<Op, VPT, NT, NS>), dim3(fold_grid(a.g, tu, VPT)),
-                     dim3(kBlock), occ_lds_bytes(tu.occ), s, a);
+  FoldArgs b = a;
+  b.grid = (uint32_t)fold_grid(a.g, tu, VPT);   // the kernel strides by its own grid
+  hipLaunchKernelGGL((fold_kernel<Op, VPT, NT, NS>), dim3(b.grid), dim3(kBlock),
+                     occ_lds_bytes(tu.occ), s, b);
   return hipGetLastError();
 }
 

@@ -69,8 +69,11 @@ struct OpF32 {
     for (int i = 0; i < 4; ++i)
       a.w[i] = bitcast<uint32_t>(bitcast<float>(a.w[i]) + bitcast<float>(b.w[i]));
   }
-  __device__ static bool has_nan(const Acc& a) {
-    return f32_nan(a.w[0]) || f32_nan(a.w[1]) || f32_nan(a.w[2]) || f32_nan(a.w[3]);
+  __device__ static bool has_nan(const Acc& a) {  // one v_cmp_u_f32 per element
+    const float x0 = bitcast<float>(a.w[0]), x1 = bitcast<float>(a.w[1]);
+    const float x2 = bitcast<float>(a.w[2]), x3 = bitcast<float>(a.w[3]);
+    return __builtin_isnan(x0) || __builtin_isnan(x1) || __builtin_isnan(x2) ||
+           __builtin_isnan(x3);
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }

@@ -5,8 +5,11 @@
 //   * in-place output (dst = source 0, the server's zero-copy accumulator,
 //     server.cc:216-218) vs a separate output stream,
 //   * slab spacing (skew) between the 9 operands.
-//   hipcc -O3 --offload-arch=gfx950 -o tools/hbm_probe2 tools/hbm_probe2.hip
+//   hipcc -O3 --offload-arch=gfx950 -Iinclude -o tools/hbm_probe2 tools/hbm_probe2.hip \
+//         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd'   ("n8_product" = libbpsr)
 #include <hip/hip_runtime.h>
+
+#include "bpsr/reduce.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -106,6 +109,15 @@ __global__ __launch_bounds__(256) void fold_persist(Ops o, unsigned bytes_per_op
   }
 }
 
+__global__ void fill_random(unsigned* p, size_t n, unsigned seed) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    // finite fp32 in about [-2, 2]: random mantissa/sign, exponent 126..128
+    p[i] = (x & 0x807fffffu) | ((126u + (x >> 23) % 3u) << 23);
+  }
+}
+
 struct V {
   const char* name;
   void (*fn)(Ops, unsigned, int, hipStream_t);
@@ -123,6 +135,15 @@ static void P(Ops o, unsigned b, int grid, hipStream_t s) {
                      o, b, ntiles);
 }
 
+// The product kernel through the C ABI on the same operands.
+template <int NS>
+static void PROD(Ops o, unsigned b, int grid, hipStream_t s) {
+  (void)grid;
+  const void* srcs[NS];
+  for (int k = 0; k < NS; ++k) srcs[k] = o.p[k];
+  byteps_reduce_sum_n(o.p[NS], srcs, NS, b, BYTEPS_REDUCE_FLOAT32, 0, s);
+}
+
 int main(int argc, char** argv) {
   const size_t B = (size_t)(argc > 1 ? atol(argv[1]) : 256) << 20;
   const int sets = 3;
@@ -134,16 +155,10 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"n8", L<2, 2, 4, false, 8>},
       {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
+      {"n8_product", PROD<8>},
       {"n8_v1_wg2cu", L<2, 2, 1, false, 8, false, 80>},
-      {"n8_persist_v2_g1", P<2, 8, 1, 160>},
-      {"n8_persist_v1_g1", P<1, 8, 1, 160>},
-      {"n8_persist_v4_g1", P<4, 8, 1, 160>},
-      {"n8_persist_v1_g2", P<1, 8, 2, 80>},
-      {"n8_persist_v2_g2", P<2, 8, 2, 80>},
-      {"n8_persist_v2_g1nolds", P<2, 8, 1, 0>},
-      {"n8_persist_v1_g4", P<1, 8, 4, 40>},
-      {"n16_persist_v1_g1", P<1, 16, 1, 160>},
-      {"n16_persist_v2_g1", P<2, 16, 1, 160>},
+      {"n8_v4_wg1cu", L<2, 2, 4, false, 8, false, 160>},
+      {"n1_copy", L<2, 2, 4, false, 1>},
       {"n16_v2_wg1cu", L<2, 2, 2, false, 16, false, 160>},
   };
   const size_t skews[] = {16384};
@@ -153,7 +168,13 @@ int main(int argc, char** argv) {
       std::vector<char*> slab(sets);
       for (int s = 0; s < sets; ++s) {
         CK(hipMalloc(&slab[s], 17 * stride));
-        CK(hipMemset(slab[s], 0, 17 * stride));
+        if (getenv("PROBE_ZERO")) {
+          CK(hipMemset(slab[s], 0, 17 * stride));
+        } else {
+          hipLaunchKernelGGL(fill_random, dim3(4096), dim3(256), 0, 0, (unsigned*)slab[s],
+                             17 * stride / 4, 77u + s);
+          CK(hipDeviceSynchronize());
+        }
       }
       for (const V& v : vs) {
         float best = 1e30f;
