@@ -148,7 +148,7 @@ int byteps_reduce_dtype_size(int dtype);
 const char* byteps_reduce_last_error(void);
 
 /* Launch tuning (process-wide; defaults chosen from measurements, see
- * DESIGN.md §4.1).  vpt: 16-B vectors per thread per tile (1, 2, 4 or 8);
+ * DESIGN.md §4.1).  vpt: 16-B vectors per thread per tile (1, 2 or 4);
  * nt: non-temporal loads and stores (0/1); max_grid: grid cap in 256-thread
  * workgroups (tile-stride beyond); occ: workgroups resident per CU, enforced
  * through the dynamic LDS request (0 = hardware limit, 1..8).  A value <= 0

@@ -86,7 +86,7 @@ static Tuning& tuning() {
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
     if (const char* v = getenv("BPSR_OCC")) t.occ = atoi(v);
-    if (t.vpt != 1 && t.vpt != 4 && t.vpt != 8) t.vpt = 2;
+    if (t.vpt != 1 && t.vpt != 4) t.vpt = 2;
     if (t.occ < 0 || t.occ > 8) t.occ = 1;
     if (t.max_grid < 1) t.max_grid = 1 << 20;
     t.nt = t.nt ? 1 : 0;
@@ -266,8 +266,8 @@ const char* byteps_reduce_last_error(void) { return g_last_error.c_str(); }
 int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ) {
   Tuning& t = tuning();
   if (vpt > 0) {
-    if (vpt != 1 && vpt != 2 && vpt != 4 && vpt != 8)
-      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2, 4 or 8");
+    if (vpt != 1 && vpt != 2 && vpt != 4)
+      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2 or 4");
     t.vpt = vpt;
   }
   if (occ > 8) return fail(BYTEPS_REDUCE_EARGS, "occ must be 0..8");

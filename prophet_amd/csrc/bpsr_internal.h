@@ -55,7 +55,7 @@ struct BatchEntry {
 };
 
 struct Tuning {
-  int vpt;       // 16-B vectors per thread per tile (1, 2, 4, 8)
+  int vpt;       // 16-B vectors per thread per tile (1, 2, 4)
   int nt;        // non-temporal loads and stores
   int max_grid;  // grid cap in workgroups (tile-stride beyond)
   int occ;       // workgroups resident per CU (0 = hardware limit), set through LDS

@@ -367,14 +367,12 @@ static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_
     switch (vpt) {
       case 1: return launch_fold_vpt<Op, 1, true>(a, tu, s);
       case 4: return launch_fold_vpt<Op, 4, true>(a, tu, s);
-      case 8: return launch_fold_vpt<Op, 8, true>(a, tu, s);
       default: return launch_fold_vpt<Op, 2, true>(a, tu, s);
     }
   }
   switch (vpt) {
     case 1: return launch_fold_vpt<Op, 1, false>(a, tu, s);
     case 4: return launch_fold_vpt<Op, 4, false>(a, tu, s);
-    case 8: return launch_fold_vpt<Op, 8, false>(a, tu, s);
     default: return launch_fold_vpt<Op, 2, false>(a, tu, s);
   }
 }

@@ -75,8 +75,8 @@ def test_argument_errors_without_gpu():
 def test_tuning_roundtrip():
     r = reducer.GpuReducer()
     old = r.get_tuning()
-    r.set_tuning(8, 0, 512, 3)
-    assert r.get_tuning() == (8, 0, 512, 3)
+    r.set_tuning(4, 0, 512, 3)
+    assert r.get_tuning() == (4, 0, 512, 3)
     with pytest.raises(reducer.ReduceError):
         r.set_tuning(3)
     with pytest.raises(reducer.ReduceError):
