@@ -81,11 +81,15 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 
 static Tuning& tuning() {
   static Tuning tu = [] {
-    Tuning t{2, 1, 1 << 20, 1};  // tools/sweep.py, profiles/r01_sweep_*.jsonl
+    Tuning t{2, 1, 1 << 20, 1, 2, 0};  // tools/sweep.py, tools/occ_sweep.py (profiles/)
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
     if (const char* v = getenv("BPSR_OCC")) t.occ = atoi(v);
+    if (const char* v = getenv("BPSR_SMALL_OCC")) t.small_occ = atoi(v);
+    if (const char* v = getenv("BPSR_SMALL_OCC_BATCH")) t.small_occ_batch = atoi(v);
+    if (t.small_occ < 0 || t.small_occ > 8) t.small_occ = 2;
+    if (t.small_occ_batch < 0 || t.small_occ_batch > 8) t.small_occ_batch = 0;
     if (t.vpt != 1 && t.vpt != 4) t.vpt = 2;
     if (t.occ < 0 || t.occ > 8) t.occ = 1;
     if (t.max_grid < 1) t.max_grid = 1 << 20;

@@ -59,6 +59,8 @@ struct Tuning {
   int nt;        // non-temporal loads and stores
   int max_grid;  // grid cap in workgroups (tile-stride beyond)
   int occ;       // workgroups resident per CU (0 = hardware limit), set through LDS
+  int small_occ;        // residency for short fold launches (occ == 1 only)
+  int small_occ_batch;  // residency for short batched launches (occ == 1 only)
 };
 
 // Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so
@@ -68,6 +70,14 @@ struct Tuning {
 constexpr size_t kLdsPerCU = 160 * 1024;
 inline size_t occ_lds_bytes(int occ) {
   return occ > 0 ? (kLdsPerCU / (size_t)occ) & ~(size_t)255 : 0;
+}
+// The 1-workgroup-per-CU cap pays on long sweeps only: below kOccMinTiles
+// tiles (16 MiB per source at vpt 2) a launch is latency-bound and more
+// residency wins (profiles/r01_occ_sweep.jsonl).
+constexpr uint64_t kOccMinTiles = 2048;
+inline int launch_occ(const Tuning& tu, uint64_t tiles, bool batched) {
+  if (tu.occ != 1 || tiles >= kOccMinTiles) return tu.occ;
+  return batched ? tu.small_occ_batch : tu.small_occ;
 }
 // Allow `kernel` to request up to 160 KiB of dynamic LDS (once per kernel).
 hipError_t allow_full_lds(const void* kernel);

@@ -346,7 +346,7 @@ static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_
   FoldArgs b = a;
   b.grid = (uint32_t)fold_grid(a.g, tu, VPT);   // the kernel strides by its own grid
   hipLaunchKernelGGL((fold_kernel<Op, VPT, NT, NS>), dim3(b.grid), dim3(kBlock),
-                     occ_lds_bytes(tu.occ), s, b);
+                     occ_lds_bytes(launch_occ(tu, b.grid, false)), s, b);
   return hipGetLastError();
 }
 
@@ -388,7 +388,7 @@ static hipError_t launch_batched_vpt(const BatchEntry* tab, const uint32_t* tile
       allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
   if (ok_nt != hipSuccess) return ok_nt;
   if (ok_t != hipSuccess) return ok_t;
-  const size_t lds = occ_lds_bytes(tu.occ);
+  const size_t lds = occ_lds_bytes(launch_occ(tu, ntiles, true));
   if (tu.nt)
     hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(grid), dim3(kBlock), lds, s, tab,
                        tile_bucket, nbuckets, ntiles);

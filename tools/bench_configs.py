@@ -150,12 +150,41 @@ def cfg3(red, dev, N=8, sets=3):
     def per_block_graph4(i):
         graphs4[i % sets].replay()
 
+    # Release groups from the Prophet PUSH-queue simulator (scheduled_queue.cc:
+    # 217-296) at batch 64 and Z_NET_B = 10000 (10 Gb/s in Mb/s), credit 16 MiB:
+    # one plan per group, the whole iteration captured in one graph.
+    from prophet_amd.prophet import ProphetPushQueue, backward_arrivals, model_checkpoints, \
+        release_groups
+    q = ProphetPushQueue(batch_size=64, net_b=10000, credit=16 << 20,
+                         checkpoints=model_checkpoints(len(sizes)))
+    rgroups = release_groups(q, backward_arrivals(sizes))
+    pmap = {(p.tensor, p.part): p for p in parts}
+    rplans = [[red.make_plan([(*views(i, pmap[(t.grad, t.part)]), t.len) for t in g],
+                             DType.FLOAT16) for g in rgroups] for i in range(sets)]
+    rgraphs = []
+    for i in range(sets):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(s)
+        with torch.cuda.stream(side):
+            for pl in rplans[i]:
+                pl.launch(side)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            for pl in rplans[i]:
+                pl.launch(side)
+        rgraphs.append(g)
+
+    def release_group_graph(i):
+        rgraphs[i % sets].replay()
+
     for name, fn in (("per_partition_launch", per_partition), ("prophet_block_batched", per_block),
                      ("single_batched_launch", all_in_one),
                      ("prophet_block_plans", per_block_plan),
                      ("prophet_block_plans_hipgraph", per_block_graph),
                      ("prophet_block_plans_4streams", per_block_plans_4streams),
-                     ("prophet_block_plans_4streams_hipgraph", per_block_graph4)):
+                     ("prophet_block_plans_4streams_hipgraph", per_block_graph4),
+                     ("prophet_release_groups_hipgraph", release_group_graph)):
         med, mn = timed(fn, 10, s)
         w, out, _ = data[0]
         fn(0)

@@ -3,7 +3,7 @@
 # trace.  Each GPU step has its own time limit; the script stops at the first
 # step that ends in anything other than success or an ordinary test failure
 # (fault, abort, segfault, timeout).  Output: gpurun_out/<tag>/...
-#   usage: tools/gpu_round.sh <tag> [steps...]   steps: test smoke bench sweep prof pmc
+#   usage: tools/gpu_round.sh <tag> [steps...]   steps: test smoke bench sweep prof pmc occ cfg3 configs
 set -u
 TAG=${1:-r01}; shift || true
 STEPS=${*:-"test smoke bench sweep prof"}
@@ -35,6 +35,9 @@ for s in $STEPS; do
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     pmc)   run pmc 900 python tools/pmc_traffic.py --out "$OUT/pmc" ;;
+    occ)   run occ 600 python tools/occ_sweep.py ;;
+    cfg3)  run cfg3 600 python tools/bench_configs.py --only cfg3,sweep ;;
+    configs) run configs 900 python tools/bench_configs.py ;;
     *) echo "unknown step $s" ;;
   esac
 done
