@@ -189,20 +189,26 @@ static int stage_acquire(size_t bytes, StageSlot** out) {
 
 // ------------------------------------------------------- batch table build --
 struct TableInfo {
-  int vpt = kBatchVPT;   // tile size of the batched kernel for this table
+  int vpt = 1;   // tile size of the batched kernel for this table
   int live = 0;          // buckets with len > 0
-  uint32_t tiles = 0;    // total tiles
-  size_t map_off = 0;    // byte offset of tile_bucket[] in the table
+  uint32_t tiles = 0;    // workgroups (element tiles first, then vector tiles)
+  uint32_t rec_stride = 0;
+  size_t recs_off = 0;   // byte offset of the tile records in the table
   size_t bytes = 0;      // bytes to upload
 };
 
-// Validate buckets and write [BatchEntry x live][pad to 256][tile_bucket x tiles]
-// into `out`.  Every live bucket gets >= 1 tile so its element work runs.
+// Element work of one bucket (head, tail, trailing bytes) in parts of
+// kElemPart elements per workgroup.
+constexpr uint64_t kElemPart = (uint64_t)kBlock * 16;
+
+// Validate buckets and write [BatchEntry x live][pad to 256][TileRec x tiles]
+// into `out` (bpsr_internal.h: TileHead).
 static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
                        std::vector<char>& out, TableInfo* ti) {
   std::vector<BatchEntry> tab;
   tab.reserve(nbuckets);
   uint64_t vecs = 0;
+  int nmax = 1;
   for (int i = 0; i < nbuckets; ++i) {
     const byteps_bucket_desc& b = buckets[i];
     if (b.n < 1 || b.n > kMaxSrcs)
@@ -221,33 +227,75 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
     e.n = b.n;
     make_geom(dtype, b.len, b.dst, b.srcs, b.n, b.dst != b.srcs[0], &e.g, &e.aligned);
     vecs += e.g.nvec;
+    nmax = std::max(nmax, b.n);
     tab.push_back(e);
   }
-  // Small batches (a Prophet block of a few MiB) get 256-vector tiles so the
-  // launch still has >= kMinTiles workgroups to spread over 256 CUs.
-  const int vpt = vecs / ((uint64_t)kBlock * kBatchVPT) >= kMinTiles ? kBatchVPT : 1;
+  // Same tile-size rule as a single fold (fold_vpt): the tuned vpt, halved
+  // while the launch would have fewer than kMinTiles tiles.
+  const int vpt = fold_vpt(vecs, tuning().vpt);
   const uint64_t tile_vecs = (uint64_t)kBlock * vpt;
+  auto elem_parts = [](const BatchEntry& e) -> uint64_t {
+    const uint64_t n_scalar = e.g.head_elems + (e.g.n_elems - e.g.tail_begin);
+    const bool trailing = e.g.copy_trailing && e.g.trailing_bytes > 0;
+    if (n_scalar == 0 && !trailing) return 0;
+    const uint64_t p = (n_scalar + kElemPart - 1) / kElemPart;
+    return std::min<uint64_t>(std::max<uint64_t>(p, 1), 65536);
+  };
   uint64_t tiles = 0;
-  for (auto& e : tab) {
-    e.first_tile = (uint32_t)tiles;
-    const uint64_t t = (e.g.nvec + tile_vecs - 1) / tile_vecs;
-    tiles += t ? t : 1;
-    if (tiles > 0xffffffffull) return fail(BYTEPS_REDUCE_EARGS, "batch too large");
-  }
-  const size_t map_off = ((sizeof(BatchEntry) * tab.size()) + 255) & ~(size_t)255;
-  out.assign(map_off + sizeof(uint32_t) * (size_t)tiles, 0);
+  for (auto& e : tab) tiles += elem_parts(e) + (e.g.nvec + tile_vecs - 1) / tile_vecs;
+  // grid.x * 256 threads must stay below 2^32
+  if (tiles >= (1ull << 32) / kBlock) return fail(BYTEPS_REDUCE_EARGS, "batch too large");
+  const uint32_t stride = tile_rec_stride(nmax);
+  const size_t recs_off = ((sizeof(BatchEntry) * tab.size()) + 255) & ~(size_t)255;
+  out.assign(recs_off + (size_t)stride * tiles, 0);
   if (!tab.empty()) std::memcpy(out.data(), tab.data(), sizeof(BatchEntry) * tab.size());
-  uint32_t* map = reinterpret_cast<uint32_t*>(out.data() + map_off);
+  char* rec = out.data() + recs_off;
+  auto put = [&](unsigned char* dst, uint32_t kind, const BatchEntry& e, uint32_t a, uint32_t b,
+                 uint32_t c, uint64_t byte0) {
+    TileHead h;
+    std::memset(&h, 0, sizeof(h));
+    h.dst = dst + byte0;
+    h.kind = kind;
+    h.n = (uint32_t)e.n;
+    h.a = a;
+    h.b = b;
+    h.c = c;
+    std::memcpy(rec, &h, sizeof(h));
+    const unsigned char** p = reinterpret_cast<const unsigned char**>(rec + kTileHeadBytes);
+    for (int k = 0; k < e.n; ++k) p[k] = e.srcs[k] + byte0;
+    rec += stride;
+  };
+  // element tiles first: they are latency-bound and start with the launch
   for (size_t b = 0; b < tab.size(); ++b) {
-    const uint32_t end = b + 1 < tab.size() ? tab[b + 1].first_tile : (uint32_t)tiles;
-    for (uint32_t t = tab[b].first_tile; t < end; ++t) map[t] = (uint32_t)b;
+    const uint64_t parts = elem_parts(tab[b]);
+    for (uint64_t q = 0; q < parts; ++q)
+      put(tab[b].dst, kTileElem, tab[b], (uint32_t)q, (uint32_t)b, (uint32_t)parts, 0);
+  }
+  for (size_t b = 0; b < tab.size(); ++b) {
+    const BatchEntry& e = tab[b];
+    for (uint64_t v0 = 0; v0 < e.g.nvec; v0 += tile_vecs) {
+      const uint64_t left = e.g.nvec - v0;
+      const bool full = left >= tile_vecs;
+      put(e.dst, full ? kTileFull : kTilePartial, e, full ? 0u : (uint32_t)left, (uint32_t)b, 0,
+          e.g.vec_off + v0 * 16);
+    }
   }
   ti->vpt = vpt;
   ti->live = (int)tab.size();
   ti->tiles = (uint32_t)tiles;
-  ti->map_off = map_off;
+  ti->rec_stride = stride;
+  ti->recs_off = recs_off;
   ti->bytes = out.size();
   return BYTEPS_REDUCE_OK;
+}
+
+static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti) {
+  BatchLaunch L;
+  L.entries = static_cast<const BatchEntry*>(dev_table);
+  L.recs = static_cast<const unsigned char*>(dev_table) + ti.recs_off;
+  L.rec_stride = ti.rec_stride;
+  L.tiles = ti.tiles;
+  return L;
 }
 
 static thread_local std::vector<char> g_table;
@@ -373,16 +421,14 @@ int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets, i
   if (nbuckets == 0) return BYTEPS_REDUCE_OK;
   TableInfo ti;
   if ((rc = build_table(buckets, nbuckets, dtype, g_table, &ti))) return rc;
-  if (ti.live == 0) return BYTEPS_REDUCE_OK;
+  if (ti.tiles == 0) return BYTEPS_REDUCE_OK;
   StageSlot* slot = nullptr;
   if ((rc = stage_acquire(ti.bytes, &slot))) return rc;
   std::memcpy(slot->host, g_table.data(), ti.bytes);
   hipStream_t s = to_stream(stream);
   hipError_t e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
-  e = launch_batched(static_cast<const BatchEntry*>(slot->dev),
-                     reinterpret_cast<const uint32_t*>(static_cast<char*>(slot->dev) + ti.map_off),
-                     ti.live, ti.tiles, ti.vpt, dtype, mode, tuning(), s);
+  e = launch_batched(batch_launch(slot->dev, ti), ti.vpt, dtype, mode, tuning(), s);
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
   e = hipEventRecord(slot->done, s);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
@@ -415,7 +461,7 @@ int byteps_reduce_plan_create(const byteps_bucket_desc* buckets, int nbuckets, i
   p->ti = ti;
   p->dev_table = nullptr;
   hipError_t e = hipGetDevice(&p->device);
-  if (e == hipSuccess && ti.live > 0) {
+  if (e == hipSuccess && ti.tiles > 0) {
     e = hipMalloc(&p->dev_table, ti.bytes);
     if (e == hipSuccess)
       e = hipMemcpy(p->dev_table, host.data(), ti.bytes, hipMemcpyHostToDevice);
@@ -431,11 +477,9 @@ int byteps_reduce_plan_create(const byteps_bucket_desc* buckets, int nbuckets, i
 
 int byteps_reduce_plan_launch(byteps_reduce_plan* p, void* stream) {
   if (!p) return fail(BYTEPS_REDUCE_EARGS, "null plan");
-  if (p->ti.live == 0) return BYTEPS_REDUCE_OK;
-  hipError_t e = launch_batched(
-      static_cast<const BatchEntry*>(p->dev_table),
-      reinterpret_cast<const uint32_t*>(static_cast<char*>(p->dev_table) + p->ti.map_off),
-      p->ti.live, p->ti.tiles, p->ti.vpt, p->dtype, p->mode, tuning(), to_stream(stream));
+  if (p->ti.tiles == 0) return BYTEPS_REDUCE_OK;
+  hipError_t e = launch_batched(batch_launch(p->dev_table, p->ti), p->ti.vpt, p->dtype, p->mode,
+                                tuning(), to_stream(stream));
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "plan kernel launch");
 }
 

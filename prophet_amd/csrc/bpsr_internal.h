@@ -16,7 +16,6 @@ enum : int { kModeReference = 0, kModeAccumF32 = 1 };
 
 constexpr int kBlock = 256;     // 4 waves of 64
 constexpr int kMaxSrcs = 32;    // BYTEPS_REDUCE_MAX_SRCS
-constexpr int kBatchVPT = 4;    // vectors per thread per tile in the batched kernel (large batches)
 // Fewer tiles than this leave CUs idle (256 CUs, several workgroups each):
 // launches that would get fewer fall back to smaller tiles.
 constexpr uint64_t kMinTiles = 2048;
@@ -44,14 +43,43 @@ struct FoldArgs {
   uint64_t grid;  // launched workgroups (set by the launcher)
 };
 
+// Per-bucket geometry of a batched launch (read by element tiles only).
 struct BatchEntry {
   const unsigned char* srcs[kMaxSrcs];
   unsigned char* dst;
   int n;
   int aligned;
   FoldGeom g;
-  uint32_t first_tile;  // index of the bucket's first tile in the launch
+};
+
+// One record per workgroup of a batched launch, rec_stride bytes apart: a
+// 32-B head followed by the n source pointers.  Vector tiles carry pointers
+// already advanced to the tile's first byte, so a workgroup reaches its data
+// after ONE scalar round trip (head + pointers) instead of map -> bucket ->
+// data.  Element tiles (unaligned head, tail, trailing bytes) are separate
+// workgroups at the front of the launch, so that latency-bound work runs
+// beside the vector tiles rather than after them.
+enum : uint32_t { kTileFull = 0, kTilePartial = 1, kTileElem = 2 };
+struct TileHead {
+  unsigned char* dst;  // vector tiles: dst + the tile's first byte
+  uint32_t kind;
+  uint32_t n;          // sources
+  uint32_t a;          // partial: valid vectors; element: part index
+  uint32_t b;          // element: bucket index into the BatchEntry table
+  uint32_t c;          // element: parts of this bucket's element work
   uint32_t pad;
+};
+constexpr uint32_t kTileHeadBytes = 32;
+static_assert(sizeof(TileHead) == kTileHeadBytes, "TileHead layout");
+// Record stride: room for max(8, nmax) pointers (the kernel reads 8 at entry).
+inline uint32_t tile_rec_stride(int nmax) {
+  return (kTileHeadBytes + 8u * (uint32_t)(nmax < 8 ? 8 : nmax) + 31u) & ~31u;
+}
+struct BatchLaunch {
+  const unsigned char* recs;    // tiles records
+  const BatchEntry* entries;    // per-bucket geometry
+  uint32_t rec_stride;
+  uint32_t tiles;
 };
 
 struct Tuning {
@@ -110,8 +138,8 @@ inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
 
 #define BPSR_DECLARE_LAUNCHERS(NAME)                                                      \
   hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s);      \
-  hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
-                                   uint32_t nt, int vpt, const Tuning& tu, hipStream_t s);
+  hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
+                                   hipStream_t s);
 BPSR_DECLARE_LAUNCHERS(f32)
 BPSR_DECLARE_LAUNCHERS(f64)
 BPSR_DECLARE_LAUNCHERS(f16)
@@ -124,8 +152,7 @@ BPSR_DECLARE_LAUNCHERS(i64)
 
 hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);
-hipError_t launch_batched(const BatchEntry* tab, const uint32_t* tile_bucket, int nbuckets,
-                          uint32_t ntiles, int vpt, int dtype, int mode, const Tuning& tu,
+hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, const Tuning& tu,
                           hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the

@@ -91,22 +91,20 @@ hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
   }
 }
 
-hipError_t launch_batched(const BatchEntry* tab, const uint32_t* ts, int nb, uint32_t nt,
-                          int vpt, int dtype, int mode, const Tuning& tu, hipStream_t s) {
+hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, const Tuning& tu,
+                          hipStream_t s) {
   const bool acc = mode == kModeAccumF32;
   switch (dtype) {
-    case kFloat32: return launch_batched_f32(tab, ts, nb, nt, vpt, tu, s);
-    case kFloat64: return launch_batched_f64(tab, ts, nb, nt, vpt, tu, s);
+    case kFloat32: return launch_batched_f32(L, vpt, tu, s);
+    case kFloat64: return launch_batched_f64(L, vpt, tu, s);
     case kFloat16:
-      return acc ? launch_batched_f16acc(tab, ts, nb, nt, vpt, tu, s)
-                 : launch_batched_f16(tab, ts, nb, nt, vpt, tu, s);
+      return acc ? launch_batched_f16acc(L, vpt, tu, s) : launch_batched_f16(L, vpt, tu, s);
     case kBFloat16:
-      return acc ? launch_batched_bf16acc(tab, ts, nb, nt, vpt, tu, s)
-                 : launch_batched_bf16(tab, ts, nb, nt, vpt, tu, s);
+      return acc ? launch_batched_bf16acc(L, vpt, tu, s) : launch_batched_bf16(L, vpt, tu, s);
     case kUInt8:
-    case kInt8: return launch_batched_i8(tab, ts, nb, nt, vpt, tu, s);
-    case kInt32: return launch_batched_i32(tab, ts, nb, nt, vpt, tu, s);
-    case kInt64: return launch_batched_i64(tab, ts, nb, nt, vpt, tu, s);
+    case kInt8: return launch_batched_i8(L, vpt, tu, s);
+    case kInt32: return launch_batched_i32(L, vpt, tu, s);
+    case kInt64: return launch_batched_i64(L, vpt, tu, s);
     default: return hipErrorInvalidValue;
   }
 }

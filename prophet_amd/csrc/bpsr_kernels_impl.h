@@ -99,14 +99,20 @@ __device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* s
 // vector decides whether the exact NaN-payload rule must be replayed
 // (fold_vector_exact) — a wave-uniform branch never taken on finite data.
 // GUARD: the last, partial tile (vectors past nvec are neither read nor written).
+// NS > 0: exactly NS sources; NS < 0: at most -NS (<= 8) sources, n at run
+// time, one load group with compile-time indices (so `srcs` may be a register
+// array); NS == 0: any n.  `xsrcs` (memory) serves the exact NaN replay.
 template <class Op, int VPT, bool NT, int NS, bool GUARD>
-__device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs, int n,
+__device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
+                                               const unsigned char* const* xsrcs, int n,
                                                unsigned char* dst, uint64_t vec_off,
                                                uint64_t v0, uint64_t nvec, int lane) {
+  constexpr int NSA = NS < 0 ? -NS : NS;
   const int ns = NS > 0 ? NS : n;
   const uint64_t off0 = vec_off + (v0 + lane) * 16;
   constexpr uint64_t kStep = (uint64_t)kBlock * 16;
-  constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
+  constexpr int G = NSA > 0 ? cmin(NSA, 32 / VPT) : cmin(8, 32 / VPT);
+  static_assert(NS >= 0 || G == NSA, "NS < 0 needs one load group");
   bool valid[VPT];
 #pragma unroll
   for (int j = 0; j < VPT; ++j) valid[j] = !GUARD || (v0 + lane + (uint64_t)j * kBlock < nvec);
@@ -133,9 +139,9 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
       }
     }
   };
-  if constexpr (NS > 0) {
+  if constexpr (NSA > 0) {
 #pragma unroll
-    for (int k0 = 0; k0 < NS; k0 += G) group(k0);
+    for (int k0 = 0; k0 < NSA; k0 += G) group(k0);
   } else {
     for (int k0 = 0; k0 < ns; k0 += G) group(k0);
   }
@@ -147,7 +153,7 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
     vec16 out = Op::finish(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (valid[j] && Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, NT>(srcs, ns, off0 + j * kStep);
+        out = fold_vector_exact<Op, NT>(xsrcs, ns, off0 + j * kStep);
     }
     if (valid[j]) st16<NT>(dst + off0 + j * kStep, out);
   }
@@ -158,11 +164,14 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
 // 32-bit lane offsets, nt as the cache-policy operand.  Same load grouping,
 // fast fold and NaN replay as fold_tile_body.
 template <class Op, int VPT, bool NT, int NS>
-__device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs, int n,
+__device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs,
+                                                   const unsigned char* const* xsrcs, int n,
                                                    unsigned char* dst, uint64_t byte0, int lane) {
   constexpr int kAux = NT ? 2 : 0;               // 2 = nt
   constexpr int kTileBytes = kBlock * VPT * 16;
-  constexpr int G = NS > 0 ? cmin(NS, 32 / VPT) : cmin(8, 32 / VPT);
+  constexpr int NSA = NS < 0 ? -NS : NS;
+  constexpr int G = NSA > 0 ? cmin(NSA, 32 / VPT) : cmin(8, 32 / VPT);
+  static_assert(NS >= 0 || G == NSA, "NS < 0 needs one load group");
   const int ns = NS > 0 ? NS : n;
   const int voff = lane * 16;
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
@@ -194,9 +203,9 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
       }
     }
   };
-  if constexpr (NS > 0) {
+  if constexpr (NSA > 0) {
 #pragma unroll
-    for (int k0 = 0; k0 < NS; k0 += G) group(k0);
+    for (int k0 = 0; k0 < NSA; k0 += G) group(k0);
   } else {
     for (int k0 = 0; k0 < ns; k0 += G) group(k0);
   }
@@ -209,7 +218,7 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
     vec16 out = Op::finish(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, NT>(srcs, ns, byte0 + voff + j * kBlock * 16);
+        out = fold_vector_exact<Op, NT>(xsrcs, ns, byte0 + voff + j * kBlock * 16);
     }
     __builtin_amdgcn_raw_buffer_store_b128(bitcast<u4>(out), rd, voff + j * kBlock * 16, 0, kAux);
   }
@@ -220,9 +229,9 @@ __device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int 
                                           unsigned char* dst, uint64_t vec_off, uint64_t v0,
                                           uint64_t nvec, int lane) {
   if (v0 + (uint64_t)kBlock * VPT <= nvec)
-    fold_tile_full_buf<Op, VPT, NT, NS>(srcs, n, dst, vec_off + v0 * 16, lane);
+    fold_tile_full_buf<Op, VPT, NT, NS>(srcs, srcs, n, dst, vec_off + v0 * 16, lane);
   else
-    fold_tile_body<Op, VPT, NT, NS, true>(srcs, n, dst, vec_off, v0, nvec, lane);
+    fold_tile_body<Op, VPT, NT, NS, true>(srcs, srcs, n, dst, vec_off, v0, nvec, lane);
 }
 
 // Element part: elements [0, head) and [tail_begin, n_elems) plus trailing
@@ -301,11 +310,11 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
   const uint64_t tile_vecs = (uint64_t)kBlock * VPT;
   const uint64_t tile = blockIdx.x;
   if ((tile + 1) * tile_vecs <= a.g.nvec)
-    fold_tile_full_buf<Op, VPT, NT, NS>(a.srcs, a.n, a.dst, a.g.vec_off + tile * tile_vecs * 16,
-                                        threadIdx.x);
+    fold_tile_full_buf<Op, VPT, NT, NS>(a.srcs, a.srcs, a.n, a.dst,
+                                        a.g.vec_off + tile * tile_vecs * 16, threadIdx.x);
   else if (tile * tile_vecs < a.g.nvec)
-    fold_tile_body<Op, VPT, NT, NS, true>(a.srcs, a.n, a.dst, a.g.vec_off, tile * tile_vecs,
-                                          a.g.nvec, threadIdx.x);
+    fold_tile_body<Op, VPT, NT, NS, true>(a.srcs, a.srcs, a.n, a.dst, a.g.vec_off,
+                                          tile * tile_vecs, a.g.nvec, threadIdx.x);
   // Element work (unaligned head, tail, fp16 F16C tail, trailing bytes) is a
   // handful of elements unless there is no vector range at all: give it to the
   // last workgroup only, so no other workgroup pays the extra argument loads.
@@ -316,23 +325,40 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
     fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0, threadIdx.x, kBlock);
 }
 
-// Batched: block b works on tile b of the concatenated tile space;
-// tile_bucket[tile] names the bucket (one load instead of a binary search:
-// the dependent-load chain is what a small block's launch waits on), and
-// tile - first_tile is the tile's index inside it.  The element work of a
-// bucket is done by its first tile.
+// Batched: workgroup b runs record b of the launch (TileHead, bpsr_internal.h).
+// Its head and first 8 source pointers are pinned into SGPRs by one empty asm,
+// so they arrive in one scalar round trip; vector tiles then go straight to
+// their data (pointers pre-advanced to the tile).  Element tiles fetch their
+// bucket's geometry from the entry table and stride over its element work.
 template <class Op, int VPT, bool NT>
-__global__ __launch_bounds__(kBlock) void batched_kernel(const BatchEntry* __restrict__ tab,
-                                                         const uint32_t* __restrict__ tile_bucket,
-                                                         int nbuckets, uint32_t ntiles) {
-  (void)nbuckets;
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const BatchEntry& e = tab[tile_bucket[tile]];
-    const uint32_t local = tile - e.first_tile;
-    fold_tile<Op, VPT, NT, 0>(e.srcs, e.n, e.dst, e.g.vec_off,
-                              (uint64_t)local * kBlock * VPT, e.g.nvec, threadIdx.x);
-    if (local == 0)
-      fold_elements<Op>(e.srcs, e.n, e.dst, e.g, e.aligned != 0, threadIdx.x, kBlock);
+__global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
+  const unsigned char* rec = L.recs + (uint64_t)blockIdx.x * L.rec_stride;
+  const TileHead& h = *reinterpret_cast<const TileHead*>(rec);
+  const unsigned char* const* msrcs =
+      reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes);
+  // Read the head and 8 pointers into registers before anything else (scalar
+  // loads: nothing has been stored yet), then pin them so they issue together.
+  unsigned char* const dst = h.dst;
+  const uint32_t kind = h.kind, n = h.n, a = h.a, b = h.b, c = h.c;
+  const unsigned char* p[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) p[k] = msrcs[k];
+  asm volatile("" ::"s"(dst), "s"(kind), "s"(n), "s"(a), "s"(p[0]), "s"(p[1]), "s"(p[2]),
+               "s"(p[3]), "s"(p[4]), "s"(p[5]), "s"(p[6]), "s"(p[7]));
+  if (kind == kTileElem) {
+    const BatchEntry& e = L.entries[b];
+    fold_elements<Op>(e.srcs, e.n, e.dst, e.g, e.aligned != 0,
+                      (uint64_t)a * kBlock + threadIdx.x, (uint64_t)c * kBlock);
+  } else if (n <= 8) {
+    if (kind == kTileFull)
+      fold_tile_full_buf<Op, VPT, NT, -8>(p, msrcs, (int)n, dst, 0, threadIdx.x);
+    else
+      fold_tile_body<Op, VPT, NT, -8, true>(p, msrcs, (int)n, dst, 0, 0, a, threadIdx.x);
+  } else {
+    if (kind == kTileFull)
+      fold_tile_full_buf<Op, VPT, NT, 0>(msrcs, msrcs, (int)n, dst, 0, threadIdx.x);
+    else
+      fold_tile_body<Op, VPT, NT, 0, true>(msrcs, msrcs, (int)n, dst, 0, 0, a, threadIdx.x);
   }
 }
 
@@ -378,32 +404,30 @@ static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_
 }
 
 template <class Op, int VPT>
-static hipError_t launch_batched_vpt(const BatchEntry* tab, const uint32_t* tile_bucket,
-                                     int nbuckets, uint32_t ntiles, const Tuning& tu,
-                                     hipStream_t s) {
-  const uint32_t grid = ntiles < (uint32_t)tu.max_grid ? ntiles : (uint32_t)tu.max_grid;
+static hipError_t launch_batched_vpt(const BatchLaunch& L, const Tuning& tu, hipStream_t s) {
   static const hipError_t ok_nt =
       allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, true>));
   static const hipError_t ok_t =
       allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
   if (ok_nt != hipSuccess) return ok_nt;
   if (ok_t != hipSuccess) return ok_t;
-  const size_t lds = occ_lds_bytes(launch_occ(tu, ntiles, true));
+  if (L.tiles == 0) return hipSuccess;
+  const size_t lds = occ_lds_bytes(launch_occ(tu, L.tiles, true));
   if (tu.nt)
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(grid), dim3(kBlock), lds, s, tab,
-                       tile_bucket, nbuckets, ntiles);
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(L.tiles), dim3(kBlock), lds, s, L);
   else
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(grid), dim3(kBlock), lds, s, tab,
-                       tile_bucket, nbuckets, ntiles);
+    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(L.tiles), dim3(kBlock), lds, s, L);
   return hipGetLastError();
 }
 
 template <class Op>
-static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_bucket,
-                                    int nbuckets, uint32_t ntiles, int vpt, const Tuning& tu,
+static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning& tu,
                                     hipStream_t s) {
-  return vpt == 1 ? launch_batched_vpt<Op, 1>(tab, tile_bucket, nbuckets, ntiles, tu, s)
-                  : launch_batched_vpt<Op, kBatchVPT>(tab, tile_bucket, nbuckets, ntiles, tu, s);
+  switch (vpt) {
+    case 1: return launch_batched_vpt<Op, 1>(L, tu, s);
+    case 4: return launch_batched_vpt<Op, 4>(L, tu, s);
+    default: return launch_batched_vpt<Op, 2>(L, tu, s);
+  }
 }
 
 }  // namespace bpsr
@@ -414,8 +438,8 @@ static hipError_t launch_batched_op(const BatchEntry* tab, const uint32_t* tile_
   hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s) {     \
     return launch_fold_op<OP>(a, tu, s);                                                  \
   }                                                                                       \
-  hipError_t launch_batched_##NAME(const BatchEntry* tab, const uint32_t* ts, int nb,     \
-                                   uint32_t nt, int vpt, const Tuning& tu, hipStream_t s) { \
-    return launch_batched_op<OP>(tab, ts, nb, nt, vpt, tu, s);                            \
+  hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
+                                   hipStream_t s) {                                       \
+    return launch_batched_op<OP>(L, vpt, tu, s);                                          \
   }                                                                                       \
   }

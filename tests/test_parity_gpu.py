@@ -185,6 +185,73 @@ def test_batched_block_matches_oracle(red, dev, port, dt):
         assert_bytes_match(dt, dst.cpu().numpy(), w, nan_class_f32_f64=False)
 
 
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.FLOAT64, DType.INT8],
+                         ids=lambda d: DType(d).name)
+@pytest.mark.parametrize("plan", [False, True], ids=["one_off", "plan"])
+def test_batched_ragged_mixed_table(red, dev, port, dt, plan):
+    """One table mixing every tile kind: source counts 1..32 (register path
+    n <= 8 and memory path n > 8), co-aligned offsets (head + tail element
+    tiles), operands that are not co-aligned (element tiles only, several
+    parts), NaN/Inf/subnormal inputs (exact replay through the records'
+    advanced pointers), trailing bytes, and empty buckets."""
+    es = elem_size(dt)
+    spec = [  # (n_elems, n_sources, offsets of dst + sources or None, class)
+        (100_000, 8, None, "special"), (4099, 9, None, "normal"), (1, 1, None, "normal"),
+        (70_001, 32, None, "bits"), (0, 8, None, "normal"), (3 * 1024 + 5, 2, [4, 4, 4], "normal"),
+        (50_000, 3, [0, es, 2 * es, 1], "normal"), (257, 12, None, "special"),
+        (300_000, 5, [2, 6, 10, 14, 2, 6], "normal"), (9, 8, None, "bits"),
+    ]
+    buckets, wants, views = [], [], []
+    for i, (ne, N, offs, cls) in enumerate(spec):
+        L = ne * es + (3 if i == 3 else 0)          # bucket 3: trailing bytes
+        ins = [np.ascontiguousarray(synth.bucket(dt, ne, k, cls, 300 + i)).view(np.uint8)
+               for k in range(N)]
+        if i == 3:
+            ins = [np.concatenate([x, np.array([k, 7, 9], np.uint8)]) for k, x in enumerate(ins)]
+        offs = offs or [0] * (N + 1)
+        offs = (offs + [offs[-1]] * (N + 1))[:N + 1]
+        bufs = [to_dev(x, dev, offset=o)[0] for x, o in zip(ins, offs[1:])]
+        dbuf, _ = to_dev(np.full(L, 0x5A, np.uint8), dev, offset=offs[0])
+        buckets.append((ptr(dbuf, offs[0]), [ptr(b, o) for b, o in zip(bufs, offs[1:])], L))
+        views.append((dbuf, offs[0], L, bufs))
+        w = np.full(L, 0x5A, np.uint8)
+        if L:
+            port.sum_n(w, ins, L, dt)
+        wants.append(w)
+    if plan:
+        p = red.make_plan(buckets, dt)
+        p.launch()
+        torch.cuda.synchronize()
+        p.close()
+    else:
+        red.sum_batched(buckets, dt)
+        torch.cuda.synchronize()
+    for (dbuf, o, L, _), w in zip(views, wants):
+        assert_bytes_match(dt, dbuf[o:o + L].cpu().numpy(), w, nan_class_f32_f64=False)
+
+
+def test_batched_large_table_vpt4_equals_torch(red, dev):
+    """A block above the small-table threshold (1024-vector tiles): 6 x 6 MiB
+    fp32 buckets, 8 sources, against torch's own left fold (bit-exact for
+    finite IEEE adds), ragged lengths."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    N = 8
+    buckets, checks = [], []
+    for i in range(6):
+        ne = (6 << 20) // 4 + 3 * i
+        srcs = [torch.randn(ne, device=dev, generator=g) for _ in range(N)]
+        dst = torch.empty_like(srcs[0])
+        buckets.append((dst, srcs, ne * 4))
+        checks.append((dst, srcs))
+    red.sum_batched(buckets, DType.FLOAT32)
+    torch.cuda.synchronize()
+    for dst, srcs in checks:
+        want = srcs[0].clone()
+        for s in srcs[1:]:
+            want.add_(s)
+        assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
+
+
 @pytest.mark.parametrize("dt", [DType.FLOAT16, DType.BFLOAT16], ids=lambda d: DType(d).name)
 def test_accum_f32_mode_within_one_ulp(red, dev, dt):
     from prophet_amd.reducer import MODE_ACCUM_F32
