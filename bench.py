@@ -143,10 +143,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    # Bind this rank's GPU before the process group exists, so RCCL's
+    # communicator (barrier, the max-over-ranks all_reduce) uses it.
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     from prophet_amd.arena import BucketArena
     from prophet_amd.dtypes import DType

@@ -81,7 +81,11 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 
 static Tuning& tuning() {
   static Tuning tu = [] {
-    Tuning t{2, 1, 1 << 20, 1, 2, 0};  // tools/sweep.py, tools/occ_sweep.py (profiles/)
+    // tools/sweep.py, tools/occ_sweep.py, tools/cfg3_probe.py (profiles/)
+    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096};
+    if (const char* v = getenv("BPSR_OCC_MIN_TILES")) t.occ_min_tiles = (uint32_t)atol(v);
+    if (const char* v = getenv("BPSR_OCC_MIN_TILES_BATCH"))
+      t.occ_min_tiles_batch = (uint32_t)atol(v);
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);

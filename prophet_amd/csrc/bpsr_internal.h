@@ -89,6 +89,8 @@ struct Tuning {
   int occ;       // workgroups resident per CU (0 = hardware limit), set through LDS
   int small_occ;        // residency for short fold launches (occ == 1 only)
   int small_occ_batch;  // residency for short batched launches (occ == 1 only)
+  uint32_t occ_min_tiles;        // fold launches shorter than this are "short"
+  uint32_t occ_min_tiles_batch;  // batched launches shorter than this are "short"
 };
 
 // Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so
@@ -99,12 +101,14 @@ constexpr size_t kLdsPerCU = 160 * 1024;
 inline size_t occ_lds_bytes(int occ) {
   return occ > 0 ? (kLdsPerCU / (size_t)occ) & ~(size_t)255 : 0;
 }
-// The 1-workgroup-per-CU cap pays on long sweeps only: below kOccMinTiles
-// tiles (16 MiB per source at vpt 2) a launch is latency-bound and more
-// residency wins (profiles/r01_occ_sweep.jsonl).
-constexpr uint64_t kOccMinTiles = 2048;
+// The 1-workgroup-per-CU cap pays on long sweeps only: below occ_min_tiles
+// tiles (4096: 32 MiB per source at vpt 2) a launch is latency-bound and more
+// residency wins (profiles/r01_occ_sweep.jsonl, r01_thr_fold.jsonl: 8 MiB
+// 16.3 -> 14.6 us).  Batched launches (one Prophet block) likewise: the cap
+// measured 9 % slower on cfg3's 13-20 MB blocks (r01_thr_batch.jsonl).
 inline int launch_occ(const Tuning& tu, uint64_t tiles, bool batched) {
-  if (tu.occ != 1 || tiles >= kOccMinTiles) return tu.occ;
+  if (tu.occ != 1) return tu.occ;
+  if (tiles >= (batched ? tu.occ_min_tiles_batch : tu.occ_min_tiles)) return 1;
   return batched ? tu.small_occ_batch : tu.small_occ;
 }
 // Allow `kernel` to request up to 160 KiB of dynamic LDS (once per kernel).
@@ -158,8 +162,12 @@ hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, co
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.
 inline int fold_vpt(uint64_t nvec, int vpt) {
-  while (vpt > 1 && (nvec + (uint64_t)kBlock * vpt - 1) / ((uint64_t)kBlock * vpt) < kMinTiles)
-    vpt >>= 1;
+  auto tiles = [nvec](int v) { return (nvec + (uint64_t)kBlock * v - 1) / ((uint64_t)kBlock * v); };
+  while (vpt > 1 && tiles(vpt) < kMinTiles) vpt >>= 1;
+  // Mid-size launches (2048..4095 tiles of 16 KiB: 32-64 MiB per source) run
+  // 4-5 % faster with the bigger tile; longer sweeps prefer 8 KiB
+  // (profiles/r01_thr_fold.jsonl).
+  if (vpt == 2 && tiles(4) >= kMinTiles && tiles(4) < 2 * kMinTiles) vpt = 4;
   return vpt;
 }
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,

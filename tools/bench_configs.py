@@ -178,13 +178,22 @@ def cfg3(red, dev, N=8, sets=3):
     def release_group_graph(i):
         rgraphs[i % sets].replay()
 
+    # Every partition in ONE plan (no block boundaries): the batched kernel's
+    # own rate on the mixed ResNet-50 sizes, without per-block launch costs.
+    splans = [red.make_plan([(*views(i, p), p.len) for p in parts], DType.FLOAT16)
+              for i in range(sets)]
+
+    def single_plan(i):
+        splans[i % sets].launch(s)
+
     for name, fn in (("per_partition_launch", per_partition), ("prophet_block_batched", per_block),
                      ("single_batched_launch", all_in_one),
                      ("prophet_block_plans", per_block_plan),
                      ("prophet_block_plans_hipgraph", per_block_graph),
                      ("prophet_block_plans_4streams", per_block_plans_4streams),
                      ("prophet_block_plans_4streams_hipgraph", per_block_graph4),
-                     ("prophet_release_groups_hipgraph", release_group_graph)):
+                     ("prophet_release_groups_hipgraph", release_group_graph),
+                     ("single_plan_no_blocks", single_plan)):
         med, mn = timed(fn, 10, s)
         w, out, _ = data[0]
         fn(0)
@@ -196,28 +205,68 @@ def cfg3(red, dev, N=8, sets=3):
              hbm_frac=round((N + 1) * total / (med * 1e-3) / 8e12, 4), exact=ok)
 
 
-def size_sweep(red, dev, N=8):
+def graph_timed(fn, launches, sets):
+    """Per-launch device time of `launches` calls captured in one hipGraph
+    (no host in the loop), median of 5 replays."""
     import torch
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for i in range(sets):
+            fn(i, side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        for i in range(launches):
+            fn(i, side)
+    g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / launches)
+    return statistics.median(ts)
+
+
+def size_sweep(red, dev, N=8):
+    """8-way fp16 single-bucket sum over the BASELINE "1 KiB - 98 MiB" range.
+    Worker slots come from one skewed arena per set (as the server allocates
+    them).  `us` = device time per launch from a hipGraph of back-to-back
+    launches; `us_python` = one ctypes call per launch from Python (host-bound
+    below a few MiB)."""
+    import torch
+    from prophet_amd.arena import BucketArena
     from prophet_amd.dtypes import DType
     s = torch.cuda.current_stream()
     sizes = [1 << k for k in range(10, 27)] + [102_228_128]
     for B in sizes:
         n = B // 2
-        sets = 3 if B >= (8 << 20) else 1
-        data = [([torch.randn(n, device=dev).half().view(torch.uint8) for _ in range(N)],
-                 torch.empty(B, dtype=torch.uint8, device=dev)) for _ in range(sets)]
+        sets = 3 if B >= (1 << 20) else 1
+        data = []
+        for _ in range(sets):
+            slots = BucketArena(N + 1, B, dev).slots()
+            for t in slots[:N]:
+                t.view(torch.float16).copy_(torch.randn(n, device=dev))
+            data.append((slots[:N], slots[N]))
 
-        def fn(i):
+        def fn(i, st=s):
             w, o = data[i % sets]
-            red.sum_n(o, w, B, DType.FLOAT16, stream=s)
-        med, mn = timed(fn, 50 if B < (16 << 20) else 10, s)
+            red.sum_n(o, w, B, DType.FLOAT16, stream=st)
+        med_py, _ = timed(fn, 50 if B < (16 << 20) else 10, s)
+        med = graph_timed(fn, 60 if B < (16 << 20) else 12, sets)
         w, o = data[0]
         fn(0)
         torch.cuda.synchronize()
         ok = bool(torch.equal(o, torch_fold(w, torch.float16)))
         emit(config="sweep_fp16", bucket_bytes=B, n_workers=N, us=round(med * 1e3, 2),
-             gibps=round(N * B / (med * 1e-3) / GIB, 1),
+             us_python=round(med_py * 1e3, 2), gibps=round(N * B / (med * 1e-3) / GIB, 1),
              hbm_frac=round((N + 1) * B / (med * 1e-3) / 8e12, 4), exact=ok)
+        del data
+        torch.cuda.empty_cache()
 
 
 def cfg4(red, dev, N=8):
@@ -355,6 +404,59 @@ def cfg1(dev, N=2, B=64 << 20):
                      policy=["fused", "incremental"][policy], n_workers=N, bucket_bytes=B,
                      round_ms=round(med * 1e3, 3), gibps=round(N * B / med / GIB, 2), exact=ok)
                 srv.close()
+    cfg1_pipelined(host, N, B)
+
+
+def cfg1_pipelined(host, N, B):
+    """cfg1 with BytePS's worker loop structure: each worker has a push thread
+    and a pull thread (core_loops.cc:492-528 PushLoop, 530-564 PullLoop); the
+    pull of a partition is issued as soon as that partition's push returned, so
+    the D2H of partition k overlaps the H2D of partition k+1."""
+    import threading
+    import torch
+    from prophet_amd.buckets import partition_tensor
+    from prophet_amd.dtypes import DType
+    from prophet_amd.server import PSServer
+    parts = [(p.key, p.offset, p.len) for p in partition_tensor(0, B)]
+    srv = PSServer(N, engine_lanes=4, policy=0)
+    outs = [torch.empty(B, dtype=torch.uint8).pin_memory() for _ in range(N)]
+
+    def rnd(init=False):
+        pushed = [[threading.Event() for _ in parts] for _ in range(N)]
+
+        def pusher(k):
+            b = host[k].view(torch.uint8)
+            for i, (key, off, ln) in enumerate(parts):
+                srv.push(key, k, b[off:off + ln], DType.FLOAT32)
+                pushed[k][i].set()
+
+        def puller(k):
+            for i, (key, off, ln) in enumerate(parts):
+                pushed[k][i].wait()
+                srv.pull(key, outs[k][off:off + ln])
+        ts = [threading.Thread(target=pusher, args=(k,)) for k in range(N)]
+        if not init:
+            ts += [threading.Thread(target=puller, args=(k,)) for k in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    rnd(init=True)
+    rnd()
+    ts_ = []
+    for _ in range(10):
+        t0 = time.perf_counter()
+        rnd()
+        ts_.append(time.perf_counter() - t0)
+    med = statistics.median(ts_)
+    want = host[0].clone()
+    for h in host[1:]:
+        want += h
+    ok = all(bool(torch.equal(o, want.view(torch.uint8))) for o in outs)
+    emit(config="cfg1", layout="17keys_push_pull_threads", pushes_from="host", policy="fused",
+         n_workers=N, bucket_bytes=B, round_ms=round(med * 1e3, 3),
+         gibps=round(N * B / med / GIB, 2), exact=ok)
+    srv.close()
 
 
 def main():

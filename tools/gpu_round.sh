@@ -3,7 +3,7 @@
 # trace.  Each GPU step has its own time limit; the script stops at the first
 # step that ends in anything other than success or an ordinary test failure
 # (fault, abort, segfault, timeout).  Output: gpurun_out/<tag>/...
-#   usage: tools/gpu_round.sh <tag> [steps...]   steps: test smoke bench sweep prof pmc occ cfg3 configs
+#   usage: tools/gpu_round.sh <tag> [steps...]   steps: test smoke bench sweep prof pmc occ cfg3 configs cfg1 lat cfg3trace
 set -u
 TAG=${1:-r01}; shift || true
 STEPS=${*:-"test smoke bench sweep prof"}
@@ -38,6 +38,17 @@ for s in $STEPS; do
     occ)   run occ 600 python tools/occ_sweep.py ;;
     cfg3)  run cfg3 600 python tools/bench_configs.py --only cfg3,sweep ;;
     configs) run configs 900 python tools/bench_configs.py ;;
+    cfg1)  run cfg1 300 python tools/bench_configs.py --only cfg1 ;;
+    lat)   run lat 300 python tools/latency_probe.py ;;
+    cfg3p) run cfg3p 300 python tools/cfg3_probe.py ;;
+    thr)   for t in 2048 4096 8192 1000000; do
+             run thr_b$t 300 env BPSR_OCC_MIN_TILES_BATCH=$t python tools/cfg3_probe.py --occ 1 --streams 1
+           done
+           for t in 2048 4096 8192; do
+             run thr_f$t 300 env BPSR_OCC_MIN_TILES=$t python tools/occ_sweep.py --mib 8,16,32,64,128 --occ 1 --vpt 2,4
+           done ;;
+    cfg3trace) run cfg3trace 600 rocprofv3 --kernel-trace --output-format csv \
+             -d "$OUT/cfg3trace" -o cfg3 -- python tools/bench_configs.py --only cfg3 ;;
     *) echo "unknown step $s" ;;
   esac
 done
