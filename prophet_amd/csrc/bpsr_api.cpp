@@ -82,10 +82,11 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 static Tuning& tuning() {
   static Tuning tu = [] {
     // tools/sweep.py, tools/occ_sweep.py, tools/cfg3_probe.py (profiles/)
-    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096};
+    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1};
     if (const char* v = getenv("BPSR_OCC_MIN_TILES")) t.occ_min_tiles = (uint32_t)atol(v);
     if (const char* v = getenv("BPSR_OCC_MIN_TILES_BATCH"))
       t.occ_min_tiles_batch = (uint32_t)atol(v);
+    if (const char* v = getenv("BPSR_AUTO_N")) t.auto_n = atoi(v) != 0;
     if (const char* v = getenv("BPSR_VPT")) t.vpt = atoi(v);
     if (const char* v = getenv("BPSR_NT")) t.nt = atoi(v);
     if (const char* v = getenv("BPSR_MAX_GRID")) t.max_grid = atoi(v);
@@ -101,6 +102,20 @@ static Tuning& tuning() {
     return t;
   }();
   return tu;
+}
+
+// Bytes in flight per CU = residency x 256 lanes x n sources x vpt x 16 B.
+// The defaults (1 workgroup per CU, vpt 2) give 64 KiB at the 8-way fold;
+// with n <= 4 sources that leaves the HBM queues short, and 2 workgroups per
+// CU with 16 KiB tiles measured +13-26 % (profiles/r01_nsweep.jsonl: 2-way
+// 256 MiB 5.21 -> 6.56 TB/s).  Applies unless BPSR_AUTO_N=0.
+static Tuning tuning_for_n(int n) {
+  Tuning t = tuning();
+  if (t.auto_n && n <= 4 && t.occ == 1) {
+    t.occ = 2;
+    t.vpt = 4;
+  }
+  return t;
 }
 
 static inline hipStream_t to_stream(void* s) {
@@ -122,7 +137,7 @@ static int fold_once(void* dst, const void* const* srcs, int n, size_t len, int 
   a.dst = static_cast<unsigned char*>(dst);
   a.n = n;
   make_geom(dtype, len, dst, srcs, n, copy_trailing, &a.g, &a.aligned);
-  hipError_t e = launch_fold(a, dtype, mode, tuning(), s);
+  hipError_t e = launch_fold(a, dtype, mode, tuning_for_n(n), s);
   if (e != hipSuccess) return hip_fail(e, "fold kernel launch");
   return BYTEPS_REDUCE_OK;
 }
@@ -194,6 +209,7 @@ static int stage_acquire(size_t bytes, StageSlot** out) {
 // ------------------------------------------------------- batch table build --
 struct TableInfo {
   int vpt = 1;   // tile size of the batched kernel for this table
+  int nmax = 1;  // most sources of any bucket (residency rule, tuning_for_n)
   int live = 0;          // buckets with len > 0
   uint32_t tiles = 0;    // workgroups (element tiles first, then vector tiles)
   uint32_t rec_stride = 0;
@@ -236,7 +252,7 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
   }
   // Same tile-size rule as a single fold (fold_vpt): the tuned vpt, halved
   // while the launch would have fewer than kMinTiles tiles.
-  const int vpt = fold_vpt(vecs, tuning().vpt);
+  const int vpt = fold_vpt(vecs, tuning_for_n(nmax).vpt);
   const uint64_t tile_vecs = (uint64_t)kBlock * vpt;
   auto elem_parts = [](const BatchEntry& e) -> uint64_t {
     const uint64_t n_scalar = e.g.head_elems + (e.g.n_elems - e.g.tail_begin);
@@ -285,6 +301,7 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
     }
   }
   ti->vpt = vpt;
+  ti->nmax = nmax;
   ti->live = (int)tab.size();
   ti->tiles = (uint32_t)tiles;
   ti->rec_stride = stride;
@@ -432,7 +449,7 @@ int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets, i
   hipStream_t s = to_stream(stream);
   hipError_t e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
-  e = launch_batched(batch_launch(slot->dev, ti), ti.vpt, dtype, mode, tuning(), s);
+  e = launch_batched(batch_launch(slot->dev, ti), ti.vpt, dtype, mode, tuning_for_n(ti.nmax), s);
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
   e = hipEventRecord(slot->done, s);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
@@ -483,7 +500,7 @@ int byteps_reduce_plan_launch(byteps_reduce_plan* p, void* stream) {
   if (!p) return fail(BYTEPS_REDUCE_EARGS, "null plan");
   if (p->ti.tiles == 0) return BYTEPS_REDUCE_OK;
   hipError_t e = launch_batched(batch_launch(p->dev_table, p->ti), p->ti.vpt, p->dtype, p->mode,
-                                tuning(), to_stream(stream));
+                                tuning_for_n(p->ti.nmax), to_stream(stream));
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "plan kernel launch");
 }
 

@@ -91,6 +91,7 @@ struct Tuning {
   int small_occ_batch;  // residency for short batched launches (occ == 1 only)
   uint32_t occ_min_tiles;        // fold launches shorter than this are "short"
   uint32_t occ_min_tiles_batch;  // batched launches shorter than this are "short"
+  int auto_n;    // residency/tile size by source count (bpsr_api.cpp tuning_for_n)
 };
 
 // Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so

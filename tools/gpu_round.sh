@@ -38,6 +38,14 @@ for s in $STEPS; do
     occ)   run occ 600 python tools/occ_sweep.py ;;
     cfg3)  run cfg3 600 python tools/bench_configs.py --only cfg3,sweep ;;
     configs) run configs 900 python tools/bench_configs.py ;;
+    dtypes) run bench_f16 300 python bench.py --dtype f16 --no-cpu-baseline &&
+            run bench_bf16 300 python bench.py --dtype bf16 --no-cpu-baseline &&
+            run bench_bf16_16 300 python bench.py --dtype bf16 --workers 16 --no-cpu-baseline &&
+            run bench_f32_16 300 python bench.py --workers 16 --no-cpu-baseline &&
+            run bench_f32_2 300 python bench.py --workers 2 --no-cpu-baseline ;;
+    nsweep) for n in 2 3 4 16; do
+              run nsweep_$n 400 python tools/occ_sweep.py --workers $n --mib 64,256 --occ 1,2,4,8 --vpt 1,2,4 || exit 1
+            done ;;
     cfg1)  run cfg1 300 python tools/bench_configs.py --only cfg1 ;;
     lat)   run lat 300 python tools/latency_probe.py ;;
     cfg3p) run cfg3p 300 python tools/cfg3_probe.py ;;

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Occupancy cap x bucket size for the 8-way fold: kernel time without host
 launch overhead (20 launches captured in one hipGraph, replayed), so small
-buckets measure the device, not Python.  One JSON line per (bytes, occ, vpt)."""
+buckets measure the device, not Python.  One JSON line per (bytes, occ, vpt).
+With --workers <= 4 run it under BPSR_AUTO_N=0, or the library's source-count
+rule (bpsr_api.cpp tuning_for_n) replaces an occ=1 request by occ 2 / vpt 4."""
 from __future__ import annotations
 
 import argparse
