@@ -35,6 +35,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
+# --dtype name -> (byteps DataType id, torch dtype name); ids: common.h:52-65 (+ bf16 = 11)
+DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
+          "u8": (3, "uint8"), "i32": (4, "int32"), "i8": (5, "int8"), "i64": (6, "int64"),
+          "bf16": (11, "bfloat16")}
 
 
 def parse():
@@ -44,7 +48,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workers", type=int, default=8, help="N-way (pushing workers)")
     p.add_argument("--bucket-mib", type=float, default=256.0)
-    p.add_argument("--dtype", default="f32", choices=["f32", "f16", "bf16"])
+    p.add_argument("--dtype", default="f32", choices=list(DTYPES))
+    p.add_argument("--mode", default="reference", choices=["reference", "accum"],
+                   help="f16/bf16: round after every add (reference) or fp32 accumulate")
     p.add_argument("--sets", type=int, default=3, help="rotated input sets")
     p.add_argument("--layout", default="arena", choices=["arena", "separate"],
                    help="worker slots in one skewed HBM arena, or separate allocations")
@@ -61,7 +67,7 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
     from oracle.oracle import PortReducer, RefReducer
     from prophet_amd import synth
 
-    es = {0: 4, 2: 2, 11: 2}[dtype_id]
+    es = {0: 4, 1: 8, 2: 2, 3: 1, 4: 4, 5: 1, 6: 8, 11: 2}[dtype_id]
     if dtype_id == 11:           # reference has no bf16: time the restatement
         kinds = [("port", PortReducer)]
     else:
@@ -154,8 +160,10 @@ def main():
     from prophet_amd.dtypes import DType
     from prophet_amd.reducer import GpuReducer
 
-    dtype_id = {"f32": DType.FLOAT32, "f16": DType.FLOAT16, "bf16": DType.BFLOAT16}[args.dtype]
-    es = 4 if args.dtype == "f32" else 2
+    dtype_id = DType(DTYPES[args.dtype][0])
+    tdt = getattr(torch, DTYPES[args.dtype][1])
+    es = torch.empty(0, dtype=tdt).element_size()
+    mode = 1 if args.mode == "accum" else 0
     N = args.workers
     B = int(args.bucket_mib * (1 << 20)) // es * es
     n_elems = B // es
@@ -166,8 +174,6 @@ def main():
     # channel aliasing of power-of-two-spaced buffers), plus the output slot.
     # Seeded N(0,1) gradients per (rank, set, worker), generated on device.
     torch.manual_seed(1000 + rank)
-    tdt = {DType.FLOAT32: torch.float32, DType.FLOAT16: torch.float16,
-           DType.BFLOAT16: torch.bfloat16}[dtype_id]
     sets = []
     for s in range(args.sets):
         if args.layout == "arena":
@@ -175,14 +181,17 @@ def main():
         else:
             slots = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(N + 1)]
         for t in slots[:N]:
-            t.view(tdt).copy_(torch.randn(n_elems, device=dev))
+            if tdt.is_floating_point:
+                t.view(tdt).copy_(torch.randn(n_elems, device=dev))
+            else:
+                t.copy_(torch.randint(0, 256, (B,), dtype=torch.uint8, device=dev))
         sets.append((slots[N], slots[:N]))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
 
     def step(i):
         dst, srcs = sets[i % len(sets)]
-        red.sum_n(dst, srcs, B, dtype_id, stream=stream)
+        red.sum_n(dst, srcs, B, dtype_id, mode=mode, stream=stream)
 
     for i in range(args.warmup):
         step(i)
@@ -214,7 +223,7 @@ def main():
     chk = srcs[0].view(tdt)[: 1 << 20].clone()
     for s in srcs[1:]:
         chk.add_(s.view(tdt)[: 1 << 20])
-    ok = bool(torch.equal(chk.view(torch.uint8), dst[: chk.numel() * es]))
+    ok = bool(torch.equal(chk.view(torch.uint8), dst[: chk.numel() * es])) if mode == 0 else None
 
     if rank != 0:
         if world > 1:
@@ -223,6 +232,8 @@ def main():
     alg_bytes = (N + 1) * B
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload = f"{N}-way {args.dtype} left-fold sum of one {B / (1 << 20):.0f} MiB bucket per GPU"
+    if mode:
+        workload += " (fp32-accumulate mode)"
     tv, tnt, tgrid, tocc = red.get_tuning()
     line = {
         "metric": "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs",

@@ -82,7 +82,11 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 static Tuning& tuning() {
   static Tuning tu = [] {
     // tools/sweep.py, tools/occ_sweep.py, tools/cfg3_probe.py (profiles/)
-    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1};
+    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1, 4, 2};
+    if (const char* v = getenv("BPSR_COPY_OCC")) t.copy_occ = atoi(v);
+    if (const char* v = getenv("BPSR_COPY_VPT")) t.copy_vpt = atoi(v);
+    if (t.copy_occ < 0 || t.copy_occ > 8) t.copy_occ = 4;
+    if (t.copy_vpt != 1 && t.copy_vpt != 4) t.copy_vpt = 2;
     if (const char* v = getenv("BPSR_OCC_MIN_TILES")) t.occ_min_tiles = (uint32_t)atol(v);
     if (const char* v = getenv("BPSR_OCC_MIN_TILES_BATCH"))
       t.occ_min_tiles_batch = (uint32_t)atol(v);

@@ -92,6 +92,8 @@ struct Tuning {
   uint32_t occ_min_tiles;        // fold launches shorter than this are "short"
   uint32_t occ_min_tiles_batch;  // batched launches shorter than this are "short"
   int auto_n;    // residency/tile size by source count (bpsr_api.cpp tuning_for_n)
+  int copy_occ;  // workgroups per CU of long copies (0 = hardware)
+  int copy_vpt;  // copy tile: kBlock * copy_vpt 16-B vectors
 };
 
 // Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so

@@ -3,48 +3,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "bpsr_internal.h"
-#include "bpsr_ops.h"
+#include <cstring>
+
+#include "bpsr_kernels_impl.h"
 
 namespace bpsr {
 
-// 16-B vectors between an unaligned head and tail (operands co-aligned mod 16),
-// bytes otherwise.  Same tiling as the fold kernel: a workgroup owns
-// kBlock*kCopyVPT contiguous vectors.
-constexpr int kCopyVPT = 8;
-
-__global__ __launch_bounds__(kBlock) void copy_kernel(unsigned char* __restrict__ dst,
-                                                      const unsigned char* __restrict__ src,
-                                                      uint64_t head, uint64_t nvec,
-                                                      uint64_t len) {
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  const uint64_t tile_vecs = (uint64_t)kBlock * kCopyVPT;
-  const uint64_t ntiles = (nvec + tile_vecs - 1) / tile_vecs;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t v0 = tile * tile_vecs + threadIdx.x;
-    if ((tile + 1) * tile_vecs <= nvec) {
-      u4 x[kCopyVPT];
-#pragma unroll
-      for (int j = 0; j < kCopyVPT; ++j)
-        x[j] = __builtin_nontemporal_load(
-            reinterpret_cast<const u4*>(src + head + (v0 + j * kBlock) * 16));
-#pragma unroll
-      for (int j = 0; j < kCopyVPT; ++j)
-        __builtin_nontemporal_store(x[j], reinterpret_cast<u4*>(dst + head + (v0 + j * kBlock) * 16));
-    } else {
-      for (uint64_t v = v0; v < nvec; v += kBlock)
-        *reinterpret_cast<u4*>(dst + head + v * 16) =
-            *reinterpret_cast<const u4*>(src + head + v * 16);
-    }
-  }
-  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t tail_begin = head + nvec * 16;
-  const uint64_t nscalar = head + (len - tail_begin);
-  for (uint64_t s = t; s < nscalar; s += stride) {
-    const uint64_t b = s < head ? s : tail_begin + (s - head);
-    dst[b] = src[b];
-  }
+// The copy is the fold kernel with one byte-typed source: same tiles, buffer
+// loads, nt policy and element path (unaligned head/tail bytes; operands not
+// co-aligned mod 16 go through the element path entirely).  Its residency is
+// its own: two streams need more workgroups per CU than the 9-stream fold to
+// keep the HBM queues full: 4 per CU with 8 KiB tiles measured 0.80 of the
+// roofline at 256 MiB vs 0.75 for the old grid-stride copy and 0.67 for
+// torch's (profiles/r01_copy_sweep.jsonl; Tuning::copy_occ / copy_vpt).
+template <int VPT>
+static hipError_t launch_copy_vpt(const FoldArgs& a0, const Tuning& tu, hipStream_t s) {
+  static const hipError_t lds_ok =
+      allow_full_lds(reinterpret_cast<const void*>(&fold_kernel<OpI8, VPT, true, 1>));
+  if (lds_ok != hipSuccess) return lds_ok;
+  FoldArgs a = a0;
+  a.grid = (uint32_t)fold_grid(a.g, tu, VPT);
+  const int occ = a.grid >= tu.occ_min_tiles ? tu.copy_occ : 0;
+  hipLaunchKernelGGL((fold_kernel<OpI8, VPT, true, 1>), dim3(a.grid), dim3(kBlock),
+                     occ_lds_bytes(occ), s, a);
+  return hipGetLastError();
 }
 
 hipError_t allow_full_lds(const void* kernel) {
@@ -54,25 +36,20 @@ hipError_t allow_full_lds(const void* kernel) {
 
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s) {
-  const uintptr_t d = (uintptr_t)dst, q = (uintptr_t)src;
-  uint64_t head = 0, nvec = 0;
-  if (((d ^ q) & 15u) == 0) {
-    head = (16u - (d & 15u)) & 15u;
-    if (head > len) head = len;
-    nvec = (len - head) / 16;
-  } else {
-    head = len;  // not co-aligned: byte path (rare; a shard view at an odd offset)
+  FoldArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.srcs[0] = static_cast<const unsigned char*>(src);
+  a.dst = static_cast<unsigned char*>(dst);
+  a.n = 1;
+  make_geom(kUInt8, len, dst, &src, 1, false, &a.g, &a.aligned);
+  int vpt = tu.copy_vpt;
+  while (vpt > 1 && (a.g.nvec + (uint64_t)kBlock * vpt - 1) / ((uint64_t)kBlock * vpt) < kMinTiles)
+    vpt >>= 1;
+  switch (vpt) {
+    case 1: return launch_copy_vpt<1>(a, tu, s);
+    case 2: return launch_copy_vpt<2>(a, tu, s);
+    default: return launch_copy_vpt<4>(a, tu, s);
   }
-  const uint64_t tile_vecs = (uint64_t)kBlock * kCopyVPT;
-  uint64_t blocks = (nvec + tile_vecs - 1) / tile_vecs;
-  const uint64_t nscalar = head + (len - head - nvec * 16);
-  const uint64_t sblocks = (nscalar + kBlock - 1) / kBlock;
-  if (sblocks > blocks) blocks = sblocks;
-  if (blocks > (uint64_t)tu.max_grid) blocks = tu.max_grid;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(copy_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s,
-                     (unsigned char*)dst, (const unsigned char*)src, head, nvec, (uint64_t)len);
-  return hipGetLastError();
 }
 
 hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,

@@ -133,7 +133,7 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
       if (NS > 0 || k0 + g < ns) {
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
-          if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
+          if (k0 + g == 0) acc[j] = Op::init_fast(x[g][j]);
           else Op::fast(acc[j], x[g][j]);
         }
       }
@@ -150,7 +150,7 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
   for (int j = 0; j < VPT; ++j) bad |= valid[j] && Op::has_nan(acc[j]);
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
-    vec16 out = Op::finish(acc[j]);
+    vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (valid[j] && Op::has_nan(acc[j]))
         out = fold_vector_exact<Op, NT>(xsrcs, ns, off0 + j * kStep);
@@ -197,7 +197,7 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
       if (NS > 0 || k0 + g < ns) {
 #pragma unroll
         for (int j = 0; j < VPT; ++j) {
-          if (k0 + g == 0) acc[j] = Op::init(x[g][j]);
+          if (k0 + g == 0) acc[j] = Op::init_fast(x[g][j]);
           else Op::fast(acc[j], x[g][j]);
         }
       }
@@ -215,7 +215,7 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
   const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + byte0, 0, kTileBytes, 0x00020000);
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
-    vec16 out = Op::finish(acc[j]);
+    vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (Op::has_nan(acc[j]))
         out = fold_vector_exact<Op, NT>(xsrcs, ns, byte0 + voff + j * kBlock * 16);

@@ -76,6 +76,8 @@ struct OpF32 {
            __builtin_isnan(x3);
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = f32_add(a, b); }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -116,6 +118,8 @@ struct OpF64 {
     return f64_nan(((uint64_t)a.w[1] << 32) | a.w[0]) || f64_nan(((uint64_t)a.w[3] << 32) | a.w[2]);
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = f64_add(a, b); }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -173,6 +177,8 @@ struct OpF16 {
     return (t & 0x80008000u) != 0;
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool tail) { a = (E)f16_add_elem(a, b, tail); }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -223,6 +229,8 @@ struct OpBF16 {
     return (t & 0x80008000u) != 0;
   }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = (E)bf16_add(a, b); }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -243,41 +251,72 @@ __device__ __forceinline__ uint32_t f2h_bits(uint32_t x) {
 template <bool BF>
 struct OpAcc16 {
   static constexpr int kSize = 2;
-  struct Acc { uint32_t f[8]; };
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 hh2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bb2 __attribute__((ext_vector_type(2)));
+  struct Acc { f2 f[4]; };  // element 2i in f[i].x, 2i+1 in f[i].y
   using E = uint16_t;
   using EAcc = uint32_t;
   __device__ static uint32_t up(uint32_t h) { return BF ? (h << 16) : h2f_bits(h); }
   __device__ static uint32_t down(uint32_t x) { return BF ? f32_to_bf16_rne(x) : f2h_bits(x); }
+  __device__ static uint32_t bits(float x) { return bitcast<uint32_t>(x); }
+  // Exact path (NaN payload rules): element by element.
   __device__ static Acc init(const vec16& v) {
     Acc a;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { a.f[2 * i] = up(v.w[i] & 0xffffu); a.f[2 * i + 1] = up(v.w[i] >> 16); }
+    for (int i = 0; i < 4; ++i)
+      a.f[i] = f2{bitcast<float>(up(v.w[i] & 0xffffu)), bitcast<float>(up(v.w[i] >> 16))};
     return a;
   }
   __device__ static void accum(Acc& a, const vec16& b) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      a.f[2 * i] = f32_add(a.f[2 * i], up(b.w[i] & 0xffffu));
-      a.f[2 * i + 1] = f32_add(a.f[2 * i + 1], up(b.w[i] >> 16));
+      a.f[i].x = bitcast<float>(f32_add(bits(a.f[i].x), up(b.w[i] & 0xffffu)));
+      a.f[i].y = bitcast<float>(f32_add(bits(a.f[i].y), up(b.w[i] >> 16)));
     }
-  }
-  __device__ static void fast(Acc& a, const vec16& b) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      a.f[2 * i] = bitcast<uint32_t>(bitcast<float>(a.f[2 * i]) + bitcast<float>(up(b.w[i] & 0xffffu)));
-      a.f[2 * i + 1] = bitcast<uint32_t>(bitcast<float>(a.f[2 * i + 1]) + bitcast<float>(up(b.w[i] >> 16)));
-    }
-  }
-  __device__ static bool has_nan(const Acc& a) {
-    bool r = false;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r |= f32_nan(a.f[i]);
-    return r;
   }
   __device__ static vec16 finish(const Acc& a) {
     vec16 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v.w[i] = down(a.f[2 * i]) | (down(a.f[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) v.w[i] = down(bits(a.f[i].x)) | (down(bits(a.f[i].y)) << 16);
+    return v;
+  }
+  // Fast path: hardware widening (v_cvt_f32_f16 / shift), v_pk_add_f32, and
+  // one packed RNE narrowing per pair (v_cvt_pk_f16_f32 / v_cvt_pk_bf16_f32).
+  // Any NaN reaches the result and sends the vector to the exact replay.
+  __device__ static f2 widen(uint32_t w) {
+    if constexpr (BF) {
+      return f2{bitcast<float>(w << 16), bitcast<float>(w & 0xffff0000u)};
+    } else {
+      return __builtin_convertvector(bitcast<hh2>(w), f2);
+    }
+  }
+  __device__ static Acc init_fast(const vec16& v) {
+    Acc a;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.f[i] = widen(v.w[i]);
+    return a;
+  }
+  __device__ static void fast(Acc& a, const vec16& b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a.f[i] += widen(b.w[i]);
+  }
+  __device__ static bool has_nan(const Acc& a) {
+    bool r = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r |= __builtin_isnan(a.f[i].x) || __builtin_isnan(a.f[i].y);
+    return r;
+  }
+  __device__ static vec16 finish_fast(const Acc& a) {
+    vec16 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (BF) {
+        v.w[i] = bitcast<uint32_t>(__builtin_convertvector(a.f[i], bb2));
+      } else {
+        v.w[i] = bitcast<uint32_t>(__builtin_convertvector(a.f[i], hh2));
+      }
+    }
     return v;
   }
   __device__ static EAcc init_e(E v, bool) { return up(v); }
@@ -302,6 +341,8 @@ struct OpI8 {  // uint8 and int8: identical two's-complement bits
   __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
   __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a = (E)(a + b); }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -320,6 +361,8 @@ struct OpI32 {
   __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
   __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a += b; }
   __device__ static E finish_e(EAcc a, bool) { return a; }
@@ -343,6 +386,8 @@ struct OpI64 {
   __device__ static void fast(Acc& a, const vec16& b) { accum(a, b); }
   __device__ static bool has_nan(const Acc&) { return false; }
   __device__ static vec16 finish(const Acc& a) { return a; }
+  __device__ static Acc init_fast(const vec16& v) { return v; }
+  __device__ static vec16 finish_fast(const Acc& a) { return a; }
   __device__ static EAcc init_e(E v, bool) { return v; }
   __device__ static void accum_e(EAcc& a, E b, bool) { a += b; }
   __device__ static E finish_e(EAcc a, bool) { return a; }

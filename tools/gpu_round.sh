@@ -46,6 +46,17 @@ for s in $STEPS; do
     nsweep) for n in 2 3 4 16; do
               run nsweep_$n 400 python tools/occ_sweep.py --workers $n --mib 64,256 --occ 1,2,4,8 --vpt 1,2,4 || exit 1
             done ;;
+    ops)   run ops 300 python tools/op_probe.py &&
+           for d in f64 i32 i64 u8 i8; do run bench_$d 300 python bench.py --dtype $d --no-cpu-baseline || exit 1; done &&
+           run bench_f16acc 300 python bench.py --dtype f16 --mode accum --no-cpu-baseline &&
+           run bench_bf16acc 300 python bench.py --dtype bf16 --mode accum --no-cpu-baseline ;;
+    copysweep) for o in 0 2 4 8; do for v in 2 4; do
+                 run copy_o${o}_v$v 120 env BPSR_COPY_OCC=$o BPSR_COPY_VPT=$v python tools/op_probe.py --mib 256 || exit 1
+                 run copy64_o${o}_v$v 120 env BPSR_COPY_OCC=$o BPSR_COPY_VPT=$v python tools/op_probe.py --mib 64 || exit 1
+               done; done ;;
+    acc)   run bench_f16acc 300 python bench.py --dtype f16 --mode accum --no-cpu-baseline &&
+           run bench_bf16acc 300 python bench.py --dtype bf16 --mode accum --no-cpu-baseline &&
+           run ops 300 python tools/op_probe.py ;;
     cfg1)  run cfg1 300 python tools/bench_configs.py --only cfg1 ;;
     lat)   run lat 300 python tools/latency_probe.py ;;
     cfg3p) run cfg3p 300 python tools/cfg3_probe.py ;;
