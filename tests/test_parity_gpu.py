@@ -374,3 +374,86 @@ def test_plan_launch_and_graph_replay(red, dev, port):
     for (dst, _), w in zip(bufs, wants):
         assert np.array_equal(dst.cpu().numpy(), w)
     plan.close()
+
+
+@pytest.mark.parametrize("L", [1, 15, 16, 17, 4095, 65_539, 3 << 20, (64 << 20) + 5])
+@pytest.mark.parametrize("offs", [(0, 0), (3, 3), (5, 9)], ids=lambda o: f"d{o[0]}s{o[1]}")
+def test_copy_sizes_offsets_guards(red, dev, L, offs):
+    """CpuReducer::copy (cpu_reducer.cc:209-220): every byte of len, nothing
+    outside it; co-aligned, misaligned and non-co-aligned operands, from the
+    element path through short launches to long (residency-capped) ones."""
+    doff, soff = offs
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(L + doff)
+    src = torch.randint(0, 256, (L + soff + 64,), dtype=torch.uint8, device=dev, generator=gen)
+    dst = torch.full((L + doff + 64,), 0xEE, dtype=torch.uint8, device=dev)
+    red.copy(dst.data_ptr() + doff, src.data_ptr() + soff, L)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[doff:doff + L], src[soff:soff + L])
+    assert bool((dst[:doff] == 0xEE).all()) and bool((dst[doff + L:] == 0xEE).all())
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5])
+@pytest.mark.parametrize("mib", [1, 24, 96])
+def test_small_source_counts_equal_torch(red, dev, n, mib):
+    """n <= 4 sources run 2 workgroups/CU with 16 KiB tiles (bpsr_api.cpp
+    tuning_for_n): fused fold, in-place 2-op sum and 3-op sum equal torch's
+    own fp32 left fold bit for bit at short and long launch sizes (odd element
+    count: partial last tile + element tail)."""
+    ne = (mib << 20) // 4 + 7
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(100 * n + mib)
+    ins = [torch.randn(ne, device=dev, generator=gen) for _ in range(n)]
+    ref = ins[0].clone()
+    for s in ins[1:]:
+        ref.add_(s)
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, ne * 4, DType.FLOAT32)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    if n == 2:
+        acc = ins[0].clone()
+        red.sum(acc, ins[1], ne * 4, DType.FLOAT32)        # dst += src, in place
+        o3 = torch.empty_like(acc)
+        red.sum3(o3, ins[0], ins[1], ne * 4, DType.FLOAT32)
+        torch.cuda.synchronize()
+        assert torch.equal(acc.view(torch.int32), ref.view(torch.int32))
+        assert torch.equal(o3.view(torch.int32), ref.view(torch.int32))
+
+
+@pytest.mark.parametrize("dt", [DType.BFLOAT16, DType.FLOAT16], ids=lambda d: DType(d).name)
+def test_full_size_16bit_accum_mode_within_one_ulp(red, dev, dt):
+    """fp32-accumulate mode at 64 MiB per source through the hardware
+    conversions of the fast path: within 1 ulp of the exactly rounded sum."""
+    n = 32 << 20
+    tdt = torch.bfloat16 if dt == DType.BFLOAT16 else torch.float16
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(int(dt))
+    ins = [torch.randn(n, device=dev, generator=gen).to(tdt) for _ in range(8)]
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, n * 2, dt, mode=1)
+    exact = ins[0].double()
+    for s in ins[1:]:
+        exact += s.double()
+    torch.cuda.synchronize()
+    mbits = 7 if dt == DType.BFLOAT16 else 10
+    mag = exact.abs().clamp_min(2.0 ** -14)
+    ulp = torch.pow(2.0, torch.floor(torch.log2(mag)) - mbits)
+    assert bool(((out.double() - exact).abs() <= ulp + 1e-30).all())
+
+
+def test_full_size_bf16_left_fold_equals_torch(red, dev):
+    """bf16 (build-defined: fp32 add, RNE to bf16 after every add) at 128 MiB
+    per source through v_cvt_pk_bf16_f32 == torch's bf16 add chain (which
+    also computes in fp32 and rounds to nearest-even)."""
+    n = 64 << 20
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    ins = [torch.randn(n, device=dev, generator=gen).bfloat16() for _ in range(8)]
+    out = torch.empty_like(ins[0])
+    red.sum_n(out, ins, n * 2, DType.BFLOAT16)
+    ref = ins[0].clone()
+    for s in ins[1:]:
+        ref.add_(s)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
