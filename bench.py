@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--layout", default="arena", choices=["arena", "separate"],
                    help="worker slots in one skewed HBM arena, or separate allocations")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-scatter", action="store_true",
+                   help="N > 1: skip the config-4 RCCL scatter leg reported beside value")
     p.add_argument("--cpu-sample-mib", type=float, default=64.0,
                    help="bucket size of the CPU baseline sample")
     return p.parse_args()
@@ -124,6 +126,67 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
                       "reps": out["all"]["reps"]},
         "cpu_model": cpu_model, "host_cpus": ncpu,
     }
+
+
+def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
+                n_elems: int | None = None, fold=None) -> dict:
+    """BASELINE config 4 on the node the bench runs on (N > 1 only): N workers'
+    fp32 VGG-16 gradient vectors (553,430,176 B each) land on GPU 0; RCCL
+    grouped P2P over xGMI moves each owner its key-space slice
+    (ShardedReducer.scatter_reduce: the only data-path collective, SURVEY.md
+    §8e), the owner folds; then the all-gather return leg (core_loops.cc:
+    249-254).  Reported beside `value`, never as it.  Verified bit-exact on
+    GPU 0 against torch's own left fold of the whole vector."""
+    import torch
+    import torch.distributed as dist
+    from prophet_amd.buckets import vgg16_param_sizes
+    from prophet_amd.shard import ShardedReducer
+    E = n_elems or sum(vgg16_param_sizes())
+    sr = ShardedReducer(E, fold=fold)   # fold=None: the HIP fold (tests inject a CPU one)
+    root = 0
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4242)
+    pushes = [torch.randn(E, device=dev, generator=gen) for _ in range(n_workers)] \
+        if rank == root else None
+    recv = [torch.empty(sr.owned, device=dev) for _ in range(n_workers)]
+    owned = torch.empty(sr.owned, device=dev)
+    full = torch.empty(E, device=dev)
+
+    def timed(fn):
+        fn()
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        sync()
+        dist.barrier()
+        t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    t_scatter = timed(lambda: sr.scatter_reduce(root, pushes, recv, owned))
+    t_gather = timed(lambda: sr.allgather(owned, full))
+    ok = None
+    if rank == root:
+        ref = pushes[0].clone()
+        for p in pushes[1:]:
+            ref.add_(p)
+        ok = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
+    lo, hi = sr.ranges[root]
+    egress = n_workers * (E - (hi - lo)) * 4
+    return {"workload": f"{n_workers} x VGG-16-sized fp32 ({E * 4} B) landed on GPU 0, "
+                        f"RCCL P2P scatter to {world} owners + owner fold, then all-gather",
+            "scatter_fold_ms": round(t_scatter * 1e3, 3),
+            "root_egress_GBps": round(egress / t_scatter / 1e9, 1),
+            "allgather_ms": round(t_gather * 1e3, 3),
+            "node_fold_GiBps": round(n_workers * E * 4 / t_scatter / GIB, 1),
+            "exact_vs_torch_fold": ok}
 
 
 def pmc_traffic(workload: str):
@@ -225,10 +288,6 @@ def main():
         chk.add_(s.view(tdt)[: 1 << 20])
     ok = bool(torch.equal(chk.view(torch.uint8), dst[: chk.numel() * es])) if mode == 0 else None
 
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
     alg_bytes = (N + 1) * B
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload = f"{N}-way {args.dtype} left-fold sum of one {B / (1 << 20):.0f} MiB bucket per GPU"
@@ -259,14 +318,41 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 5)},
         "check_vs_torch_fold": ok,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1:
+        if rank == 0 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)
+            except Exception as e:  # report, never hide
+                line["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(line), flush=True)
+        return
+    # N > 1: the headline line is complete; the config-4 scatter leg runs after
+    # it under a watchdog, so a stuck or failing collective can cost only the
+    # extra field, never the line.
+    import threading
+    lock = threading.Lock()
+    state = {"printed": False}
+
+    def emit_and_maybe_exit(exit_now: bool):
+        with lock:
+            if rank == 0 and not state["printed"]:
+                print(json.dumps(line), flush=True)
+                state["printed"] = True
+        if exit_now:
+            os._exit(0)
+
+    watchdog = threading.Timer(180.0, lambda: (line.setdefault(
+        "scatter", {"error": "timed out after 180 s"}), emit_and_maybe_exit(True)))
+    watchdog.daemon = True
+    watchdog.start()
+    if not args.no_scatter:
         try:
-            line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)
+            line["scatter"] = scatter_leg(dev, world, rank, N)
         except Exception as e:  # report, never hide
-            line["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            line["scatter"] = {"error": repr(e)}
+    emit_and_maybe_exit(False)
+    dist.destroy_process_group()
+    watchdog.cancel()
 
 
 if __name__ == "__main__":

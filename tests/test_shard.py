@@ -161,3 +161,39 @@ def test_local_reduce_allreduce_rank_order_gloo(world):
     PortReducer().sum_n(want, ins, want.nbytes, DType.FLOAT16)
     for r in range(world):
         assert results[r] == want.tobytes(), f"rank {r}"
+
+
+def _worker_bench_leg(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        res = bench.scatter_leg(torch.device("cpu"), world, rank, 4, reps=2, n_elems=20_011,
+                                fold=_oracle_fold())
+        q.put((rank, res))
+    except Exception as e:      # fail fast instead of a queue timeout
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_scatter_leg_gloo(world):
+    """bench.py's config-4 leg (reported beside `value` at N > 1 GPUs): scatter
+    from GPU 0, owner fold, all-gather; the root's check against torch's left
+    fold passes and every rank reports the same max-over-ranks times."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_bench_leg, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert isinstance(results[r], dict), results[r]
+    assert results[0]["exact_vs_torch_fold"] is True
+    assert len({results[r]["scatter_fold_ms"] for r in range(world)}) == 1
