@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define BYTEPS_REDUCE_ABI_VERSION 1
+#define BYTEPS_REDUCE_ABI_VERSION 2
 
 /* Data type ids: byteps/common/common.h:52-65 (mshadow order), plus bf16 as a
  * build extension (the reference has none). */
@@ -79,7 +79,8 @@ enum byteps_reduce_status {
   BYTEPS_REDUCE_EDTYPE = -1,   /* unsupported data type                      */
   BYTEPS_REDUCE_EARGS = -2,    /* bad pointer / count / overlap / mode        */
   BYTEPS_REDUCE_EHIP = -3,     /* HIP runtime error (launch, copy, event)     */
-  BYTEPS_REDUCE_ERCCL = -4     /* collective error (reserved for shard APIs)  */
+  BYTEPS_REDUCE_ERCCL = -4,    /* collective error (reserved for shard APIs)  */
+  BYTEPS_REDUCE_ETIMEOUT = -5  /* a block queue launch gave up on a release   */
 };
 
 /* Most sources one kernel launch folds; byteps_reduce_sum_n chains launches
@@ -133,6 +134,42 @@ int byteps_reduce_plan_create(const byteps_bucket_desc* buckets, int nbuckets, i
                               int mode, byteps_reduce_plan** plan);
 int byteps_reduce_plan_launch(byteps_reduce_plan* plan, void* stream);
 int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
+
+/* Persistent block consumer: the buckets of one training iteration, grouped
+ * into Prophet blocks in release order (block i = buckets
+ * [block_end[i-1], block_end[i]), block_end[nblocks-1] == nbuckets), folded by
+ * ONE resident kernel per iteration instead of one launch per block.  The
+ * kernel takes tiles in table order and starts a block's tiles once that block
+ * and every block before it are released, so a block is folded as soon as its
+ * pushes have landed — no per-block launch, no per-block drain.  It replaces
+ * the per-block release loop of scheduled_queue.cc:244-296 followed by one
+ * reduce call per released partition.
+ *
+ *   launch(q, s)           enqueue the iteration's consumer on stream s;
+ *   release(q, b, s)       mark block b released once the work queued before it
+ *                          on stream s (e.g. the block's H2D pushes) has
+ *                          completed; b < 0 releases every block;
+ *   status(q, s)           synchronise s and report whether a launch gave up:
+ *                          a workgroup that waits longer than the timeout
+ *                          (default 2 s) for a release sets a sticky error, every
+ *                          workgroup then stops and status returns
+ *                          BYTEPS_REDUCE_ETIMEOUT (and clears it).
+ *
+ * Every block must be released in every iteration; the launch's last workgroup
+ * clears the releases, so releases for the next iteration must be ordered
+ * after this launch (same stream, or an event).  One launch of a queue at a
+ * time.  Table residency as for plans (buffers fixed after InitTensor). */
+typedef struct byteps_reduce_blockq byteps_reduce_blockq;
+int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
+                                const int* block_end, int nblocks, int dtype, int mode,
+                                byteps_reduce_blockq** q);
+/* Persistent workgroups per CU (1..8, default 1; <= 0 keeps) and the release
+ * timeout in seconds (<= 0 keeps). */
+int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s);
+int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream);
+int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* stream);
+int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream);
+int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
 
 /* CpuReducer::copy(dst, src, len), cpu_reducer.cc:209-220 (device to device). */
 int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream);

@@ -226,17 +226,25 @@ struct TableInfo {
 constexpr uint64_t kElemPart = (uint64_t)kBlock * 16;
 
 // Validate buckets and write [BatchEntry x live][pad to 256][TileRec x tiles]
-// into `out` (bpsr_internal.h: TileHead).
+// into `out` (bpsr_internal.h: TileHead).  With `block_end` (a block queue:
+// block i = buckets [block_end[i-1], block_end[i])), the records are laid out
+// block by block — each block's element tiles, then its vector tiles — and
+// `block_first` receives every block's first record (nblocks + 1 entries).
 static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
-                       std::vector<char>& out, TableInfo* ti) {
+                       std::vector<char>& out, TableInfo* ti, const int* block_end = nullptr,
+                       int nblocks = 0, std::vector<uint32_t>* block_first = nullptr,
+                       int force_vpt = 0) {
   std::vector<BatchEntry> tab;
+  std::vector<int> tab_block;  // block of each live bucket
   tab.reserve(nbuckets);
+  int blk = 0;
   uint64_t vecs = 0;
   int nmax = 1;
   for (int i = 0; i < nbuckets; ++i) {
     const byteps_bucket_desc& b = buckets[i];
     if (b.n < 1 || b.n > kMaxSrcs)
       return fail(BYTEPS_REDUCE_EARGS, "bucket %d: n=%d outside [1, %d]", i, b.n, kMaxSrcs);
+    while (block_end && blk < nblocks && i >= block_end[blk]) ++blk;
     if (b.len == 0) continue;
     if (!b.dst) return fail(BYTEPS_REDUCE_EARGS, "bucket %d: null dst", i);
     for (int k = 0; k < b.n; ++k) {
@@ -253,10 +261,11 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
     vecs += e.g.nvec;
     nmax = std::max(nmax, b.n);
     tab.push_back(e);
+    tab_block.push_back(blk);
   }
   // Same tile-size rule as a single fold (fold_vpt): the tuned vpt, halved
   // while the launch would have fewer than kMinTiles tiles.
-  const int vpt = fold_vpt(vecs, tuning_for_n(nmax).vpt);
+  const int vpt = force_vpt ? force_vpt : fold_vpt(vecs, tuning_for_n(nmax).vpt);
   const uint64_t tile_vecs = (uint64_t)kBlock * vpt;
   auto elem_parts = [](const BatchEntry& e) -> uint64_t {
     const uint64_t n_scalar = e.g.head_elems + (e.g.n_elems - e.g.tail_begin);
@@ -274,6 +283,7 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
   out.assign(recs_off + (size_t)stride * tiles, 0);
   if (!tab.empty()) std::memcpy(out.data(), tab.data(), sizeof(BatchEntry) * tab.size());
   char* rec = out.data() + recs_off;
+  uint32_t cur_block = 0;
   auto put = [&](unsigned char* dst, uint32_t kind, const BatchEntry& e, uint32_t a, uint32_t b,
                  uint32_t c, uint64_t byte0) {
     TileHead h;
@@ -284,25 +294,45 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
     h.a = a;
     h.b = b;
     h.c = c;
+    h.block = cur_block;
     std::memcpy(rec, &h, sizeof(h));
     const unsigned char** p = reinterpret_cast<const unsigned char**>(rec + kTileHeadBytes);
     for (int k = 0; k < e.n; ++k) p[k] = e.srcs[k] + byte0;
     rec += stride;
   };
-  // element tiles first: they are latency-bound and start with the launch
-  for (size_t b = 0; b < tab.size(); ++b) {
-    const uint64_t parts = elem_parts(tab[b]);
-    for (uint64_t q = 0; q < parts; ++q)
-      put(tab[b].dst, kTileElem, tab[b], (uint32_t)q, (uint32_t)b, (uint32_t)parts, 0);
-  }
-  for (size_t b = 0; b < tab.size(); ++b) {
-    const BatchEntry& e = tab[b];
-    for (uint64_t v0 = 0; v0 < e.g.nvec; v0 += tile_vecs) {
-      const uint64_t left = e.g.nvec - v0;
-      const bool full = left >= tile_vecs;
-      put(e.dst, full ? kTileFull : kTilePartial, e, full ? 0u : (uint32_t)left, (uint32_t)b, 0,
-          e.g.vec_off + v0 * 16);
+  // Records of the live buckets [b0, b1): element tiles first (they are
+  // latency-bound and start with the launch), then the vector tiles.
+  auto emit = [&](size_t b0, size_t b1) {
+    for (size_t b = b0; b < b1; ++b) {
+      const uint64_t parts = elem_parts(tab[b]);
+      for (uint64_t q = 0; q < parts; ++q)
+        put(tab[b].dst, kTileElem, tab[b], (uint32_t)q, (uint32_t)b, (uint32_t)parts, 0);
     }
+    for (size_t b = b0; b < b1; ++b) {
+      const BatchEntry& e = tab[b];
+      for (uint64_t v0 = 0; v0 < e.g.nvec; v0 += tile_vecs) {
+        const uint64_t left = e.g.nvec - v0;
+        const bool full = left >= tile_vecs;
+        put(e.dst, full ? kTileFull : kTilePartial, e, full ? 0u : (uint32_t)left, (uint32_t)b,
+            0, e.g.vec_off + v0 * 16);
+      }
+    }
+  };
+  char* const rec0 = rec;
+  if (!block_end) {
+    emit(0, tab.size());
+  } else {
+    block_first->assign((size_t)nblocks + 1, 0);
+    size_t b0 = 0;
+    for (int k = 0; k < nblocks; ++k) {
+      size_t b1 = b0;
+      while (b1 < tab.size() && tab_block[b1] == k) ++b1;
+      (*block_first)[k] = (uint32_t)((rec - rec0) / stride);
+      cur_block = (uint32_t)k;
+      emit(b0, b1);
+      b0 = b1;
+    }
+    (*block_first)[nblocks] = (uint32_t)tiles;
   }
   ti->vpt = vpt;
   ti->nmax = nmax;
@@ -514,6 +544,155 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* p) {
   if (p->dev_table) e = hipFree(p->dev_table);
   delete p;
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "plan free");
+}
+
+// ------------------------------------------------------------ block queue --
+struct byteps_reduce_blockq {
+  int device = 0;
+  int dtype = 0;
+  int mode = 0;
+  int nblocks = 0;
+  int occ = 1;               // persistent workgroups per CU (cfg3: 1 beats 2 and 4)
+  int cus = 0;
+  double timeout_s = 2.0;
+  uint64_t clock_khz = 0;    // wall_clock64() rate
+  void* dev_table = nullptr; // BatchEntry table + tile records
+  uint32_t* flags = nullptr; // [nblocks] release words, then [nblocks + 1] block_first
+  BlockqCtl* ctl = nullptr;
+  uint32_t* host_err = nullptr;  // pinned word for blockq_status
+  TableInfo ti;
+};
+
+static void blockq_free(byteps_reduce_blockq* q) {
+  if (q->dev_table) (void)hipFree(q->dev_table);
+  if (q->flags) (void)hipFree(q->flags);
+  if (q->ctl) (void)hipFree(q->ctl);
+  if (q->host_err) (void)hipHostFree(q->host_err);
+  delete q;
+}
+
+int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
+                                const int* block_end, int nblocks, int dtype, int mode,
+                                byteps_reduce_blockq** out) {
+  if (!out) return fail(BYTEPS_REDUCE_EARGS, "null block-queue out-pointer");
+  *out = nullptr;
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (nbuckets < 0 || (nbuckets > 0 && !buckets))
+    return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
+  if (nblocks < 1 || !block_end) return fail(BYTEPS_REDUCE_EARGS, "need >= 1 block");
+  for (int k = 0; k < nblocks; ++k) {
+    const int lo = k ? block_end[k - 1] : 0;
+    if (block_end[k] < lo || block_end[k] > nbuckets)
+      return fail(BYTEPS_REDUCE_EARGS, "block_end[%d]=%d not in [%d, %d]", k, block_end[k], lo,
+                  nbuckets);
+  }
+  if (block_end[nblocks - 1] != nbuckets)
+    return fail(BYTEPS_REDUCE_EARGS, "last block ends at %d, not at nbuckets=%d",
+                block_end[nblocks - 1], nbuckets);
+  std::vector<char> host;
+  std::vector<uint32_t> first;
+  TableInfo ti;
+  int force_vpt = 0;  // tile size override for measurements (default: the fold rule)
+  if (const char* v = getenv("BPSR_BQ_VPT")) force_vpt = atoi(v);
+  if (force_vpt != 1 && force_vpt != 2 && force_vpt != 4) force_vpt = 0;
+  if ((rc = build_table(buckets, nbuckets, dtype, host, &ti, block_end, nblocks, &first,
+                        force_vpt)))
+    return rc;
+  auto* q = new byteps_reduce_blockq();
+  q->dtype = dtype;
+  q->mode = mode;
+  q->nblocks = nblocks;
+  q->ti = ti;
+  int khz = 0;
+  hipError_t e = hipGetDevice(&q->device);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&q->cus, hipDeviceAttributeMultiprocessorCount, q->device);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, q->device);
+  q->clock_khz = khz > 0 ? (uint64_t)khz : 100000;
+  const size_t flag_bytes = sizeof(uint32_t) * (2 * (size_t)nblocks + 1);
+  if (e == hipSuccess && ti.tiles > 0) e = hipMalloc(&q->dev_table, ti.bytes);
+  if (e == hipSuccess && ti.tiles > 0)
+    e = hipMemcpy(q->dev_table, host.data(), ti.bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->flags), flag_bytes);
+  if (e == hipSuccess) e = hipMemset(q->flags, 0, sizeof(uint32_t) * nblocks);
+  if (e == hipSuccess)
+    e = hipMemcpy(q->flags + nblocks, first.data(), sizeof(uint32_t) * (nblocks + 1),
+                  hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->ctl), sizeof(BlockqCtl));
+  if (e == hipSuccess) e = hipMemset(q->ctl, 0, sizeof(BlockqCtl));
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&q->host_err), sizeof(uint32_t));
+  if (e != hipSuccess) {
+    blockq_free(q);
+    return hip_fail(e, "block queue setup");
+  }
+  *out = q;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (wg_per_cu > 8) return fail(BYTEPS_REDUCE_EARGS, "wg_per_cu %d > 8", wg_per_cu);
+  if (wg_per_cu > 0) q->occ = wg_per_cu;
+  if (timeout_s > 0) q->timeout_s = timeout_s;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (q->ti.tiles == 0) return BYTEPS_REDUCE_OK;
+  BlockqLaunch Q;
+  Q.L = batch_launch(q->dev_table, q->ti);
+  Q.flags = q->flags;
+  Q.block_first = q->flags + q->nblocks;
+  Q.ctl = q->ctl;
+  Q.nblocks = (uint32_t)q->nblocks;
+  const uint64_t cap = (uint64_t)q->cus * (uint64_t)q->occ;
+  Q.grid = (uint32_t)std::min<uint64_t>(q->ti.tiles, cap);
+  Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
+  Q.pad[0] = Q.pad[1] = 0;
+  // residency cap through LDS (the kernel's own 20 B of static LDS included)
+  const size_t lds = q->occ > 0 ? ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255 : 0;
+  const Tuning tu = tuning_for_n(q->ti.nmax);
+  hipError_t e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, q->dtype, q->mode,
+                               to_stream(stream));
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
+}
+
+int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* stream) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (block >= q->nblocks) return fail(BYTEPS_REDUCE_EARGS, "block %d >= %d", block, q->nblocks);
+  hipStream_t s = to_stream(stream);
+  // A one-wave kernel storing the words at system scope (write-through); a
+  // hipMemset node was not seen by the consumer's polls under graph replay, and
+  // hipStreamWriteValue32 measured slower for per-block releases.
+  hipError_t e = block < 0 ? launch_blockq_release(q->flags, (uint32_t)q->nblocks, s)
+                           : launch_blockq_release(q->flags + block, 1, s);
+  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block release");
+}
+
+int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  hipStream_t s = to_stream(stream);
+  hipError_t e = hipMemcpyAsync(q->host_err, &q->ctl->err, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "block queue status");
+  if (*q->host_err == 0) return BYTEPS_REDUCE_OK;
+  e = hipMemsetAsync(&q->ctl->err, 0, sizeof(uint32_t), s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "block queue status reset");
+  return fail(BYTEPS_REDUCE_ETIMEOUT,
+              "block queue: a block was not released within %.3f s; the launch stopped early",
+              q->timeout_s);
+}
+
+int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q) {
+  if (!q) return BYTEPS_REDUCE_OK;
+  blockq_free(q);
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream) {

@@ -67,7 +67,7 @@ struct TileHead {
   uint32_t a;          // partial: valid vectors; element: part index
   uint32_t b;          // element: bucket index into the BatchEntry table
   uint32_t c;          // element: parts of this bucket's element work
-  uint32_t pad;
+  uint32_t block;      // block queue: the release block this tile belongs to
 };
 constexpr uint32_t kTileHeadBytes = 32;
 static_assert(sizeof(TileHead) == kTileHeadBytes, "TileHead layout");
@@ -80,6 +80,29 @@ struct BatchLaunch {
   const BatchEntry* entries;    // per-bucket geometry
   uint32_t rec_stride;
   uint32_t tiles;
+};
+
+// Persistent block consumer (byteps_reduce_blockq_*).  One launch folds the
+// whole table; resident workgroups sweep the tiles in table order, and a
+// workgroup starts a tile only once the tile's block and every block before it
+// have been released (flags[b] != 0, written stream-ordered by
+// byteps_reduce_blockq_release).
+// The launch's last workgroup re-arms the queue (flags, done counter).
+struct BlockqCtl {
+  uint32_t pad0;
+  uint32_t done;  // workgroups finished in this launch
+  uint32_t err;   // sticky: a workgroup gave up waiting for a release
+  uint32_t pad;
+};
+struct BlockqLaunch {
+  BatchLaunch L;
+  uint32_t* flags;              // one word per block, != 0 = released
+  const uint32_t* block_first;  // first tile of each block, [nblocks] = tiles
+  BlockqCtl* ctl;
+  uint32_t nblocks;
+  uint32_t grid;            // launched (persistent) workgroups
+  uint64_t timeout_ticks;   // wall_clock64() ticks a workgroup waits for a release
+  uint32_t pad[2];
 };
 
 struct Tuning {
@@ -146,7 +169,9 @@ inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
 #define BPSR_DECLARE_LAUNCHERS(NAME)                                                      \
   hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s);      \
   hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
-                                   hipStream_t s);
+                                   hipStream_t s);                                        \
+  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
+                                  hipStream_t s);
 BPSR_DECLARE_LAUNCHERS(f32)
 BPSR_DECLARE_LAUNCHERS(f64)
 BPSR_DECLARE_LAUNCHERS(f16)
@@ -161,6 +186,9 @@ hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);
 hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, const Tuning& tu,
                           hipStream_t s);
+hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, int dtype, int mode,
+                         hipStream_t s);
+hipError_t launch_blockq_release(uint32_t* flags, uint32_t count, hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.

@@ -86,4 +86,37 @@ hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, co
   }
 }
 
+// Block-queue release: flags[first .. first+count) = 1 by system-scope atomic
+// stores, so the consumer's system-scope polls see them whatever cache the
+// writer ran behind (a hipMemset node inside a replayed hipGraph was not seen).
+__global__ void blockq_release_kernel(uint32_t* flags, uint32_t count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) __hip_atomic_store(flags + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_blockq_release(uint32_t* flags, uint32_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(blockq_release_kernel, dim3((count + 63) / 64), dim3(64), 0, s, flags, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, int dtype, int mode,
+                         hipStream_t s) {
+  const bool acc = mode == kModeAccumF32;
+  switch (dtype) {
+    case kFloat32: return launch_blockq_f32(Q, vpt, nt, lds, s);
+    case kFloat64: return launch_blockq_f64(Q, vpt, nt, lds, s);
+    case kFloat16:
+      return acc ? launch_blockq_f16acc(Q, vpt, nt, lds, s) : launch_blockq_f16(Q, vpt, nt, lds, s);
+    case kBFloat16:
+      return acc ? launch_blockq_bf16acc(Q, vpt, nt, lds, s)
+                 : launch_blockq_bf16(Q, vpt, nt, lds, s);
+    case kUInt8:
+    case kInt8: return launch_blockq_i8(Q, vpt, nt, lds, s);
+    case kInt32: return launch_blockq_i32(Q, vpt, nt, lds, s);
+    case kInt64: return launch_blockq_i64(Q, vpt, nt, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace bpsr

@@ -163,10 +163,18 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
 // based at the tile's first byte (wave-uniform: kernel arguments + blockIdx),
 // 32-bit lane offsets, nt as the cache-policy operand.  Same load grouping,
 // fast fold and NaN replay as fold_tile_body.
-template <class Op, int VPT, bool NT, int NS>
+// `mid` runs once the tile's loads have all been consumed and before its
+// stores issue (blockq_kernel consumes its prefetched work-queue values there,
+// where they are complete, so nothing is left pending across the stores).
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+template <class Op, int VPT, bool NT, int NS, class Mid = NoMid>
 __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs,
                                                    const unsigned char* const* xsrcs, int n,
-                                                   unsigned char* dst, uint64_t byte0, int lane) {
+                                                   unsigned char* dst, uint64_t byte0, int lane,
+                                                   const Mid& mid = Mid()) {
   constexpr int kAux = NT ? 2 : 0;               // 2 = nt
   constexpr int kTileBytes = kBlock * VPT * 16;
   constexpr int NSA = NS < 0 ? -NS : NS;
@@ -209,6 +217,7 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
   } else {
     for (int k0 = 0; k0 < ns; k0 += G) group(k0);
   }
+  mid();
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < VPT; ++j) bad = bad || Op::has_nan(acc[j]);
@@ -325,40 +334,197 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
     fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0, threadIdx.x, kBlock);
 }
 
-// Batched: workgroup b runs record b of the launch (TileHead, bpsr_internal.h).
-// Its head and first 8 source pointers are pinned into SGPRs by one empty asm,
-// so they arrive in one scalar round trip; vector tiles then go straight to
-// their data (pointers pre-advanced to the tile).  Element tiles fetch their
-// bucket's geometry from the entry table and stride over its element work.
-template <class Op, int VPT, bool NT>
-__global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
-  const unsigned char* rec = L.recs + (uint64_t)blockIdx.x * L.rec_stride;
+// One tile record of a batched table (TileHead, bpsr_internal.h), already in
+// registers: the head, the first 8 source pointers (wave-uniform, SGPRs) and
+// the record's pointer array `msrcs` (for n > 8 and the exact NaN replay).
+// Vector tiles go straight to their data (pointers pre-advanced to the tile);
+// element tiles fetch their bucket's geometry from the entry table and stride
+// over its element work.
+struct RecRegs {
+  unsigned char* dst;
+  uint32_t kind, n, a, b, c;
+  const unsigned char* p[8];
+};
+
+template <class Op, int VPT, bool NT, class Mid = NoMid>
+__device__ __forceinline__ void run_record(const RecRegs& r, const unsigned char* const* msrcs,
+                                           const BatchEntry* entries, const Mid& mid = Mid()) {
+  if (r.kind == kTileElem) {
+    const BatchEntry& e = entries[r.b];
+    fold_elements<Op>(e.srcs, e.n, e.dst, e.g, e.aligned != 0,
+                      (uint64_t)r.a * kBlock + threadIdx.x, (uint64_t)r.c * kBlock);
+    mid();
+  } else if (r.n <= 8) {
+    if (r.kind == kTileFull) {
+      fold_tile_full_buf<Op, VPT, NT, -8>(r.p, msrcs, (int)r.n, r.dst, 0, threadIdx.x, mid);
+    } else {
+      fold_tile_body<Op, VPT, NT, -8, true>(r.p, msrcs, (int)r.n, r.dst, 0, 0, r.a, threadIdx.x);
+      mid();
+    }
+  } else {
+    if (r.kind == kTileFull) {
+      fold_tile_full_buf<Op, VPT, NT, 0>(msrcs, msrcs, (int)r.n, r.dst, 0, threadIdx.x, mid);
+    } else {
+      fold_tile_body<Op, VPT, NT, 0, true>(msrcs, msrcs, (int)r.n, r.dst, 0, 0, r.a,
+                                           threadIdx.x);
+      mid();
+    }
+  }
+}
+
+// Read a record's head + 8 pointers in C++: the compiler emits scalar loads
+// when nothing in the kernel can have written the table before (batched_kernel),
+// and one empty asm pins them so they issue together (one scalar round trip).
+__device__ __forceinline__ RecRegs load_record(const unsigned char* rec) {
   const TileHead& h = *reinterpret_cast<const TileHead*>(rec);
   const unsigned char* const* msrcs =
       reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes);
-  // Read the head and 8 pointers into registers before anything else (scalar
-  // loads: nothing has been stored yet), then pin them so they issue together.
-  unsigned char* const dst = h.dst;
-  const uint32_t kind = h.kind, n = h.n, a = h.a, b = h.b, c = h.c;
-  const unsigned char* p[8];
+  RecRegs r;
+  r.dst = h.dst;
+  r.kind = h.kind;
+  r.n = h.n;
+  r.a = h.a;
+  r.b = h.b;
+  r.c = h.c;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) p[k] = msrcs[k];
-  asm volatile("" ::"s"(dst), "s"(kind), "s"(n), "s"(a), "s"(p[0]), "s"(p[1]), "s"(p[2]),
-               "s"(p[3]), "s"(p[4]), "s"(p[5]), "s"(p[6]), "s"(p[7]));
-  if (kind == kTileElem) {
-    const BatchEntry& e = L.entries[b];
-    fold_elements<Op>(e.srcs, e.n, e.dst, e.g, e.aligned != 0,
-                      (uint64_t)a * kBlock + threadIdx.x, (uint64_t)c * kBlock);
-  } else if (n <= 8) {
-    if (kind == kTileFull)
-      fold_tile_full_buf<Op, VPT, NT, -8>(p, msrcs, (int)n, dst, 0, threadIdx.x);
-    else
-      fold_tile_body<Op, VPT, NT, -8, true>(p, msrcs, (int)n, dst, 0, 0, a, threadIdx.x);
-  } else {
-    if (kind == kTileFull)
-      fold_tile_full_buf<Op, VPT, NT, 0>(msrcs, msrcs, (int)n, dst, 0, threadIdx.x);
-    else
-      fold_tile_body<Op, VPT, NT, 0, true>(msrcs, msrcs, (int)n, dst, 0, 0, a, threadIdx.x);
+  for (int k = 0; k < 8; ++k) r.p[k] = msrcs[k];
+  asm volatile("" ::"s"(r.dst), "s"(r.kind), "s"(r.n), "s"(r.a), "s"(r.p[0]), "s"(r.p[1]),
+               "s"(r.p[2]), "s"(r.p[3]), "s"(r.p[4]), "s"(r.p[5]), "s"(r.p[6]), "s"(r.p[7]));
+  return r;
+}
+
+// A record's head + 8 pointers as 24 words staged in LDS (blockq_kernel
+// prefetches the next tile's record there while the current tile streams):
+// uniform LDS reads, then SGPRs.
+constexpr int kRecWords = (kTileHeadBytes + 8 * 8) / 4;
+__device__ __forceinline__ RecRegs regs_from_words(const uint32_t* w) {
+  uint32_t v[kRecWords];
+#pragma unroll
+  for (int k = 0; k < kRecWords; ++k) v[k] = __builtin_amdgcn_readfirstlane(w[k]);
+  auto ptr = [&](int k) {
+    return reinterpret_cast<unsigned char*>(((uint64_t)v[k + 1] << 32) | v[k]);
+  };
+  RecRegs r;
+  r.dst = ptr(0);
+  r.kind = v[2];
+  r.n = v[3];
+  r.a = v[4];
+  r.b = v[5];
+  r.c = v[6];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.p[k] = ptr(8 + 2 * k);
+  return r;
+}
+
+// Batched: workgroup b runs record b of the launch.
+template <class Op, int VPT, bool NT>
+__global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
+  const unsigned char* rec = L.recs + (uint64_t)blockIdx.x * L.rec_stride;
+  run_record<Op, VPT, NT>(load_record(rec),
+                          reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes),
+                          L.entries);
+}
+
+// Persistent block consumer (byteps_reduce_blockq_*).  Q.grid resident
+// workgroups sweep the tile records of the whole table in order — workgroup w
+// takes tiles w, w + grid, w + 2*grid, ... — so the chip still streams the
+// table as one advancing window, across block boundaries, with no launch
+// boundary between blocks.  The record of the next tile is loaded while the
+// current tile streams (every thread one word, staged in LDS) and consumed
+// (`mid`) right after the tile's loads, before its stores: nothing is left
+// pending across the stores, so the next tile's loads issue while the stores
+// drain.  (A work-queue atomic in place of the static order put a vmcnt(0)
+// at the top of every iteration — the returned-atomic register's write-after-
+// write guard — and so an HBM write round trip per tile.)
+// Blocks are consumed in table order: a workgroup may start tile t once every
+// block up to t's is released.  It keeps the first tile past the released
+// prefix it last saw (`ready_tiles`), so a tile costs one compare unless it
+// crosses that mark; then wave 0 scans the flags 64 at a time (one load per
+// lane), sleeping between polls, and the workgroup acquires at system scope
+// (the data may have landed by DMA or from another queue).  Every wave reaches
+// the exit: all its tiles done, or a release that does not come within
+// Q.timeout_ticks sets the sticky ctl->err, which every waiting workgroup sees
+// on its next poll.  The last workgroup to finish re-arms the queue.  Every
+// access to the flags is a system-scope atomic (releases: blockq_release_kernel).
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <class Op, int VPT, bool NT>
+__global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
+  // record slots alternate: iteration i reads slot i&1 and stages the next
+  // record into the other one, so no wave overwrites a record still being read
+  __shared__ __attribute__((aligned(16))) uint32_t s_rec[2][kRecWords];
+  __shared__ uint32_t s_ready, s_ready_tiles, s_abort;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t tw = tid % (uint32_t)kRecWords;
+  auto rec_at = [&](uint32_t t) { return Q.L.recs + (uint64_t)t * Q.L.rec_stride; };
+  if (blockIdx.x < Q.L.tiles)
+    s_rec[0][tw] = reinterpret_cast<const uint32_t*>(rec_at(blockIdx.x))[tw];
+  __syncthreads();
+  uint32_t ready = 0, ready_tiles = 0;  // blocks [0, ready) = tiles [0, ready_tiles) released
+  uint32_t it = 0;
+  for (uint32_t t = blockIdx.x; t < Q.L.tiles; t += Q.grid, ++it) {
+    if (t >= ready_tiles) {
+      if (tid < 64) {
+        const uint32_t lane = tid;
+        uint32_t r = ready, rt = ready_tiles;
+        bool abort = false;
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+          const uint32_t b = r + lane;
+          const bool rel = b >= Q.nblocks || ld_sys(Q.flags + b) != 0;
+          const uint64_t pending = __ballot(!rel);
+          const uint32_t r2 = pending == 0 ? (r + 64 < Q.nblocks ? r + 64 : Q.nblocks)
+                                           : r + (uint32_t)__builtin_ctzll(pending);
+          if (r2 != r) {
+            r = r2;
+            rt = Q.block_first[r];
+          }
+          if (rt > t) break;
+          if (pending == 0) continue;  // next chunk of flags
+          if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            abort = true;
+            break;
+          }
+          if (wall_clock64() - t0 > Q.timeout_ticks) {
+            if (lane == 0)
+              __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            abort = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+        if (lane == 0) {
+          s_ready = r;
+          s_ready_tiles = rt;
+          s_abort = abort ? 1u : 0u;
+        }
+      }
+      __syncthreads();
+      if (s_abort) break;
+      ready = __builtin_amdgcn_readfirstlane(s_ready);
+      ready_tiles = __builtin_amdgcn_readfirstlane(s_ready_tiles);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    const uint32_t tn = t + Q.grid;
+    const uint32_t w = reinterpret_cast<const uint32_t*>(rec_at(tn < Q.L.tiles ? tn : t))[tw];
+    const uint32_t nslot = (it + 1) & 1;
+    auto mid = [&]() __attribute__((always_inline)) { s_rec[nslot][tw] = w; };
+    run_record<Op, VPT, NT>(regs_from_words(s_rec[it & 1]),
+                            reinterpret_cast<const unsigned char* const*>(rec_at(t) +
+                                                                          kTileHeadBytes),
+                            Q.L.entries, mid);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (atomicAdd(&Q.ctl->done, 1u) == Q.grid - 1) {
+      // every other workgroup has finished: re-arm
+      for (uint32_t b = 0; b < Q.nblocks; ++b)
+        __hip_atomic_store(Q.flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&Q.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -430,6 +596,32 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
   }
 }
 
+template <class Op, int VPT, bool NT>
+static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, hipStream_t s) {
+  // the kernel's own static LDS (the tile broadcast words) comes on top of the
+  // dynamic residency request, so allow 256 B less than the CU's 160 KiB
+  static const hipError_t ok =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&blockq_kernel<Op, VPT, NT>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCU - 256);
+  if (ok != hipSuccess) return ok;
+  hipLaunchKernelGGL((blockq_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
+  return hipGetLastError();
+}
+
+template <class Op>
+static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,
+                                   hipStream_t s) {
+  if (Q.grid == 0) return hipSuccess;
+  switch (vpt * 2 + (nt ? 1 : 0)) {
+    case 2: return launch_blockq_k<Op, 1, false>(Q, lds, s);
+    case 3: return launch_blockq_k<Op, 1, true>(Q, lds, s);
+    case 4: return launch_blockq_k<Op, 2, false>(Q, lds, s);
+    case 8: return launch_blockq_k<Op, 4, false>(Q, lds, s);
+    case 9: return launch_blockq_k<Op, 4, true>(Q, lds, s);
+    default: return launch_blockq_k<Op, 2, true>(Q, lds, s);
+  }
+}
+
 }  // namespace bpsr
 
 // One translation unit per dtype family defines its entry points with this.
@@ -441,5 +633,9 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
   hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
                                    hipStream_t s) {                                       \
     return launch_batched_op<OP>(L, vpt, tu, s);                                          \
+  }                                                                                       \
+  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
+                                  hipStream_t s) {                                        \
+    return launch_blockq_op<OP>(Q, vpt, nt, lds, s);                                      \
   }                                                                                       \
   }

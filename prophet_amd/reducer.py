@@ -36,7 +36,7 @@ MAX_SRCS = 32
 MODE_REFERENCE = 0
 MODE_ACCUM_F32 = 1
 
-OK, EDTYPE, EARGS, EHIP, ERCCL = 0, -1, -2, -3, -4
+OK, EDTYPE, EARGS, EHIP, ERCCL, ETIMEOUT = 0, -1, -2, -3, -4, -5
 
 _vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
 
@@ -48,6 +48,8 @@ EXPORTS = (
     "byteps_reduce_dtype_size", "byteps_reduce_last_error",
     "byteps_reduce_set_tuning", "byteps_reduce_get_tuning",
     "byteps_reduce_plan_create", "byteps_reduce_plan_launch", "byteps_reduce_plan_destroy",
+    "byteps_reduce_blockq_create", "byteps_reduce_blockq_config", "byteps_reduce_blockq_launch",
+    "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
 )
 
 
@@ -92,6 +94,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                             ctypes.POINTER(_vp)]
     L.byteps_reduce_plan_launch.argtypes = [_vp, _vp]
     L.byteps_reduce_plan_destroy.argtypes = [_vp]
+    L.byteps_reduce_blockq_create.argtypes = [ctypes.POINTER(BucketDesc), _int,
+                                              ctypes.POINTER(_int), _int, _int, _int,
+                                              ctypes.POINTER(_vp)]
+    L.byteps_reduce_blockq_config.argtypes = [_vp, _int, ctypes.c_double]
+    L.byteps_reduce_blockq_launch.argtypes = [_vp, _vp]
+    L.byteps_reduce_blockq_release.argtypes = [_vp, _int, _vp]
+    L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
+    L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     _LIB = L
     return L
 
@@ -176,6 +186,14 @@ class GpuReducer:
         alive (and at the same addresses) for the plan's lifetime."""
         return Plan(self.lib, buckets, dtype, mode)
 
+    def make_blockq(self, blocks: Sequence[Sequence[tuple]], dtype: int,
+                    mode: int = MODE_REFERENCE) -> "BlockQueue":
+        """One iteration's Prophet blocks (in release order; each a list of
+        ``(dst, srcs, length)`` buckets) folded by ONE persistent launch per
+        iteration that starts each block once it is released
+        (``byteps_reduce_blockq_*``)."""
+        return BlockQueue(self.lib, blocks, dtype, mode)
+
     def sync(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_sync(_stream_of(None, stream)))
 
@@ -223,6 +241,55 @@ class Plan:
     def close(self) -> None:
         if self.handle:
             self.lib.byteps_reduce_plan_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BlockQueue:
+    """``byteps_reduce_blockq``: a persistent consumer over an iteration's blocks.
+
+    Per iteration: ``launch()`` once, then ``release(b)`` for every block (in
+    any stream order; a block is consumed once it and all earlier blocks are
+    released), ``status()`` to learn whether the launch gave up waiting."""
+
+    def __init__(self, lib, blocks, dtype, mode):
+        self.lib = lib
+        self.handle = _vp()
+        buckets = [b for blk in blocks for b in blk]
+        ends, acc = [], 0
+        for blk in blocks:
+            acc += len(blk)
+            ends.append(acc)
+        self.nblocks = len(blocks)
+        self._keep = buckets
+        self.first = buckets[0][0] if buckets else None
+        arr = (_int * max(1, len(ends)))(*ends)
+        _check(lib.byteps_reduce_blockq_create(_descs(buckets), len(buckets), arr, len(ends),
+                                               int(dtype), int(mode),
+                                               ctypes.byref(self.handle)))
+
+    def config(self, wg_per_cu: int = 0, timeout_s: float = 0.0) -> None:
+        _check(self.lib.byteps_reduce_blockq_config(self.handle, int(wg_per_cu),
+                                                    float(timeout_s)))
+
+    def launch(self, stream=None) -> None:
+        _check(self.lib.byteps_reduce_blockq_launch(self.handle, _stream_of(self.first, stream)))
+
+    def release(self, block: int = -1, stream=None) -> None:
+        _check(self.lib.byteps_reduce_blockq_release(self.handle, int(block),
+                                                     _stream_of(self.first, stream)))
+
+    def status(self, stream=None) -> None:
+        _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.byteps_reduce_blockq_destroy(self.handle)
             self.handle = _vp()
 
     def __del__(self):

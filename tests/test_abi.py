@@ -42,7 +42,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_dtype_sizes():
     lib = reducer.load_library()
-    assert lib.byteps_reduce_version() == 1
+    assert lib.byteps_reduce_version() == 2
     for dt in ALL_DTYPES:
         assert lib.byteps_reduce_dtype_size(int(dt)) == elem_size(dt)
     assert lib.byteps_reduce_dtype_size(7) == reducer.EDTYPE

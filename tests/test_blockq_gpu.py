@@ -1,0 +1,245 @@
+"""GPU parity of the persistent block consumer (byteps_reduce_blockq_*).
+
+One launch per iteration folds every block of the table, starting each block
+once it (and every block before it) is released.  Bar: bit-exact with the CPU
+oracle for every block, in every iteration, whichever way the blocks are
+released (all up front, one by one from another stream after their pushes
+land by DMA, from a captured hipGraph), and a launch whose releases never come
+stops by itself and reports BYTEPS_REDUCE_ETIMEOUT.
+"""
+import numpy as np
+import pytest
+
+from oracle.oracle import PortReducer
+from prophet_amd import synth
+from prophet_amd.dtypes import DType, elem_size
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def red(dev):
+    from prophet_amd.reducer import GpuReducer
+    return GpuReducer(device=0)
+
+
+@pytest.fixture(scope="module")
+def port():
+    return PortReducer(nthreads=8)
+
+
+class Table:
+    """Receive slots + outputs for a list of blocks of (n_elems, n_sources, class)."""
+
+    def __init__(self, dev, dt, blocks, offsets=False):
+        self.dt, self.es = dt, elem_size(dt)
+        self.blocks = []     # per block: list of (dst, [srcs], len)
+        self.views = []      # flat: (dst tensor, [src tensors], len, n_elems, N, class)
+        for bi, blk in enumerate(blocks):
+            out = []
+            for ne, N, cls in blk:
+                L = ne * self.es
+                o = (self.es * (len(self.views) % 3)) if offsets else 0
+                srcs = [torch.empty(L + 16, dtype=torch.uint8, device=dev)[o:o + L]
+                        for _ in range(N)]
+                dst = torch.full((L + 16,), 0x5A, dtype=torch.uint8, device=dev)[o:o + L]
+                out.append((dst, srcs, L))
+                self.views.append((dst, srcs, L, ne, N, cls))
+            self.blocks.append(out)
+
+    def host_inputs(self, seed):
+        """Pinned host pushes and the oracle's fold of every bucket."""
+        pushes, wants = [], []
+        for i, (dst, srcs, L, ne, N, cls) in enumerate(self.views):
+            ins = [np.ascontiguousarray(synth.bucket(self.dt, ne, k, cls, seed + i)).view(np.uint8)
+                   for k in range(N)]
+            pushes.append([torch.from_numpy(x).pin_memory() for x in ins])
+            w = np.full(L, 0x5A, np.uint8)
+            if L:
+                PortReducer(nthreads=8).sum_n(w, ins, L, self.dt)
+            wants.append(w)
+        return pushes, wants
+
+    def upload(self, pushes, stream=None):
+        for (dst, srcs, L, *_), ps in zip(self.views, pushes):
+            for s, p in zip(srcs, ps):
+                if L:
+                    s.copy_(p, non_blocking=True)
+
+    def check(self, wants):
+        for i, ((dst, _, L, *_), w) in enumerate(zip(self.views, wants)):
+            got = dst.cpu().numpy()
+            if not np.array_equal(got, w):
+                bad = np.flatnonzero(got != w)
+                raise AssertionError(f"bucket {i}: {len(bad)} bytes differ, first at {bad[0]}")
+
+
+# ragged buckets, an empty block, element-only buckets, > 8 sources
+MIXED = [
+    [(100_000, 8, "special"), (4099, 9, "normal"), (1, 1, "normal")],
+    [],
+    [(70_001, 32, "bits"), (0, 8, "normal"), (257, 12, "special")],
+    [(300_000, 5, "normal")],
+    [(9, 8, "bits"), (3 * 1024 + 5, 2, "normal"), (1 << 20, 8, "normal")],
+]
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.BFLOAT16, DType.INT32,
+                                DType.FLOAT64, DType.UINT8], ids=lambda d: DType(d).name)
+def test_release_all_three_iterations(red, dev, dt):
+    """Release every block up front; the queue re-arms itself between launches."""
+    tab = Table(dev, dt, MIXED, offsets=True)
+    q = red.make_blockq(tab.blocks, dt)
+    for it in range(3):
+        pushes, wants = tab.host_inputs(100 * it + 7)
+        tab.upload(pushes)
+        torch.cuda.synchronize()
+        q.release(-1)
+        q.launch()
+        q.status()
+        torch.cuda.synchronize()
+        tab.check(wants)
+    q.close()
+
+
+@pytest.mark.parametrize("occ", [1, 2, 4])
+def test_live_release_after_dma(red, dev, occ):
+    """The consumer is launched first; a copy stream then pushes each block's
+    data by H2D DMA and releases the block behind it.  Every block must see
+    its own freshly landed bytes (acquire after the release), over iterations
+    whose data differ."""
+    from prophet_amd.buckets import resnet50_param_sizes, prophet_blocks
+    dt = DType.FLOAT16
+    sizes = resnet50_param_sizes()
+    groups = prophet_blocks(len(sizes))
+    # every ResNet-50 gradient of every block, at a quarter of its size (test time)
+    blocks = [[(max(1, sizes[i] // 4), 8, "normal") for i in g] for g in groups]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=occ, timeout_s=5.0)
+    comp, copy = torch.cuda.Stream(), torch.cuda.Stream()
+    for it in range(2):
+        pushes, wants = tab.host_inputs(1000 * it + 3)
+        torch.cuda.synchronize()
+        q.launch(comp)
+        k = 0
+        with torch.cuda.stream(copy):
+            for b, blk in enumerate(tab.blocks):
+                for dst, srcs, L in blk:
+                    for s, p in zip(srcs, pushes[k]):
+                        s.copy_(p, non_blocking=True)
+                    k += 1
+                q.release(b, copy)
+        comp.synchronize()
+        copy.synchronize()
+        q.status(comp)
+        tab.check(wants)
+    q.close()
+
+
+def test_out_of_order_release_waits_for_prefix(red, dev):
+    """Blocks released last-to-first from a side stream: nothing past an
+    unreleased block is started, and the result is still exact."""
+    dt = DType.FLOAT32
+    blocks = [[(200_000 + 17 * b, 8, "normal")] for b in range(6)]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    pushes, wants = tab.host_inputs(55)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    comp, side = torch.cuda.Stream(), torch.cuda.Stream()
+    q.launch(comp)
+    for b in reversed(range(len(blocks))):
+        q.release(b, side)
+    comp.synchronize()
+    q.status(comp)
+    tab.check(wants)
+    q.close()
+
+
+def test_missing_release_times_out_and_recovers(red, dev):
+    """Blocks 0-1 released, block 2 never: the launch gives up after its
+    timeout, reports ETIMEOUT once, has folded the released blocks, and the
+    queue works normally afterwards."""
+    from prophet_amd.reducer import ETIMEOUT, ReduceError
+    dt = DType.FLOAT32
+    blocks = [[(500_000, 8, "normal")], [(123_457, 8, "normal")], [(400_000, 8, "normal")],
+              [(1000, 8, "normal")]]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    q.config(timeout_s=0.2)
+    pushes, wants = tab.host_inputs(77)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    q.release(0, s)
+    q.release(1, s)
+    q.launch(s)
+    with pytest.raises(ReduceError) as ei:
+        q.status(s)
+    assert ei.value.code == ETIMEOUT
+    for i in (0, 1):
+        assert np.array_equal(tab.views[i][0].cpu().numpy(), wants[i])
+    q.status(s)  # cleared
+    q.release(-1, s)
+    q.launch(s)
+    q.status(s)
+    tab.check(wants)
+    q.close()
+
+
+def test_graph_replay_matches_plans(red, dev, port):
+    """Release + launch captured into a hipGraph and replayed on new data:
+    bit-identical with one plan per block (ResNet-50 fp16 Prophet blocks)."""
+    from prophet_amd.buckets import resnet50_param_sizes, prophet_blocks
+    dt = DType.FLOAT16
+    sizes = resnet50_param_sizes()
+    groups = prophet_blocks(len(sizes))
+    blocks = [[(sizes[i], 8, "normal") for i in g] for g in groups]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        q.release(-1, side)
+        q.launch(side)
+    gen = torch.Generator(device=dev)
+    for it in range(2):
+        gen.manual_seed(it)
+        for dst, srcs, L, *_ in tab.views:
+            for s in srcs:
+                s.view(torch.float16).copy_(torch.randn(L // 2, generator=gen, device=dev))
+        g.replay()
+        torch.cuda.synchronize()
+        q.status()
+        got = [v[0].clone() for v in tab.views]
+        plans = [red.make_plan(blk, dt) for blk in tab.blocks]
+        for p in plans:
+            p.launch()
+        torch.cuda.synchronize()
+        for a, v in zip(got, tab.views):
+            assert torch.equal(a, v[0])
+        for p in plans:
+            p.close()
+    q.close()
+
+
+def test_bad_tables_rejected(red, dev):
+    from prophet_amd.reducer import EARGS, ReduceError
+    import ctypes
+    from prophet_amd.reducer import BucketDesc, _vp, _int
+    h = _vp()
+    descs = (BucketDesc * 1)()
+    for ends in ([2], [0, 2], []):
+        arr = (_int * max(1, len(ends)))(*ends)
+        rc = red.lib.byteps_reduce_blockq_create(descs, 1, arr, len(ends), 0, 0, ctypes.byref(h))
+        assert rc == EARGS
+    assert red.lib.byteps_reduce_blockq_release(None, 0, None) == EARGS

@@ -31,6 +31,9 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
+VARIANTS = "all"
+
+
 def emit(**kw):
     print(json.dumps(kw), flush=True)
 
@@ -186,14 +189,72 @@ def cfg3(red, dev, N=8, sets=3):
     def single_plan(i):
         splans[i % sets].launch(s)
 
-    for name, fn in (("per_partition_launch", per_partition), ("prophet_block_batched", per_block),
+    # Persistent block consumer: ONE launch per iteration over the 12 blocks,
+    # each started once released (byteps_reduce_blockq_*).  Releases are
+    # stream-ordered one-wave kernels writing the block words, here all before
+    # the launch (data resident, as for the back-to-back plans above), or one
+    # per block from a second stream while the consumer runs.
+    bqs = {}
+    for occ in (1, 2):
+        bqs[occ] = []
+        for i in range(sets):
+            bq = red.make_blockq([[(*views(i, p), p.len) for p in bp] for bp in by_block],
+                                 DType.FLOAT16)
+            bq.config(wg_per_cu=occ, timeout_s=5.0)
+            bqs[occ].append(bq)
+
+    def blockq_fn(occ):
+        def fn(i):
+            bq = bqs[occ][i % sets]
+            bq.release(-1, s)
+            bq.launch(s)
+        return fn
+
+    def blockq_graph(occ):
+        gs = []
+        for i in range(sets):
+            bq = bqs[occ][i]
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            side.wait_stream(s)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=side):
+                bq.release(-1, side)
+                bq.launch(side)
+            gs.append(g)
+        return lambda i: gs[i % sets].replay()
+
+    bq_variants = []
+    for occ in (1, 2):
+        bq_variants.append((f"prophet_blockq_occ{occ}", blockq_fn(occ)))
+        bq_variants.append((f"prophet_blockq_occ{occ}_hipgraph", blockq_graph(occ)))
+
+    rel_stream = torch.cuda.Stream()
+
+    def blockq_live(i):
+        """Consumer launched first on s; the 12 releases follow on another
+        stream (as the push path issues them behind each block's H2D).  The
+        releases are ordered after the previous launch (which re-arms the
+        queue) by an event recorded before this one."""
+        bq = bqs[1][i % sets]
+        ev = torch.cuda.Event()
+        ev.record(s)
+        rel_stream.wait_event(ev)
+        bq.launch(s)
+        for b in range(len(by_block)):
+            bq.release(b, rel_stream)
+
+    bq_variants.append(("prophet_blockq_live_release", blockq_live))
+
+    for name, fn in bq_variants + ([] if VARIANTS == "blockq" else [("per_partition_launch", per_partition),
+                     ("prophet_block_batched", per_block),
                      ("single_batched_launch", all_in_one),
                      ("prophet_block_plans", per_block_plan),
                      ("prophet_block_plans_hipgraph", per_block_graph),
                      ("prophet_block_plans_4streams", per_block_plans_4streams),
                      ("prophet_block_plans_4streams_hipgraph", per_block_graph4),
                      ("prophet_release_groups_hipgraph", release_group_graph),
-                     ("single_plan_no_blocks", single_plan)):
+                     ("single_plan_no_blocks", single_plan)]):
         med, mn = timed(fn, 10, s)
         w, out, _ = data[0]
         fn(0)
@@ -462,7 +523,10 @@ def cfg1_pipelined(host, N, B):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--only", default="cfg1,cfg3,sweep,cfg4,cfg5")
+    p.add_argument("--variants", default="all", help="cfg3: all | blockq")
     a = p.parse_args()
+    global VARIANTS
+    VARIANTS = a.variants
     import torch
     from prophet_amd.reducer import GpuReducer
     dev = torch.device("cuda:0")

@@ -29,6 +29,11 @@ run() {  # name limit cmd...
 for s in $STEPS; do
   case $s in
     test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 ;;
+    blockq) run blockq 300 python -u -m pytest tests/test_blockq_gpu.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    cfg3only) run cfg3only 300 python tools/bench_configs.py --only cfg3 ;;
+    bqexp) for v in 1 2 4; do
+             run bqexp_v$v 300 env BPSR_BQ_VPT=$v python tools/bench_configs.py --only cfg3 --variants blockq || exit 1
+           done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     sweep) run sweep 600 python tools/sweep.py ;;
