@@ -158,7 +158,10 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * Every block must be released in every iteration; the launch's last workgroup
  * clears the releases, so releases for the next iteration must be ordered
  * after this launch (same stream, or an event).  One launch of a queue at a
- * time.  Table residency as for plans (buffers fixed after InitTensor). */
+ * time.  Table residency as for plans (buffers fixed after InitTensor).  When
+ * a block's data lands after the launch, its buffers should not share a 128-B
+ * line with an earlier block's (a line read for the earlier block may be
+ * cached ahead of the later block's DMA). */
 typedef struct byteps_reduce_blockq byteps_reduce_blockq;
 int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                                 const int* block_end, int nblocks, int dtype, int mode,
