@@ -8,6 +8,7 @@ re-built as hand-written CDNA4 HIP kernels behind a C ABI
 Python surface:
   * :class:`prophet_amd.reducer.GpuReducer` — mirrors ``CpuReducer``
     (``sum``/``copy``/``GetDataType``) on device pointers, through the C ABI.
+  * :mod:`prophet_amd.torch_ops` — the same ops as ``torch.ops.bpsr.*``.
   * :mod:`prophet_amd.dtypes` — the reference DataType ids.
   * :mod:`prophet_amd.synth` — deterministic synthetic buckets.
 """

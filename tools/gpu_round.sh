@@ -30,6 +30,7 @@ for s in $STEPS; do
   case $s in
     test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 ;;
     blockq) run blockq 300 python -u -m pytest tests/test_blockq_gpu.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    torchops) run torchops 300 python -u -m pytest tests/test_torch_ops.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     cfg3only) run cfg3only 300 python tools/bench_configs.py --only cfg3 ;;
     bqexp) for v in 1 2 4; do
              run bqexp_v$v 300 env BPSR_BQ_VPT=$v python tools/bench_configs.py --only cfg3 --variants blockq || exit 1
