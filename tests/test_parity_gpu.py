@@ -457,3 +457,33 @@ def test_full_size_bf16_left_fold_equals_torch(red, dev):
         ref.add_(s)
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+
+
+@pytest.mark.parametrize("dt,tdt", [(DType.UINT8, torch.uint8), (DType.FLOAT32, torch.float32)],
+                         ids=["u8_4GiB", "f32_2G_elems"])
+def test_beyond_32bit_lengths(red, dev, dt, tdt):
+    """`len` is size_t in the reference (cpu_reducer.h:49): a bucket past 4 GiB
+    (u8: > 2^32 elements) and one past 2^31 fp32 elements (8 GiB) fold
+    correctly everywhere — the element head/tail at the far end, 64-bit tile
+    offsets and the ragged last tile — checked against torch's own fold at the
+    start, around the 2^31/2^32 boundaries and at the end; the bytes past
+    `len` stay untouched (guard)."""
+    es = elem_size(dt)
+    n = ((1 << 32) + 4099) if dt == DType.UINT8 else ((1 << 31) + 1027)
+    L = n * es
+    g = torch.Generator(device=dev).manual_seed(99)
+    if dt == DType.UINT8:
+        ins = [torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev, generator=g)
+               for _ in range(2)]
+    else:
+        ins = [torch.randn(n, device=dev, generator=g) for _ in range(2)]
+    out = torch.full((n + 64,), 7, dtype=tdt, device=dev)
+    red.sum_n(out, ins, L, dt)
+    torch.cuda.synchronize()
+    for lo in (0, (1 << 31) - 5000, min(n - 9000, (1 << 32) - 5000), n - 9000):
+        hi = min(lo + 9000, n)
+        want = ins[0][lo:hi] + ins[1][lo:hi]
+        assert torch.equal(out[lo:hi].view(torch.uint8), want.view(torch.uint8)), lo
+    assert bool((out[n:] == 7).all())
+    del ins, out
+    torch.cuda.empty_cache()
