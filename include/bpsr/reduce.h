@@ -166,7 +166,9 @@ typedef struct byteps_reduce_blockq byteps_reduce_blockq;
 int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                                 const int* block_end, int nblocks, int dtype, int mode,
                                 byteps_reduce_blockq** q);
-/* Persistent workgroups per CU (1..8, default 1; <= 0 keeps) and the release
+/* Consumer shape: wg_per_cu = 0 (default) dispatch-ordered — one workgroup
+ * per tile, each gated on the released-tile mark the release kernel raises;
+ * 1..8 persistent workgroups per CU sweeping the table; < 0 keeps.  Release
  * timeout in seconds (<= 0 keeps). */
 int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s);
 int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream);

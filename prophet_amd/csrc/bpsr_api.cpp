@@ -552,7 +552,8 @@ struct byteps_reduce_blockq {
   int dtype = 0;
   int mode = 0;
   int nblocks = 0;
-  int occ = 1;               // persistent workgroups per CU (cfg3: 1 beats 2 and 4)
+  int occ = 0;               // 0: dispatch-ordered; > 0: persistent workgroups per CU
+  int gate_occ = 2;          // dispatch-ordered: resident workgroups per CU, at most
   int cus = 0;
   double timeout_s = 2.0;
   uint64_t clock_khz = 0;    // wall_clock64() rate
@@ -593,6 +594,9 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   std::vector<char> host;
   std::vector<uint32_t> first;
   TableInfo ti;
+  int gate_occ = 2;
+  if (const char* v = getenv("BPSR_BQ_GATE_OCC")) gate_occ = atoi(v);
+  if (gate_occ < 1 || gate_occ > 8) gate_occ = 2;
   int force_vpt = 0;  // tile size override for measurements (default: the fold rule)
   if (const char* v = getenv("BPSR_BQ_VPT")) force_vpt = atoi(v);
   if (force_vpt != 1 && force_vpt != 2 && force_vpt != 4) force_vpt = 0;
@@ -603,6 +607,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   q->dtype = dtype;
   q->mode = mode;
   q->nblocks = nblocks;
+  q->gate_occ = gate_occ;
   q->ti = ti;
   int khz = 0;
   hipError_t e = hipGetDevice(&q->device);
@@ -635,7 +640,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
 int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
   if (wg_per_cu > 8) return fail(BYTEPS_REDUCE_EARGS, "wg_per_cu %d > 8", wg_per_cu);
-  if (wg_per_cu > 0) q->occ = wg_per_cu;
+  if (wg_per_cu >= 0) q->occ = wg_per_cu;
   if (timeout_s > 0) q->timeout_s = timeout_s;
   return BYTEPS_REDUCE_OK;
 }
@@ -649,15 +654,31 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.block_first = q->flags + q->nblocks;
   Q.ctl = q->ctl;
   Q.nblocks = (uint32_t)q->nblocks;
-  const uint64_t cap = (uint64_t)q->cus * (uint64_t)q->occ;
-  Q.grid = (uint32_t)std::min<uint64_t>(q->ti.tiles, cap);
   Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
   Q.pad[0] = Q.pad[1] = 0;
-  // residency cap through LDS (the kernel's own 20 B of static LDS included)
-  const size_t lds = q->occ > 0 ? ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255 : 0;
   const Tuning tu = tuning_for_n(q->ti.nmax);
-  hipError_t e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, q->dtype, q->mode,
-                               to_stream(stream));
+  hipStream_t s = to_stream(stream);
+  const bool gated = q->occ == 0;
+  size_t lds;
+  if (gated) {
+    // One workgroup per tile.  Residency is capped (LDS) so that workgroups
+    // spinning on a release never take a CU's last registers: the release
+    // kernels and the copies that precede them must still get onto the CU
+    // (at hardware occupancy — 3 of these workgroups per CU — a live release
+    // behind H2D copies on another stream never arrived).
+    Q.grid = q->ti.tiles;
+    int occ = launch_occ(tu, q->ti.tiles, true);
+    if (occ == 0 || occ > q->gate_occ) occ = q->gate_occ;
+    lds = occ_lds_bytes(occ);
+  } else {
+    const uint64_t cap = (uint64_t)q->cus * (uint64_t)q->occ;
+    Q.grid = (uint32_t)std::min<uint64_t>(q->ti.tiles, cap);
+    // residency cap through LDS (the kernel's own static LDS included)
+    lds = ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255;
+  }
+  hipError_t e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, s);
+  if (e == hipSuccess && gated)  // re-arm behind the launch, as the persistent kernel's last workgroup does
+    e = launch_blockq_rearm(q->flags, (uint32_t)q->nblocks, q->ctl, s);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
 }
 
@@ -668,8 +689,10 @@ int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* strea
   // A one-wave kernel storing the words at system scope (write-through); a
   // hipMemset node was not seen by the consumer's polls under graph replay, and
   // hipStreamWriteValue32 measured slower for per-block releases.
-  hipError_t e = block < 0 ? launch_blockq_release(q->flags, (uint32_t)q->nblocks, s)
-                           : launch_blockq_release(q->flags + block, 1, s);
+  const uint32_t first = block < 0 ? 0u : (uint32_t)block;
+  const uint32_t count = block < 0 ? (uint32_t)q->nblocks : 1u;
+  hipError_t e = launch_blockq_release(q->flags, first, count, (uint32_t)q->nblocks,
+                                       q->flags + q->nblocks, q->ctl, s);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block release");
 }
 

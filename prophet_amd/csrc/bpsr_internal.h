@@ -89,7 +89,7 @@ struct BatchLaunch {
 // byteps_reduce_blockq_release).
 // The launch's last workgroup re-arms the queue (flags, done counter).
 struct BlockqCtl {
-  uint32_t pad0;
+  uint32_t released;  // tiles [0, released) are in released blocks (release kernel)
   uint32_t done;  // workgroups finished in this launch
   uint32_t err;   // sticky: a workgroup gave up waiting for a release
   uint32_t pad;
@@ -171,7 +171,7 @@ inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
   hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
                                    hipStream_t s);                                        \
   hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
-                                  hipStream_t s);
+                                  bool gated, hipStream_t s);
 BPSR_DECLARE_LAUNCHERS(f32)
 BPSR_DECLARE_LAUNCHERS(f64)
 BPSR_DECLARE_LAUNCHERS(f16)
@@ -186,9 +186,12 @@ hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);
 hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, const Tuning& tu,
                           hipStream_t s);
-hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, int dtype, int mode,
-                         hipStream_t s);
-hipError_t launch_blockq_release(uint32_t* flags, uint32_t count, hipStream_t s);
+hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, bool gated,
+                         int dtype, int mode, hipStream_t s);
+hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count,
+                                 uint32_t nblocks, const uint32_t* block_first, BlockqCtl* ctl,
+                                 hipStream_t s);
+hipError_t launch_blockq_rearm(uint32_t* flags, uint32_t nblocks, BlockqCtl* ctl, hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.

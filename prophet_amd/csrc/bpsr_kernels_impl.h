@@ -523,9 +523,44 @@ __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
       // every other workgroup has finished: re-arm
       for (uint32_t b = 0; b < Q.nblocks; ++b)
         __hip_atomic_store(Q.flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&Q.ctl->released, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&Q.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// Dispatch-ordered block consumer (the block queue's default mode): one tile
+// record per workgroup, grid = tiles, like batched_kernel — hardware dispatch
+// in tile order keeps the sweep as tight as one batched launch — and each
+// workgroup first checks the released-tile mark that the release kernel
+// publishes (ctl->released, system-scope, raised monotonically).  A workgroup
+// whose tile is not yet released polls the mark (per wave, `s_sleep` between
+// polls, bounded by the timeout) and acquires before its loads; one whose
+// tile is released reads data no workgroup of this launch has touched since
+// the launch's own acquire (blocks do not share lines), so it needs none.
+template <class Op, int VPT, bool NT>
+__global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
+  const uint32_t t = blockIdx.x;
+  const unsigned char* rec = Q.L.recs + (uint64_t)t * Q.L.rec_stride;
+  // the mark (vector load) and the record (scalar loads) travel together
+  const uint32_t relv = ld_sys(&Q.ctl->released);
+  const RecRegs r = load_record(rec);
+  const uint32_t rel = __builtin_amdgcn_readfirstlane(relv);
+  if (t >= rel) {
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(4);
+      if (__builtin_amdgcn_readfirstlane(ld_sys(&Q.ctl->released)) > t) break;
+      if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+      if (wall_clock64() - t0 > Q.timeout_ticks) {
+        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  run_record<Op, VPT, NT>(r, reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes),
+                          Q.L.entries);
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -597,8 +632,15 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
 }
 
 template <class Op, int VPT, bool NT>
-static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, hipStream_t s) {
-  // the kernel's own static LDS (the tile broadcast words) comes on top of the
+static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated, hipStream_t s) {
+  if (gated) {
+    static const hipError_t okg =
+        allow_full_lds(reinterpret_cast<const void*>(&blockq_gate_kernel<Op, VPT, NT>));
+    if (okg != hipSuccess) return okg;
+    hipLaunchKernelGGL((blockq_gate_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
+    return hipGetLastError();
+  }
+  // the kernel's own static LDS (the record staging words) comes on top of the
   // dynamic residency request, so allow 256 B less than the CU's 160 KiB
   static const hipError_t ok =
       hipFuncSetAttribute(reinterpret_cast<const void*>(&blockq_kernel<Op, VPT, NT>),
@@ -610,15 +652,15 @@ static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, hipStream_t
 
 template <class Op>
 static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,
-                                   hipStream_t s) {
+                                   bool gated, hipStream_t s) {
   if (Q.grid == 0) return hipSuccess;
   switch (vpt * 2 + (nt ? 1 : 0)) {
-    case 2: return launch_blockq_k<Op, 1, false>(Q, lds, s);
-    case 3: return launch_blockq_k<Op, 1, true>(Q, lds, s);
-    case 4: return launch_blockq_k<Op, 2, false>(Q, lds, s);
-    case 8: return launch_blockq_k<Op, 4, false>(Q, lds, s);
-    case 9: return launch_blockq_k<Op, 4, true>(Q, lds, s);
-    default: return launch_blockq_k<Op, 2, true>(Q, lds, s);
+    case 2: return launch_blockq_k<Op, 1, false>(Q, lds, gated, s);
+    case 3: return launch_blockq_k<Op, 1, true>(Q, lds, gated, s);
+    case 4: return launch_blockq_k<Op, 2, false>(Q, lds, gated, s);
+    case 8: return launch_blockq_k<Op, 4, false>(Q, lds, gated, s);
+    case 9: return launch_blockq_k<Op, 4, true>(Q, lds, gated, s);
+    default: return launch_blockq_k<Op, 2, true>(Q, lds, gated, s);
   }
 }
 
@@ -635,7 +677,7 @@ static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, bool nt, size
     return launch_batched_op<OP>(L, vpt, tu, s);                                          \
   }                                                                                       \
   hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
-                                  hipStream_t s) {                                        \
-    return launch_blockq_op<OP>(Q, vpt, nt, lds, s);                                      \
+                                  bool gated, hipStream_t s) {                            \
+    return launch_blockq_op<OP>(Q, vpt, nt, lds, gated, s);                               \
   }                                                                                       \
   }

@@ -273,7 +273,9 @@ class BlockQueue:
                                                int(dtype), int(mode),
                                                ctypes.byref(self.handle)))
 
-    def config(self, wg_per_cu: int = 0, timeout_s: float = 0.0) -> None:
+    def config(self, wg_per_cu: int = -1, timeout_s: float = 0.0) -> None:
+        """``wg_per_cu`` 0: dispatch-ordered consumer (default); 1..8:
+        persistent workgroups per CU; < 0 keeps.  ``timeout_s`` <= 0 keeps."""
         _check(self.lib.byteps_reduce_blockq_config(self.handle, int(wg_per_cu),
                                                     float(timeout_s)))
 

@@ -92,12 +92,19 @@ MIXED = [
 ]
 
 
+# consumer shapes: 0 = dispatch-ordered (one workgroup per tile, gated on the
+# released mark), 1 = persistent (one workgroup per CU sweeping the table)
+SHAPES = pytest.mark.parametrize("shape", [0, 1], ids=["dispatch", "persistent"])
+
+
+@SHAPES
 @pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.BFLOAT16, DType.INT32,
                                 DType.FLOAT64, DType.UINT8], ids=lambda d: DType(d).name)
-def test_release_all_three_iterations(red, dev, dt):
+def test_release_all_three_iterations(red, dev, dt, shape):
     """Release every block up front; the queue re-arms itself between launches."""
     tab = Table(dev, dt, MIXED, offsets=True)
     q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=shape)
     for it in range(3):
         pushes, wants = tab.host_inputs(100 * it + 7)
         tab.upload(pushes)
@@ -110,9 +117,10 @@ def test_release_all_three_iterations(red, dev, dt):
     q.close()
 
 
-@pytest.mark.parametrize("occ", [1, 2, 4])
+@pytest.mark.parametrize("occ", [0, 1, 2, 4])
 def test_live_release_after_dma(red, dev, occ):
-    """The consumer is launched first; a copy stream then pushes each block's
+    """The consumer is launched first (occ 0: dispatch-ordered, else
+    persistent workgroups per CU); a copy stream then pushes each block's
     data by H2D DMA and releases the block behind it.  Every block must see
     its own freshly landed bytes (acquire after the release), over iterations
     whose data differ."""
@@ -145,13 +153,15 @@ def test_live_release_after_dma(red, dev, occ):
     q.close()
 
 
-def test_out_of_order_release_waits_for_prefix(red, dev):
+@SHAPES
+def test_out_of_order_release_waits_for_prefix(red, dev, shape):
     """Blocks released last-to-first from a side stream: nothing past an
     unreleased block is started, and the result is still exact."""
     dt = DType.FLOAT32
     blocks = [[(200_000 + 17 * b, 8, "normal")] for b in range(6)]
     tab = Table(dev, dt, blocks)
     q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=shape)
     pushes, wants = tab.host_inputs(55)
     tab.upload(pushes)
     torch.cuda.synchronize()
@@ -165,7 +175,8 @@ def test_out_of_order_release_waits_for_prefix(red, dev):
     q.close()
 
 
-def test_missing_release_times_out_and_recovers(red, dev):
+@SHAPES
+def test_missing_release_times_out_and_recovers(red, dev, shape):
     """Blocks 0-1 released, block 2 never: the launch gives up after its
     timeout, reports ETIMEOUT once, has folded the released blocks, and the
     queue works normally afterwards."""
@@ -175,7 +186,7 @@ def test_missing_release_times_out_and_recovers(red, dev):
               [(1000, 8, "normal")]]
     tab = Table(dev, dt, blocks)
     q = red.make_blockq(tab.blocks, dt)
-    q.config(timeout_s=0.2)
+    q.config(wg_per_cu=shape, timeout_s=0.2)
     pushes, wants = tab.host_inputs(77)
     tab.upload(pushes)
     torch.cuda.synchronize()
@@ -196,7 +207,8 @@ def test_missing_release_times_out_and_recovers(red, dev):
     q.close()
 
 
-def test_graph_replay_matches_plans(red, dev, port):
+@SHAPES
+def test_graph_replay_matches_plans(red, dev, port, shape):
     """Release + launch captured into a hipGraph and replayed on new data:
     bit-identical with one plan per block (ResNet-50 fp16 Prophet blocks)."""
     from prophet_amd.buckets import resnet50_param_sizes, prophet_blocks
@@ -206,6 +218,7 @@ def test_graph_replay_matches_plans(red, dev, port):
     blocks = [[(sizes[i], 8, "normal") for i in g] for g in groups]
     tab = Table(dev, dt, blocks)
     q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=shape)
     side = torch.cuda.Stream()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=side):

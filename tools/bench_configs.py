@@ -195,7 +195,7 @@ def cfg3(red, dev, N=8, sets=3):
     # the launch (data resident, as for the back-to-back plans above), or one
     # per block from a second stream while the consumer runs.
     bqs = {}
-    for occ in (1, 2):
+    for occ in (0, 1):
         bqs[occ] = []
         for i in range(sets):
             bq = red.make_blockq([[(*views(i, p), p.len) for p in bp] for bp in by_block],
@@ -225,18 +225,18 @@ def cfg3(red, dev, N=8, sets=3):
         return lambda i: gs[i % sets].replay()
 
     bq_variants = []
-    for occ in (1, 2):
-        bq_variants.append((f"prophet_blockq_occ{occ}", blockq_fn(occ)))
-        bq_variants.append((f"prophet_blockq_occ{occ}_hipgraph", blockq_graph(occ)))
+    for occ, nm in ((0, "dispatch"), (1, "persistent")):
+        bq_variants.append((f"prophet_blockq_{nm}", blockq_fn(occ)))
+        bq_variants.append((f"prophet_blockq_{nm}_hipgraph", blockq_graph(occ)))
 
     rel_stream = torch.cuda.Stream()
 
-    def blockq_live(i):
+    def blockq_live(i, occ=0):
         """Consumer launched first on s; the 12 releases follow on another
         stream (as the push path issues them behind each block's H2D).  The
         releases are ordered after the previous launch (which re-arms the
         queue) by an event recorded before this one."""
-        bq = bqs[1][i % sets]
+        bq = bqs[occ][i % sets]
         ev = torch.cuda.Event()
         ev.record(s)
         rel_stream.wait_event(ev)
@@ -244,7 +244,9 @@ def cfg3(red, dev, N=8, sets=3):
         for b in range(len(by_block)):
             bq.release(b, rel_stream)
 
-    bq_variants.append(("prophet_blockq_live_release", blockq_live))
+    bq_variants.append(("prophet_blockq_dispatch_live_release", blockq_live))
+    bq_variants.append(("prophet_blockq_persistent_live_release",
+                        lambda i: blockq_live(i, occ=1)))
 
     for name, fn in bq_variants + ([] if VARIANTS == "blockq" else [("per_partition_launch", per_partition),
                      ("prophet_block_batched", per_block),
