@@ -1,5 +1,5 @@
 """Key-space sharding: ownership math (core_loops.cc:208-247) and the
-multi-process data path over gloo (world_size 2 and 3, CPU).
+multi-process data path over gloo (world_size 2, 3 and 8 — the driver's node size — on CPU).
 
 The local fold in these CPU tests is the oracle (test infrastructure), injected
 into ShardedReducer; the product default is the HIP fold (tests/test_parity_gpu.py
@@ -91,7 +91,7 @@ def _worker(rank, world, port, n_elems, n_workers, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_scatter_reduce_allgather_gloo(world):
     n_elems, n_workers = 10_007, 5
     ctx = mp.get_context("spawn")
@@ -178,7 +178,7 @@ def _worker_bench_leg(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_scatter_leg_gloo(world):
     """bench.py's config-4 leg (reported beside `value` at N > 1 GPUs): scatter
     from GPU 0, owner fold, all-gather; the root's check against torch's left

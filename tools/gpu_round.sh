@@ -32,6 +32,9 @@ for s in $STEPS; do
     blockq) run blockq 300 python -u -m pytest tests/test_blockq_gpu.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     torchops) run torchops 300 python -u -m pytest tests/test_torch_ops.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     cfg3only) run cfg3only 300 python tools/bench_configs.py --only cfg3 ;;
+    batchocc) for o in 0 2 4; do
+             run batch_occ$o 300 env BPSR_SMALL_OCC_BATCH=$o python tools/bench_configs.py --only cfg3 || exit 1
+           done ;;
     gateocc) for o in 1 2 3; do
              run gate_occ$o 300 env BPSR_BQ_GATE_OCC=$o python tools/bench_configs.py --only cfg3 --variants blockq || exit 1
            done ;;
