@@ -119,3 +119,30 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     bad = server.ServerConfig(2, 0, 0, 0, 0)      # server.cc:332 CHECK_GE(threads, 1)
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
     assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS
+
+
+def test_block_queue_argument_errors_without_gpu():
+    """byteps_reduce_blockq_* validates the block partition and handles before
+    any HIP call: bad block ends, a last block that does not end at nbuckets,
+    no blocks, null handles."""
+    lib = reducer.load_library()
+    descs = (reducer.BucketDesc * 2)()
+    for i in range(2):
+        descs[i].dst = 0x10000 * (i + 1)
+        descs[i].srcs[0] = 0x100000 * (i + 1)
+        descs[i].len = 64
+        descs[i].n = 1
+    h = ctypes.c_void_p()
+    for ends in ([3], [1], [2, 1], [1, 3]):
+        arr = (ctypes.c_int * len(ends))(*ends)
+        rc = lib.byteps_reduce_blockq_create(descs, 2, arr, len(ends), 0, 0, ctypes.byref(h))
+        assert rc == reducer.EARGS, ends
+        assert not h.value
+    arr = (ctypes.c_int * 1)(2)
+    assert lib.byteps_reduce_blockq_create(descs, 2, arr, 0, 0, 0, ctypes.byref(h)) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_create(descs, 2, arr, 1, 9, 0, ctypes.byref(h)) == reducer.EDTYPE
+    assert lib.byteps_reduce_blockq_launch(None, None) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_release(None, 0, None) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_status(None, None) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_config(None, 0, 1.0) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_destroy(None) == reducer.OK
