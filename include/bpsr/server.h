@@ -80,6 +80,19 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
  * then copies the store (len bytes) to `out`. */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
+/* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
+ * with an SArray over the store itself).  Blocks like byteps_server_pull, then
+ * sets *data to a pinned host mirror of the store holding this round's result
+ * (*len = key length).  The server fills the mirror with ONE device-to-host
+ * copy per round, queued behind the round's fold on its own stream, instead of
+ * one copy per puller; from the first view of a key on, every later round is
+ * mirrored as soon as it finishes.  Two mirrors alternate by round, each at a
+ * fixed address (register them with the NIC once).  Sync mode: the view stays
+ * valid until this worker's next pull of the key returns.  Async mode: each
+ * call copies the current store; the view is valid until the next call on the
+ * key.  The caller must not write through the view. */
+int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** data, size_t* len);
+
 /* Introspection for tests/debug (BYTEPS_SERVER_DEBUG analogue): completed
  * rounds, engine lane, and the arrival order of the last completed round. */
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,

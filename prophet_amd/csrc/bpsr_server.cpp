@@ -28,6 +28,7 @@ constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots (
 struct Lane {
   hipStream_t fold = nullptr;  // folds, in round order per key
   hipStream_t copy = nullptr;  // push/pull copies
+  hipStream_t d2h = nullptr;   // per-round store -> host mirror copies
 };
 
 struct KeyState {
@@ -55,6 +56,11 @@ struct KeyState {
   hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the round
   hipEvent_t copied = nullptr;
   bool has_done = false;
+  // pinned host mirror of the store for zero-copy pull responses
+  // (byteps_server_pull_host_view; server.cc:42-70 responds from the store
+  // itself).  Two buffers by round parity, filled by ONE D2H per round.
+  char* mirror[2] = {nullptr, nullptr};
+  hipEvent_t mirrored = nullptr;  // recorded on the lane's d2h stream
 };
 
 }  // namespace
@@ -151,6 +157,18 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
   return e == hipSuccess ? 0 : hip_fail(e, "push copy");
 }
 
+// Queue the D2H of the store into mirror[round & 1] on the lane's d2h stream,
+// behind the round's fold (caller holds ks->mu).  Its own stream, so the copy
+// overlaps the H2D pushes of the lane's other keys (PCIe is full duplex).
+int queue_mirror(byteps_server* s, KeyState* ks, uint64_t round) {
+  Lane& L = s->lanes[ks->lane];
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ks->mirror[round & 1], ks->store, ks->len, hipMemcpyDeviceToHost, L.d2h);
+  if (e == hipSuccess) e = hipEventRecord(ks->mirrored, L.d2h);
+  return e == hipSuccess ? 0 : hip_fail(e, "store mirror copy");
+}
+
 // A push's bytes are in slot w: advance the state machine (caller holds ks->mu).
 int arrive(byteps_server* s, KeyState* ks, int w) {
   const int N = s->cfg.num_workers;
@@ -208,6 +226,7 @@ int arrive(byteps_server* s, KeyState* ks, int w) {
   hipError_t e = hipEventRecord(ks->done, L.fold);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
   ks->has_done = true;
+  if (ks->mirror[0] && (rc = queue_mirror(s, ks, ks->rounds + 1))) return rc;
   ks->last_order = ks->order;
   ks->order.clear();
   ks->arrived = 0;
@@ -279,6 +298,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   for (auto& L : s->lanes) {
     hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
     if (e != hipSuccess) {
       byteps_server_destroy(s.release());
       return hip_fail(e, "hipStreamCreate");
@@ -294,16 +314,21 @@ int byteps_server_destroy(byteps_server* s) {
   for (auto& L : s->lanes) {
     if (L.fold) (void)hipStreamSynchronize(L.fold);
     if (L.copy) (void)hipStreamSynchronize(L.copy);
+    if (L.d2h) (void)hipStreamSynchronize(L.d2h);
   }
   for (auto& kv : s->keys) {
     KeyState* ks = kv.second.get();
     if (ks->done) (void)hipEventDestroy(ks->done);
     if (ks->copied) (void)hipEventDestroy(ks->copied);
+    if (ks->mirrored) (void)hipEventDestroy(ks->mirrored);
+    for (char* m : ks->mirror)
+      if (m) (void)hipHostFree(m);
     if (ks->arena) (void)hipFree(ks->arena);
   }
   for (auto& L : s->lanes) {
     if (L.fold) (void)hipStreamDestroy(L.fold);
     if (L.copy) (void)hipStreamDestroy(L.copy);
+    if (L.d2h) (void)hipStreamDestroy(L.d2h);
   }
   delete s;
   return BYTEPS_REDUCE_OK;
@@ -401,6 +426,55 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
     }
     ks->cv.notify_all();
   }
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** data,
+                                 size_t* len) {
+  if (!s || !data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  *data = nullptr;
+  if (len) *len = 0;
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated)  // server.cc:282-283
+    return fail(BYTEPS_REDUCE_EARGS,
+                "Processing pull request when the key %llu has not been inited yet",
+                (unsigned long long)key);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished; });
+  hipError_t e = hipSuccess;
+  if (!ks->mirror[0]) {  // first view of this key: pin the mirrors (fixed
+                         // addresses from now on, as server.cc:60-69 reuses its
+                         // response buffer to avoid re-registering memory)
+    for (char*& m : ks->mirror) {
+      void* p = nullptr;
+      if ((e = hipHostMalloc(&p, ks->len, hipHostMallocDefault)) != hipSuccess)
+        return hip_fail(e, "hipHostMalloc(store mirror)");
+      m = static_cast<char*>(p);
+    }
+    if ((e = hipEventCreateWithFlags(&ks->mirrored, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hipEventCreate");
+    if (!s->cfg.async_mode && (rc = queue_mirror(s, ks, ks->rounds))) return rc;
+  }
+  // async mode: the store changes with every push, so each view is a fresh D2H
+  if (s->cfg.async_mode && (rc = queue_mirror(s, ks, ks->rounds))) return rc;
+  const char* view = ks->mirror[ks->rounds & 1];
+  hipEvent_t ev = ks->mirrored;
+  lk.unlock();
+  // The event still names this round's copy: the next round cannot finish
+  // before this pull is counted below.
+  if ((e = hipEventSynchronize(ev)) != hipSuccess) return hip_fail(e, "store mirror sync");
+  lk.lock();
+  if (!s->cfg.async_mode) {
+    if (++ks->pull_cnt == s->cfg.num_workers) {  // server.cc:105-113
+      ks->push_finished = false;
+      ks->pull_cnt = 0;
+    }
+    ks->cv.notify_all();
+  }
+  *data = view;
+  if (len) *len = ks->len;
   return BYTEPS_REDUCE_OK;
 }
 

@@ -20,7 +20,8 @@ HOST, DEVICE = 0, 1
 SERVER_EXPORTS = (
     "byteps_server_config_from_env", "byteps_server_create", "byteps_server_destroy",
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
-    "byteps_server_push_ready", "byteps_server_pull", "byteps_server_key_info",
+    "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
+    "byteps_server_key_info",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -42,6 +43,8 @@ def _lib():
         L.byteps_server_recv_slot.argtypes = [_vp, _u64, _int, ctypes.POINTER(_vp)]
         L.byteps_server_push_ready.argtypes = [_vp, _u64, _int]
         L.byteps_server_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
+        L.byteps_server_pull_host_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
+                                                   ctypes.POINTER(_sz)]
         L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
                                              ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
         L._server_bound = True
@@ -93,6 +96,16 @@ class PSServer:
         p, n, loc = _buf(out)
         _check(self.lib.byteps_server_pull(self.handle, key, p, n if nbytes is None else nbytes,
                                            loc))
+
+    def pull_view(self, key: int) -> memoryview:
+        """Zero-copy pull response (server.cc:42-70): a read-only memoryview of
+        the pinned host mirror the server fills with one D2H per round.  Valid
+        until this worker's next pull of the key returns (sync mode)."""
+        p, n = _vp(), _sz()
+        _check(self.lib.byteps_server_pull_host_view(self.handle, key, ctypes.byref(p),
+                                                     ctypes.byref(n)))
+        buf = (ctypes.c_char * n.value).from_address(p.value)
+        return memoryview(buf).cast("B").toreadonly()
 
     def key_info(self, key: int):
         rounds, lane = _u64(), _int()

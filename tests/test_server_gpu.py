@@ -206,3 +206,75 @@ def test_engine_lanes_least_loaded_sticky():
         load[want] += s
         assert srv.key_info(k)[1] == want
     srv.close()
+
+
+def _init_round(srv, dt, N, sizes):
+    for j, n in enumerate(sizes):
+        ts = [threading.Thread(target=srv.push, args=(j, w, data(dt, n, w, 0, j), dt))
+              for w in range(N)]       # init pushes block until all arrived
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+def test_pull_host_view_rounds(port, policy):
+    """Zero-copy pull responses (byteps_server_pull_host_view, server.cc:42-70):
+    one D2H per round into a pinned mirror; every worker's view is bit-exact
+    with the oracle's fold in arrival order; a round-r view still holds round r
+    after round r+1 finished (two mirrors by round parity); views and copying
+    pulls count toward the same re-arm (server.cc:105-113)."""
+    from prophet_amd.server import PSServer
+    dt, N = DType.FLOAT32, 4
+    sizes = [5, 1_000_003, 4_096_000 // 4]
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2, policy=policy)
+    _init_round(srv, dt, N, sizes)
+    held = {}
+    for rnd in range(1, 5):
+        for j, n in enumerate(sizes):
+            order = random.Random(rnd * 10 + j).sample(range(N), N)
+            for w in order:
+                srv.push(j, w, data(dt, n, w, rnd, j), dt)
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, rnd, j) for w in order], n * es, dt)
+            assert srv.key_info(j)[2] == order
+            for w in range(N):
+                if w == N - 1 and rnd % 2:          # a copying pull counts too
+                    out = np.zeros(n * es, np.uint8)
+                    srv.pull(j, out)
+                    got = out
+                else:
+                    v = srv.pull_view(j)
+                    assert v.readonly and v.nbytes == n * es
+                    got = np.frombuffer(v, np.uint8)
+                assert np.array_equal(got, want), f"round {rnd} key {j} worker {w}"
+            if (rnd - 1, j) in held:   # previous round's view: other mirror, intact
+                v0, w0 = held.pop((rnd - 1, j))
+                assert np.array_equal(np.frombuffer(v0, np.uint8), w0)
+            held[(rnd, j)] = (v, want.copy())
+    srv.close()
+
+
+def test_pull_host_view_async_and_errors(port):
+    from prophet_amd.server import PSServer
+    from prophet_amd.reducer import ReduceError
+    dt, N, n = DType.FLOAT32, 2, 70_001
+    with pytest.raises(ReduceError):
+        with PSServer(N) as srv:
+            srv.pull_view(99)                         # key not inited (server.cc:282)
+    srv = PSServer(N, async_mode=True)
+    init = data(dt, n, 0, 0, 0)          # same init data from both: store = it
+    ts = [threading.Thread(target=srv.push, args=(0, w, init, dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    acc = init.view(np.float32).copy()
+    for w in (1, 0, 1):
+        srv.push(0, w, data(dt, n, w, 7, 0), dt)
+        acc += data(dt, n, w, 7, 0).view(np.float32)
+        v = srv.pull_view(0)                           # async: answered at once
+        assert np.array_equal(np.frombuffer(v, np.uint8), acc.view(np.uint8))
+    srv.close()

@@ -468,13 +468,18 @@ def cfg1(dev, N=2, B=64 << 20):
                      round_ms=round(med * 1e3, 3), gibps=round(N * B / med / GIB, 2), exact=ok)
                 srv.close()
     cfg1_pipelined(host, N, B)
+    cfg1_pipelined(host, N, B, view=True)
 
 
-def cfg1_pipelined(host, N, B):
+def cfg1_pipelined(host, N, B, view=False):
     """cfg1 with BytePS's worker loop structure: each worker has a push thread
     and a pull thread (core_loops.cc:492-528 PushLoop, 530-564 PullLoop); the
     pull of a partition is issued as soon as that partition's push returned, so
-    the D2H of partition k overlaps the H2D of partition k+1."""
+    the D2H of partition k overlaps the H2D of partition k+1.
+    view=True: pulls are zero-copy responses (byteps_server_pull_host_view, the
+    analogue of server.cc:42-70 answering from the store's SArray): one D2H per
+    key per round into a pinned mirror that a transport would send from, instead
+    of one D2H per puller.  The exactness round copies the views out."""
     import threading
     import torch
     from prophet_amd.buckets import partition_tensor
@@ -484,7 +489,9 @@ def cfg1_pipelined(host, N, B):
     srv = PSServer(N, engine_lanes=4, policy=0)
     outs = [torch.empty(B, dtype=torch.uint8).pin_memory() for _ in range(N)]
 
-    def rnd(init=False):
+    import numpy as np
+
+    def rnd(init=False, check=False):
         pushed = [[threading.Event() for _ in parts] for _ in range(N)]
 
         def pusher(k):
@@ -496,7 +503,12 @@ def cfg1_pipelined(host, N, B):
         def puller(k):
             for i, (key, off, ln) in enumerate(parts):
                 pushed[k][i].wait()
-                srv.pull(key, outs[k][off:off + ln])
+                if not view:
+                    srv.pull(key, outs[k][off:off + ln])
+                else:
+                    v = srv.pull_view(key)
+                    if check:
+                        outs[k][off:off + ln].numpy()[:] = np.frombuffer(v, np.uint8)
         ts = [threading.Thread(target=pusher, args=(k,)) for k in range(N)]
         if not init:
             ts += [threading.Thread(target=puller, args=(k,)) for k in range(N)]
@@ -512,11 +524,14 @@ def cfg1_pipelined(host, N, B):
         rnd()
         ts_.append(time.perf_counter() - t0)
     med = statistics.median(ts_)
+    if view:
+        rnd(check=True)
     want = host[0].clone()
     for h in host[1:]:
         want += h
     ok = all(bool(torch.equal(o, want.view(torch.uint8))) for o in outs)
-    emit(config="cfg1", layout="17keys_push_pull_threads", pushes_from="host", policy="fused",
+    emit(config="cfg1", layout="17keys_push_pull_threads" + ("_pull_view" if view else ""),
+         pushes_from="host", policy="fused",
          n_workers=N, bucket_bytes=B, round_ms=round(med * 1e3, 3),
          gibps=round(N * B / med / GIB, 2), exact=ok)
     srv.close()

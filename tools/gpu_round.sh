@@ -70,6 +70,7 @@ for s in $STEPS; do
            run bench_bf16acc 300 python bench.py --dtype bf16 --mode accum --no-cpu-baseline &&
            run ops 300 python tools/op_probe.py ;;
     cfg1)  run cfg1 300 python tools/bench_configs.py --only cfg1 ;;
+    server) run server 300 python -u -m pytest tests/test_server_gpu.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     lat)   run lat 300 python tools/latency_probe.py ;;
     cfg3p) run cfg3p 300 python tools/cfg3_probe.py ;;
     thr)   for t in 2048 4096 8192 1000000; do
