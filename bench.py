@@ -102,7 +102,8 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
             round_once()
         ts = []
         t_begin = time.perf_counter()
-        while len(ts) < 10 or (time.perf_counter() - t_begin < 4.0 and len(ts) < 200):
+        budget = 10.0 if label == "default" else 4.0   # seconds of CPU work per leg
+        while len(ts) < 10 or (time.perf_counter() - t_begin < budget and len(ts) < 2000):
             ts.append(round_once())
         med = statistics.median(ts)
         out[label] = dict(threads=threads, gibps=n_workers * L / med / GIB,
@@ -121,7 +122,8 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
         "value": round(d["gibps"], 3), "unit": "GiB/s", "cores": d["threads"], "kind": kind,
         "sample": (f"{n_workers}-way server round (zero-copy first arrival, {n_workers - 1} "
                    f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket, "
-                   f"median of {d['reps']} reps; BYTEPS_OMP_THREAD_PER_GPU=4 (reference default)"),
+                   f"median of {d['reps']} reps (~10 s of CPU work); "
+                   f"BYTEPS_OMP_THREAD_PER_GPU=4 (reference default)"),
         "all_cores": {"value": round(out["all"]["gibps"], 3), "cores": out["all"]["threads"],
                       "reps": out["all"]["reps"]},
         "cpu_model": cpu_model, "host_cpus": ncpu,

@@ -80,7 +80,8 @@ enum byteps_reduce_status {
   BYTEPS_REDUCE_EARGS = -2,    /* bad pointer / count / overlap / mode        */
   BYTEPS_REDUCE_EHIP = -3,     /* HIP runtime error (launch, copy, event)     */
   BYTEPS_REDUCE_ERCCL = -4,    /* collective error (reserved for shard APIs)  */
-  BYTEPS_REDUCE_ETIMEOUT = -5  /* a block queue launch gave up on a release   */
+  BYTEPS_REDUCE_ETIMEOUT = -5, /* a block queue launch gave up on a release   */
+  BYTEPS_REDUCE_ECANCELED = -6 /* a queued server pull dropped at shutdown    */
 };
 
 /* Most sources one kernel launch folds; byteps_reduce_sum_n chains launches

@@ -93,6 +93,22 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
  * key.  The caller must not write through the view. */
 int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** data, size_t* len);
 
+/* Non-blocking pull for a transport's receive thread: the reference's default
+ * non-blocking engine queues a pull that arrives before the round has finished
+ * (q_pull_reqmeta_, server.cc:286-305) and the engine thread answers it once
+ * COPY_MERGED is done (server.cc:100-114).  Here the call returns at once; a
+ * server-owned responder thread later calls
+ *   cb(ctx, key, data, len, status)
+ * with data/len = the zero-copy view byteps_server_pull_host_view would give
+ * (same validity), status 0, and counts the pull toward the key's re-arm when
+ * cb returns — so cb sends (or copies) the response before returning, as
+ * SendPullResponse does.  Pulls still waiting at byteps_server_destroy get
+ * status BYTEPS_REDUCE_ECANCELED and data NULL.  cb must not call back into
+ * the server for the same key. */
+typedef void (*byteps_server_pull_cb)(void* ctx, uint64_t key, const void* data, size_t len,
+                                      int status);
+int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_cb cb, void* ctx);
+
 /* Introspection for tests/debug (BYTEPS_SERVER_DEBUG analogue): completed
  * rounds, engine lane, and the arrival order of the last completed round. */
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,

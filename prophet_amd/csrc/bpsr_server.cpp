@@ -8,12 +8,14 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -32,6 +34,7 @@ struct Lane {
 };
 
 struct KeyState {
+  uint64_t key = 0;
   std::mutex mu;
   std::condition_variable cv;
   bool allocated = false;
@@ -61,6 +64,23 @@ struct KeyState {
   // itself).  Two buffers by round parity, filled by ONE D2H per round.
   char* mirror[2] = {nullptr, nullptr};
   hipEvent_t mirrored = nullptr;  // recorded on the lane's d2h stream
+  // byteps_server_pull_async requests waiting for this round to finish
+  // (the reference's q_pull_reqmeta_, server.cc:304)
+  struct Waiting {
+    byteps_server_pull_cb cb;
+    void* ctx;
+  };
+  std::vector<Waiting> waiting;
+};
+
+// A pull ready to be answered by the responder thread.
+struct Response {
+  uint64_t key;
+  KeyState* ks;
+  byteps_server_pull_cb cb;
+  void* ctx;
+  const char* view;  // mirror holding the answered round
+  int status;
 };
 
 }  // namespace
@@ -72,6 +92,13 @@ struct byteps_server {
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
   std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
+  // responder thread for byteps_server_pull_async (the engine threads'
+  // SendPullResponse of queued pulls, server.cc:100-114)
+  std::mutex rq_mu;
+  std::condition_variable rq_cv;
+  std::deque<bpsr::Response> rq;
+  bool rq_stop = false;
+  std::thread responder;
 };
 
 namespace bpsr {
@@ -102,6 +129,7 @@ KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
   if (it != s->keys.end()) return it->second.get();
   if (!create) return nullptr;
   auto ks = std::make_unique<KeyState>();
+  ks->key = key;
   KeyState* p = ks.get();
   s->keys.emplace(key, std::move(ks));
   return p;
@@ -169,6 +197,70 @@ int queue_mirror(byteps_server* s, KeyState* ks, uint64_t round) {
   return e == hipSuccess ? 0 : hip_fail(e, "store mirror copy");
 }
 
+// Pin the key's two store mirrors on first use (fixed addresses from then on,
+// as server.cc:60-69 reuses its response buffer to avoid re-registering
+// memory); with queue_now, also mirror the finished current round.  Caller
+// holds ks->mu.
+int ensure_mirror(byteps_server* s, KeyState* ks, bool queue_now) {
+  if (ks->mirror[0]) return 0;
+  hipError_t e;
+  for (char*& m : ks->mirror) {
+    void* p = nullptr;
+    if ((e = hipHostMalloc(&p, ks->len, hipHostMallocDefault)) != hipSuccess)
+      return hip_fail(e, "hipHostMalloc(store mirror)");
+    m = static_cast<char*>(p);
+  }
+  if ((e = hipEventCreateWithFlags(&ks->mirrored, hipEventDisableTiming)) != hipSuccess)
+    return hip_fail(e, "hipEventCreate");
+  return queue_now ? queue_mirror(s, ks, ks->rounds) : 0;
+}
+
+// Hand a ready pull of the current round to the responder (caller holds ks->mu).
+void respond_later(byteps_server* s, uint64_t key, KeyState* ks, byteps_server_pull_cb cb,
+                   void* ctx, int status) {
+  Response r{key, ks, cb, ctx, ks->mirror[ks->rounds & 1], status};
+  std::lock_guard<std::mutex> g(s->rq_mu);
+  s->rq.push_back(r);
+  s->rq_cv.notify_one();
+}
+
+// Count one answered pull; after NumWorkers the key re-arms (server.cc:105-113).
+// Caller holds ks->mu.
+void count_pull(byteps_server* s, KeyState* ks) {
+  if (s->cfg.async_mode) return;
+  if (++ks->pull_cnt == s->cfg.num_workers) {
+    ks->push_finished = false;
+    ks->pull_cnt = 0;
+  }
+  ks->cv.notify_all();
+}
+
+void responder_main(byteps_server* s) {
+  (void)hipSetDevice(s->cfg.device);
+  for (;;) {
+    Response r;
+    {
+      std::unique_lock<std::mutex> lk(s->rq_mu);
+      s->rq_cv.wait(lk, [&] { return s->rq_stop || !s->rq.empty(); });
+      if (s->rq.empty()) return;  // stopping and drained
+      r = s->rq.front();
+      s->rq.pop_front();
+    }
+    int status = r.status;
+    if (status == 0) {
+      // The event still names this round's copy: the next round cannot finish
+      // before this pull is counted below.
+      hipError_t e = hipEventSynchronize(r.ks->mirrored);
+      if (e != hipSuccess) status = hip_fail(e, "store mirror sync");
+    }
+    r.cb(r.ctx, r.key, status == 0 ? r.view : nullptr, status == 0 ? r.ks->len : 0, status);
+    if (r.status == 0) {
+      std::lock_guard<std::mutex> g(r.ks->mu);
+      count_pull(s, r.ks);
+    }
+  }
+}
+
 // A push's bytes are in slot w: advance the state machine (caller holds ks->mu).
 int arrive(byteps_server* s, KeyState* ks, int w) {
   const int N = s->cfg.num_workers;
@@ -234,6 +326,8 @@ int arrive(byteps_server* s, KeyState* ks, int w) {
   ks->rounds++;
   ks->push_finished = true;
   ks->pull_cnt = 0;
+  for (auto& wp : ks->waiting) respond_later(s, ks->key, ks, wp.cb, wp.ctx, 0);
+  ks->waiting.clear();
   ks->cv.notify_all();
   return 0;
 }
@@ -304,6 +398,12 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
       return hip_fail(e, "hipStreamCreate");
     }
   }
+  try {
+    s->responder = std::thread(responder_main, s.get());
+  } catch (...) {
+    byteps_server_destroy(s.release());
+    return fail(BYTEPS_REDUCE_EARGS, "cannot start the pull responder thread");
+  }
   *out = s.release();
   return BYTEPS_REDUCE_OK;
 }
@@ -311,6 +411,21 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
 int byteps_server_destroy(byteps_server* s) {
   if (!s) return BYTEPS_REDUCE_OK;
   (void)hipSetDevice(s->cfg.device);
+  if (s->responder.joinable()) {
+    for (auto& kv : s->keys) {  // pulls whose round never finished: cancelled
+      KeyState* ks = kv.second.get();
+      std::lock_guard<std::mutex> g(ks->mu);
+      for (auto& wp : ks->waiting)
+        respond_later(s, kv.first, ks, wp.cb, wp.ctx, BYTEPS_REDUCE_ECANCELED);
+      ks->waiting.clear();
+    }
+    {
+      std::lock_guard<std::mutex> g(s->rq_mu);
+      s->rq_stop = true;
+    }
+    s->rq_cv.notify_all();
+    s->responder.join();
+  }
   for (auto& L : s->lanes) {
     if (L.fold) (void)hipStreamSynchronize(L.fold);
     if (L.copy) (void)hipStreamSynchronize(L.copy);
@@ -444,19 +559,7 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   std::unique_lock<std::mutex> lk(ks->mu);
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished; });
   hipError_t e = hipSuccess;
-  if (!ks->mirror[0]) {  // first view of this key: pin the mirrors (fixed
-                         // addresses from now on, as server.cc:60-69 reuses its
-                         // response buffer to avoid re-registering memory)
-    for (char*& m : ks->mirror) {
-      void* p = nullptr;
-      if ((e = hipHostMalloc(&p, ks->len, hipHostMallocDefault)) != hipSuccess)
-        return hip_fail(e, "hipHostMalloc(store mirror)");
-      m = static_cast<char*>(p);
-    }
-    if ((e = hipEventCreateWithFlags(&ks->mirrored, hipEventDisableTiming)) != hipSuccess)
-      return hip_fail(e, "hipEventCreate");
-    if (!s->cfg.async_mode && (rc = queue_mirror(s, ks, ks->rounds))) return rc;
-  }
+  if ((rc = ensure_mirror(s, ks, !s->cfg.async_mode))) return rc;
   // async mode: the store changes with every push, so each view is a fresh D2H
   if (s->cfg.async_mode && (rc = queue_mirror(s, ks, ks->rounds))) return rc;
   const char* view = ks->mirror[ks->rounds & 1];
@@ -466,15 +569,33 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   // before this pull is counted below.
   if ((e = hipEventSynchronize(ev)) != hipSuccess) return hip_fail(e, "store mirror sync");
   lk.lock();
-  if (!s->cfg.async_mode) {
-    if (++ks->pull_cnt == s->cfg.num_workers) {  // server.cc:105-113
-      ks->push_finished = false;
-      ks->pull_cnt = 0;
-    }
-    ks->cv.notify_all();
-  }
+  count_pull(s, ks);
   *data = view;
   if (len) *len = ks->len;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_cb cb,
+                             void* ctx) {
+  if (!s || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated)  // server.cc:282-283
+    return fail(BYTEPS_REDUCE_EARGS,
+                "Processing pull request when the key %llu has not been inited yet",
+                (unsigned long long)key);
+  std::lock_guard<std::mutex> g(ks->mu);
+  if (s->cfg.async_mode) {  // answered at once from a fresh copy of the store
+    if ((rc = ensure_mirror(s, ks, false)) || (rc = queue_mirror(s, ks, ks->rounds))) return rc;
+    respond_later(s, key, ks, cb, ctx, 0);
+    return BYTEPS_REDUCE_OK;
+  }
+  if ((rc = ensure_mirror(s, ks, ks->push_finished))) return rc;
+  if (ks->push_finished)  // server.cc:293-301: push already finished
+    respond_later(s, key, ks, cb, ctx, 0);
+  else                    // server.cc:303-304: queued until the round finishes
+    ks->waiting.push_back({cb, ctx});
   return BYTEPS_REDUCE_OK;
 }
 

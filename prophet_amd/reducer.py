@@ -36,7 +36,7 @@ MAX_SRCS = 32
 MODE_REFERENCE = 0
 MODE_ACCUM_F32 = 1
 
-OK, EDTYPE, EARGS, EHIP, ERCCL, ETIMEOUT = 0, -1, -2, -3, -4, -5
+OK, EDTYPE, EARGS, EHIP, ERCCL, ETIMEOUT, ECANCELED = 0, -1, -2, -3, -4, -5, -6
 
 _vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
 

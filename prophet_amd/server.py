@@ -21,10 +21,12 @@ SERVER_EXPORTS = (
     "byteps_server_config_from_env", "byteps_server_create", "byteps_server_destroy",
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
-    "byteps_server_key_info",
+    "byteps_server_pull_async", "byteps_server_key_info",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+# void cb(void* ctx, uint64_t key, const void* data, size_t len, int status)
+PULL_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _vp, _sz, _int)
 
 
 class ServerConfig(ctypes.Structure):
@@ -45,6 +47,7 @@ def _lib():
         L.byteps_server_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
         L.byteps_server_pull_host_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
                                                    ctypes.POINTER(_sz)]
+        L.byteps_server_pull_async.argtypes = [_vp, _u64, PULL_CB, _vp]
         L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
                                              ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
         L._server_bound = True
@@ -74,6 +77,7 @@ class PSServer:
         self.lib = _lib()
         self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device)
         self.handle = _vp()
+        self._pending = {}
         _check(self.lib.byteps_server_create(ctypes.byref(self.cfg), ctypes.byref(self.handle)))
 
     def init_key(self, key: int, nbytes: int, dtype: int) -> None:
@@ -106,6 +110,29 @@ class PSServer:
                                                      ctypes.byref(n)))
         buf = (ctypes.c_char * n.value).from_address(p.value)
         return memoryview(buf).cast("B").toreadonly()
+
+    def pull_async(self, key: int, callback) -> None:
+        """Non-blocking pull (byteps_server_pull_async; server.cc:286-305 queues
+        it until the round finishes).  ``callback(key, view, status)`` runs on the
+        server's responder thread with ``view`` a read-only memoryview of the
+        round's host mirror (None unless status == 0); the pull counts toward
+        the key's re-arm when the callback returns."""
+        def tramp(_ctx, k, data, n, status):
+            try:
+                view = None
+                if status == 0:
+                    view = memoryview((ctypes.c_char * n).from_address(data)).cast("B") \
+                        .toreadonly()
+                callback(int(k), view, int(status))
+            finally:
+                self._pending.pop(token, None)
+        cfn = PULL_CB(tramp)
+        token = id(cfn)
+        self._pending[token] = cfn          # keep the thunk alive until it ran
+        rc = self.lib.byteps_server_pull_async(self.handle, key, cfn, None)
+        if rc != 0:
+            self._pending.pop(token, None)
+        _check(rc)
 
     def key_info(self, key: int):
         rounds, lane = _u64(), _int()

@@ -120,6 +120,7 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
     assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS
     assert lib.byteps_server_pull_host_view(None, 1, None, None) == reducer.EARGS
+    assert lib.byteps_server_pull_async(None, 1, server.PULL_CB(), None) == reducer.EARGS
 
 
 def test_block_queue_argument_errors_without_gpu():

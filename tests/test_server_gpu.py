@@ -278,3 +278,86 @@ def test_pull_host_view_async_and_errors(port):
         v = srv.pull_view(0)                           # async: answered at once
         assert np.array_equal(np.frombuffer(v, np.uint8), acc.view(np.uint8))
     srv.close()
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+def test_pull_async_queued_until_round_finishes(port, policy):
+    """byteps_server_pull_async: pulls issued before the round's pushes are
+    queued (q_pull_reqmeta_, server.cc:303-304) and answered by the responder
+    once the round finishes (server.cc:100-114) — never earlier; views are
+    bit-exact with the oracle fold in arrival order; callbacks count toward the
+    re-arm together with blocking pulls, so the next round proceeds."""
+    from prophet_amd.server import PSServer
+    dt, N = DType.FLOAT16, 4
+    sizes = [3, 262_147]
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2, policy=policy)
+    _init_round(srv, dt, N, sizes)
+    for rnd in range(1, 4):
+        got, fired = {}, threading.Semaphore(0)
+
+        def cb(key, view, status, w=None):
+            got[(w, key)] = (status, None if view is None else bytes(view))
+            fired.release()
+        nasync = 0
+        for j in range(len(sizes)):
+            for w in range(N):
+                if rnd == 2 and w == 0:
+                    continue                       # this one pulls blocking, below
+                srv.pull_async(j, lambda k, v, st, w=w: cb(k, v, st, w))
+                nasync += 1
+        wants = {}
+        for j, n in enumerate(sizes):
+            order = random.Random(rnd * 7 + j).sample(range(N), N)
+            for i, w in enumerate(order):
+                if i == N - 1:
+                    time.sleep(0.05)
+                    assert not any(k[1] == j for k in got), "answered before the round finished"
+                srv.push(j, w, data(dt, n, w, rnd, j), dt)
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, rnd, j) for w in order], n * es, dt)
+            wants[j] = want
+            if rnd == 2:
+                out = np.zeros(n * es, np.uint8)
+                srv.pull(j, out)
+                got[(0, j)] = (0, out.tobytes())
+        for _ in range(nasync):
+            assert fired.acquire(timeout=30)
+        for j in range(len(sizes)):
+            for w in range(N):
+                st, b = got[(w, j)]
+                assert st == 0
+                assert np.array_equal(np.frombuffer(b, np.uint8), wants[j]), (rnd, j, w)
+        for j in range(len(sizes)):
+            assert srv.key_info(j)[0] == rnd
+    srv.close()
+
+
+def test_pull_async_cancelled_at_shutdown_and_async_mode(port):
+    from prophet_amd.reducer import ECANCELED
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 1000
+    srv = PSServer(N)
+    _init_round(srv, dt, N, [n])
+    seen = []
+    done = threading.Event()
+    srv.pull_async(0, lambda k, v, st: (seen.append((k, v, st)), done.set()))
+    srv.push(0, 1, data(dt, n, 1, 1, 0), dt)       # round 1 never completes
+    srv.close()
+    assert done.wait(10) and seen == [(0, None, ECANCELED)]
+
+    srv = PSServer(N, async_mode=True)
+    init = data(dt, n, 0, 0, 0)
+    ts = [threading.Thread(target=srv.push, args=(0, w, init, dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    srv.push(0, 0, data(dt, n, 0, 5, 0), dt)
+    box = []
+    ev = threading.Event()
+    srv.pull_async(0, lambda k, v, st: (box.append((st, bytes(v))), ev.set()))
+    assert ev.wait(10)
+    want = (init.view(np.float32) + data(dt, n, 0, 5, 0).view(np.float32)).view(np.uint8)
+    assert box[0][0] == 0 and np.array_equal(np.frombuffer(box[0][1], np.uint8), want)
+    srv.close()
