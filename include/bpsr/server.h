@@ -71,6 +71,19 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
 int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data,
                        size_t len, int dtype, int location);
 
+/* Non-blocking push: queues the copy into the worker's slot and advances the
+ * state machine at once (arrival order = call order; the round's fold runs
+ * behind the copies on the device), then acknowledges from the server's
+ * responder thread with cb(ctx, key, worker, status) once the bytes are in HBM
+ * and `data` may be reused — the point at which the reference answers a push
+ * (server.cc:255 SendPushResponse).  Init pushes (round 0) do not wait for the
+ * other workers' init pushes.  Like byteps_server_push, a worker's push for the
+ * next round issued before the current round finished waits for it. */
+typedef void (*byteps_server_push_cb)(void* ctx, uint64_t key, int worker, int status);
+int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
+                             size_t len, int dtype, int location, byteps_server_push_cb cb,
+                             void* ctx);
+
 /* Zero-copy transport path: where worker `worker`'s push for `key` must land,
  * then the arrival notice once the bytes are there (visible to the device). */
 int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot);

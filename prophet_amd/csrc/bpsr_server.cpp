@@ -81,6 +81,8 @@ struct Response {
   void* ctx;
   const char* view;  // mirror holding the answered round
   int status;
+  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
+  int worker = -1;
 };
 
 }  // namespace
@@ -172,7 +174,8 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
 
 // Bring `len` bytes into worker `w`'s slot on the lane's copy stream, after
 // the previous round's fold has consumed the slot; wait for the copy.
-int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc) {
+int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc,
+            bool wait = true) {
   Lane& L = s->lanes[ks->lane];
   hipError_t e = hipSuccess;
   if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->done, 0);
@@ -181,7 +184,7 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
                        loc == BYTEPS_SERVER_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
                        L.copy);
   if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
-  if (e == hipSuccess) e = hipEventSynchronize(ks->copied);
+  if (e == hipSuccess && wait) e = hipEventSynchronize(ks->copied);
   return e == hipSuccess ? 0 : hip_fail(e, "push copy");
 }
 
@@ -246,6 +249,11 @@ void responder_main(byteps_server* s) {
       r = s->rq.front();
       s->rq.pop_front();
     }
+    if (r.push_cb) {  // the push's bytes are in HBM: the sender's buffer is free
+      hipError_t e = hipEventSynchronize(r.ks->copied);
+      r.push_cb(r.ctx, r.key, r.worker, e == hipSuccess ? 0 : hip_fail(e, "push copy sync"));
+      continue;
+    }
     int status = r.status;
     if (status == 0) {
       // The event still names this round's copy: the next round cannot finish
@@ -267,6 +275,12 @@ int arrive(byteps_server* s, KeyState* ks, int w) {
   Lane& L = s->lanes[ks->lane];
   void* fold_stream = reinterpret_cast<void*>(L.fold);
   int rc = 0;
+  // Folds run behind the slots' H2D copies (byteps_server_push_async returns
+  // before they finish; the copy stream is in order, so the last recorded copy
+  // covers every earlier one) and behind the last mirror D2H of the store.
+  hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
+  if (we == hipSuccess && ks->mirror[0]) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
+  if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
   if (!ks->inited) {
     // Round 0: server.cc:175-199 — after all NumWorkers init pushes the store
     // is initialised by copying the LAST arrived push.
@@ -475,6 +489,28 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   }
   if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
   return arrive_and_wait_init(s, ks, worker, lk);
+}
+
+int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
+                             size_t len, int dtype, int location, byteps_server_push_cb cb,
+                             void* ctx) {
+  if (!s || !data || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = get_key(s, key, true);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  if ((rc = allocate(s, ks, len, dtype))) return rc;
+  if (s->cfg.async_mode == 0 && ks->inited && ks->got[worker])
+    ks->cv.wait(lk, [&] { return !ks->got[worker]; });
+  if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
+  if ((rc = arrive(s, ks, worker))) return rc;  // arrival order = call order
+  Response r{key, ks, nullptr, ctx, nullptr, 0, cb, worker};
+  std::lock_guard<std::mutex> g(s->rq_mu);
+  s->rq.push_back(r);
+  s->rq_cv.notify_one();
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot) {

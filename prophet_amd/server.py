@@ -21,12 +21,14 @@ SERVER_EXPORTS = (
     "byteps_server_config_from_env", "byteps_server_create", "byteps_server_destroy",
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
-    "byteps_server_pull_async", "byteps_server_key_info",
+    "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
 # void cb(void* ctx, uint64_t key, const void* data, size_t len, int status)
 PULL_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _vp, _sz, _int)
+# void cb(void* ctx, uint64_t key, int worker, int status)
+PUSH_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _int, _int)
 
 
 class ServerConfig(ctypes.Structure):
@@ -48,6 +50,8 @@ def _lib():
         L.byteps_server_pull_host_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
                                                    ctypes.POINTER(_sz)]
         L.byteps_server_pull_async.argtypes = [_vp, _u64, PULL_CB, _vp]
+        L.byteps_server_push_async.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int, PUSH_CB,
+                                               _vp]
         L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
                                              ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
         L._server_bound = True
@@ -87,6 +91,30 @@ class PSServer:
         p, n, loc = _buf(data)
         _check(self.lib.byteps_server_push(self.handle, key, worker, p,
                                            n if nbytes is None else nbytes, int(dtype), loc))
+
+    def push_async(self, key: int, worker: int, data, dtype: int, callback=None,
+                   nbytes: int | None = None) -> None:
+        """Non-blocking push (byteps_server_push_async): returns once the copy is
+        queued and the arrival recorded; ``callback(key, worker, status)`` runs on
+        the responder thread when ``data`` may be reused.  ``data`` is kept
+        alive until then."""
+        p, n, loc = _buf(data)
+
+        def tramp(_ctx, k, w, status):
+            try:
+                if callback is not None:
+                    callback(int(k), int(w), int(status))
+            finally:
+                self._pending.pop(token, None)
+        cfn = PUSH_CB(tramp)
+        token = id(cfn)
+        self._pending[token] = (cfn, data)
+        rc = self.lib.byteps_server_push_async(self.handle, key, worker, p,
+                                               n if nbytes is None else nbytes, int(dtype),
+                                               loc, cfn, None)
+        if rc != 0:
+            self._pending.pop(token, None)
+        _check(rc)
 
     def recv_slot(self, key: int, worker: int) -> int:
         out = _vp()

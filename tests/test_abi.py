@@ -121,6 +121,8 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS
     assert lib.byteps_server_pull_host_view(None, 1, None, None) == reducer.EARGS
     assert lib.byteps_server_pull_async(None, 1, server.PULL_CB(), None) == reducer.EARGS
+    assert lib.byteps_server_push_async(None, 1, 0, None, 0, 0, 0, server.PUSH_CB(),
+                                        None) == reducer.EARGS
 
 
 def test_block_queue_argument_errors_without_gpu():
