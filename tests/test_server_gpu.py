@@ -361,3 +361,70 @@ def test_pull_async_cancelled_at_shutdown_and_async_mode(port):
     want = (init.view(np.float32) + data(dt, n, 0, 5, 0).view(np.float32)).view(np.uint8)
     assert box[0][0] == 0 and np.array_equal(np.frombuffer(box[0][1], np.uint8), want)
     srv.close()
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+def test_push_async_rounds(port, policy):
+    """byteps_server_push_async: arrival order = call order (init: the store is
+    the LAST call's data, server.cc:175-199), the fold runs behind the H2D copies
+    on the device, the acknowledgement (server.cc:255) comes once the bytes are
+    in HBM — the test then scribbles over the sender's buffer, and the round's
+    result must not change; blocking pulls, views and async pulls all agree."""
+    from prophet_amd.server import PSServer
+    dt, N = DType.FLOAT32, 4
+    sizes = [9, 500_003]
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2, policy=policy)
+    acks = threading.Semaphore(0)
+    status = []
+
+    def ack(key, w, st, buf=None):
+        status.append(st)
+        if buf is not None:
+            buf[:] = 0xEE                       # the sender reuses its buffer
+        acks.release()
+    for j, n in enumerate(sizes):                # init round, non-blocking
+        for w in range(N):
+            b = data(dt, n, w, 0, j).copy()
+            srv.push_async(j, w, b, dt, lambda k, ww, st, b=b: ack(k, ww, st, b))
+    for _ in range(N * len(sizes)):
+        assert acks.acquire(timeout=30)
+    for rnd in range(1, 4):
+        for j, n in enumerate(sizes):
+            order = random.Random(100 * rnd + j).sample(range(N), N)
+            for w in order:
+                b = data(dt, n, w, rnd, j).copy()
+                srv.push_async(j, w, b, dt, lambda k, ww, st, b=b: ack(k, ww, st, b))
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, rnd, j) for w in order], n * es, dt)
+            for w in range(N):
+                if w == 0:
+                    out = np.zeros(n * es, np.uint8)
+                    srv.pull(j, out)
+                else:
+                    out = np.frombuffer(srv.pull_view(j), np.uint8)
+                assert np.array_equal(out, want), (rnd, j, w)
+            assert srv.key_info(j)[2] == order
+        for _ in range(N * len(sizes)):
+            assert acks.acquire(timeout=30)
+    assert status and all(st == 0 for st in status)
+    # round 1's expected values were built from the init stores: init = last call
+    srv.close()
+
+
+def test_push_async_init_store_is_last_call(port):
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT16, 3, 4099
+    srv = PSServer(N)
+    done = threading.Semaphore(0)
+    for w in (2, 0, 1):                          # worker 1's init push arrives last
+        srv.push_async(0, w, data(dt, n, w, 0, 0), dt, lambda k, ww, st: done.release())
+    for _ in range(N):
+        assert done.acquire(timeout=30)
+    for w in range(N):
+        srv.push_async(0, w, np.zeros(n * 2, np.uint8), dt)
+    out = np.zeros(n * 2, np.uint8)
+    srv.pull(0, out)                             # 0 + 0 + 0 in fp16: +0 bits
+    assert not out.any()
+    assert srv.key_info(0)[0] == 1
+    srv.close()

@@ -469,9 +469,10 @@ def cfg1(dev, N=2, B=64 << 20):
                 srv.close()
     cfg1_pipelined(host, N, B)
     cfg1_pipelined(host, N, B, view=True)
+    cfg1_pipelined(host, N, B, view=True, push_async=True)
 
 
-def cfg1_pipelined(host, N, B, view=False):
+def cfg1_pipelined(host, N, B, view=False, push_async=False):
     """cfg1 with BytePS's worker loop structure: each worker has a push thread
     and a pull thread (core_loops.cc:492-528 PushLoop, 530-564 PullLoop); the
     pull of a partition is issued as soon as that partition's push returned, so
@@ -479,14 +480,17 @@ def cfg1_pipelined(host, N, B, view=False):
     view=True: pulls are zero-copy responses (byteps_server_pull_host_view, the
     analogue of server.cc:42-70 answering from the store's SArray): one D2H per
     key per round into a pinned mirror that a transport would send from, instead
-    of one D2H per puller.  The exactness round copies the views out."""
+    of one D2H per puller.  The exactness round copies the views out.
+    push_async=True: pushes are non-blocking (byteps_server_push_async): a push
+    thread queues all its partitions' H2D copies back to back."""
     import threading
     import torch
     from prophet_amd.buckets import partition_tensor
     from prophet_amd.dtypes import DType
     from prophet_amd.server import PSServer
     parts = [(p.key, p.offset, p.len) for p in partition_tensor(0, B)]
-    srv = PSServer(N, engine_lanes=4, policy=0)
+    lanes = int(os.environ.get("BPSR_CFG1_LANES", "4"))
+    srv = PSServer(N, engine_lanes=lanes, policy=0)
     outs = [torch.empty(B, dtype=torch.uint8).pin_memory() for _ in range(N)]
 
     import numpy as np
@@ -497,7 +501,10 @@ def cfg1_pipelined(host, N, B, view=False):
         def pusher(k):
             b = host[k].view(torch.uint8)
             for i, (key, off, ln) in enumerate(parts):
-                srv.push(key, k, b[off:off + ln], DType.FLOAT32)
+                if push_async:
+                    srv.push_async(key, k, b[off:off + ln], DType.FLOAT32)
+                else:
+                    srv.push(key, k, b[off:off + ln], DType.FLOAT32)
                 pushed[k][i].set()
 
         def puller(k):
@@ -530,8 +537,9 @@ def cfg1_pipelined(host, N, B, view=False):
     for h in host[1:]:
         want += h
     ok = all(bool(torch.equal(o, want.view(torch.uint8))) for o in outs)
-    emit(config="cfg1", layout="17keys_push_pull_threads" + ("_pull_view" if view else ""),
-         pushes_from="host", policy="fused",
+    emit(config="cfg1", layout="17keys_push_pull_threads" + ("_pull_view" if view else "")
+         + ("_push_async" if push_async else ""),
+         pushes_from="host", policy="fused", lanes=lanes,
          n_workers=N, bucket_bytes=B, round_ms=round(med * 1e3, 3),
          gibps=round(N * B / med / GIB, 2), exact=ok)
     srv.close()
