@@ -27,9 +27,25 @@
 typedef float f4 __attribute__((ext_vector_type(4)));
 struct Ops { char* p[17]; };
 
-template <int LAUX, int SAUX, int VPT, bool INPLACE, int NSRC = 8, bool INDEP = false>
+// XMAP: blockIdx -> tile.  0 = identity (the product: dispatch order = address
+// order); 1 = one contiguous range of tiles per XCD (workgroups go to XCDs
+// round-robin, blockIdx % 8); C > 1 = chunks of C consecutive tiles per XCD,
+// the 8 XCDs' chunks adjacent (needs grid % (8*C) == 0).
+template <int XMAP>
+__device__ __forceinline__ unsigned xcd_tile(unsigned bid, unsigned grid) {
+  if (XMAP == 0) return bid;
+  const unsigned x = bid % 8u, k = bid / 8u;
+  if (XMAP == 1) {
+    const unsigned per = grid / 8u, rem = grid % 8u;
+    return x * per + (x < rem ? x : rem) + k;
+  }
+  return ((k / XMAP) * 8u + x) * XMAP + k % XMAP;
+}
+
+template <int LAUX, int SAUX, int VPT, bool INPLACE, int NSRC = 8, bool INDEP = false,
+          int XMAP = 0>
 __global__ __launch_bounds__(256) void fold8(Ops o, unsigned bytes_per_op) {
-  const unsigned tile = blockIdx.x;
+  const unsigned tile = xcd_tile<XMAP>(blockIdx.x, gridDim.x);
   const unsigned off0 = (tile * 256u * VPT + threadIdx.x) * 16u;
   __amdgpu_buffer_rsrc_t r[NSRC + 1];
 #pragma unroll
@@ -122,10 +138,12 @@ struct V {
   const char* name;
   void (*fn)(Ops, unsigned, int, hipStream_t);
 };
-template <int LA, int SA, int VPT, bool IP, int NS = 8, bool IND = false, int LDS_KB = 0>
+template <int LA, int SA, int VPT, bool IP, int NS = 8, bool IND = false, int LDS_KB = 0,
+          int XMAP = 0>
 static void L(Ops o, unsigned b, int grid, hipStream_t s) {
   // LDS_KB of dynamic LDS per workgroup caps residency (160 KiB per CU)
-  hipLaunchKernelGGL((fold8<LA, SA, VPT, IP, NS, IND>), dim3(grid), dim3(256), LDS_KB * 1024, s, o, b);
+  hipLaunchKernelGGL((fold8<LA, SA, VPT, IP, NS, IND, XMAP>), dim3(grid), dim3(256), LDS_KB * 1024,
+                     s, o, b);
 }
 
 template <int VPT, int NS, int GRID_PER_CU, int LDS_KB>
@@ -156,6 +174,11 @@ int main(int argc, char** argv) {
       {"n8", L<2, 2, 4, false, 8>},
       {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
       {"n8_product", PROD<8>},
+      {"n8_v2_wg1cu_xcdrange", L<2, 2, 2, false, 8, false, 160, 1>},
+      {"n8_v2_wg1cu_xcdchunk4", L<2, 2, 2, false, 8, false, 160, 4>},
+      {"n8_v2_wg1cu_xcdchunk64", L<2, 2, 2, false, 8, false, 160, 64>},
+      {"n8_v2_hw_xcdrange", L<2, 2, 2, false, 8, false, 0, 1>},
+      {"n8_v2_hw", L<2, 2, 2, false, 8, false, 0, 0>},
       {"n8_v1_wg2cu", L<2, 2, 1, false, 8, false, 80>},
       {"n8_v4_wg1cu", L<2, 2, 4, false, 8, false, 160>},
       {"n1_copy", L<2, 2, 4, false, 1>},
