@@ -63,6 +63,7 @@ struct KeyState {
   // (byteps_server_pull_host_view; server.cc:42-70 responds from the store
   // itself).  Two buffers by round parity, filled by ONE D2H per round.
   char* mirror[2] = {nullptr, nullptr};
+  void* mirror_dev[2] = {nullptr, nullptr};  // the same pages as the device sees them
   hipEvent_t mirrored = nullptr;  // recorded on the lane's d2h stream
   // byteps_server_pull_async requests waiting for this round to finish
   // (the reference's q_pull_reqmeta_, server.cc:304)
@@ -194,9 +195,15 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
 int queue_mirror(byteps_server* s, KeyState* ks, uint64_t round) {
   Lane& L = s->lanes[ks->lane];
   hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(ks->mirror[round & 1], ks->store, ks->len, hipMemcpyDeviceToHost, L.d2h);
-  if (e == hipSuccess) e = hipEventRecord(ks->mirrored, L.d2h);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+  // The copy kernel writes the pinned mirror straight over PCIe.  A
+  // hipMemcpyAsync D2H queued behind a pending event wait was handed to an SDMA
+  // engine that ran at ~13 GB/s beside the H2D pushes (rocprofv3 memory-copy
+  // trace); the kernel path runs at the link's rate.
+  int rc = byteps_reduce_copy(ks->mirror_dev[round & 1], ks->store, ks->len,
+                              reinterpret_cast<void*>(L.d2h));
+  if (rc) return rc;
+  e = hipEventRecord(ks->mirrored, L.d2h);
   return e == hipSuccess ? 0 : hip_fail(e, "store mirror copy");
 }
 
@@ -207,11 +214,13 @@ int queue_mirror(byteps_server* s, KeyState* ks, uint64_t round) {
 int ensure_mirror(byteps_server* s, KeyState* ks, bool queue_now) {
   if (ks->mirror[0]) return 0;
   hipError_t e;
-  for (char*& m : ks->mirror) {
+  for (int i = 0; i < 2; ++i) {
     void* p = nullptr;
     if ((e = hipHostMalloc(&p, ks->len, hipHostMallocDefault)) != hipSuccess)
       return hip_fail(e, "hipHostMalloc(store mirror)");
-    m = static_cast<char*>(p);
+    ks->mirror[i] = static_cast<char*>(p);
+    if ((e = hipHostGetDevicePointer(&ks->mirror_dev[i], p, 0)) != hipSuccess)
+      return hip_fail(e, "hipHostGetDevicePointer(store mirror)");
   }
   if ((e = hipEventCreateWithFlags(&ks->mirrored, hipEventDisableTiming)) != hipSuccess)
     return hip_fail(e, "hipEventCreate");

@@ -1,4 +1,4 @@
-mkdir -p gpurun_out/r01s46
+OUT=gpurun_out/${TAG:-r01_lanes}; mkdir -p $OUT
 for l in 1 2 4 8; do BPSR_CFG1_LANES=$l timeout -k 10 200 python -c "
 import sys; sys.path.insert(0,'tools'); sys.path.insert(0,'.')
 import torch, bench_configs as b
@@ -7,4 +7,4 @@ N,B=2,64<<20
 host=[torch.randn(B//4).pin_memory() for _ in range(N)]
 b.cfg1_pipelined(host,N,B,view=True)
 b.cfg1_pipelined(host,N,B,view=True,push_async=True)
-" >> gpurun_out/r01s46/lanes.log 2>&1 || exit 1; done
+" >> $OUT/lanes.log 2>&1 || exit 1; done
