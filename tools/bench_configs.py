@@ -372,29 +372,44 @@ def cfg4(red, dev, N=8):
 def cfg5(red, dev, N=16, B=256 << 20, chunk=32 << 20):
     import torch
     from prophet_amd.dtypes import DType
+    streamed(red, dev, "cfg5", N, B, torch.bfloat16, DType.BFLOAT16, chunk)
+
+
+def cfg2_e2e(red, dev, N=8, B=256 << 20, chunk=32 << 20):
+    """Config 2's workload (8 x 256 MiB fp32) from pinned host memory to a pinned
+    host result through the streaming path: the PCIe-inclusive rate the north
+    star asks DESIGN.md to record beside the device-resident headline."""
+    import torch
+    from prophet_amd.dtypes import DType
+    streamed(red, dev, "cfg2_e2e", N, B, torch.float32, DType.FLOAT32, chunk)
+
+
+def streamed(red, dev, name, N, B, tdt, dtype_id, chunk):
+    import torch
     from prophet_amd.stream import StreamingReducer
-    n = B // 2
+    es = torch.empty(0, dtype=tdt).element_size()
+    n = B // es
     t0 = time.perf_counter()
     host = [torch.empty(B, dtype=torch.uint8, pin_memory=True) for _ in range(N)]
     g = torch.Generator()
     for k, h in enumerate(host):
         g.manual_seed(1000 + k)
-        h.view(torch.bfloat16).copy_(torch.randn(n, generator=g))
+        h.view(tdt).copy_(torch.randn(n, generator=g))
     out = torch.empty(B, dtype=torch.uint8, pin_memory=True)
     setup_s = time.perf_counter() - t0
     sr = StreamingReducer(N, chunk_bytes=chunk, depth=3, device=dev, reducer=red)
-    sr.reduce(host, out, B, DType.BFLOAT16)          # warm-up
+    sr.reduce(host, out, B, dtype_id)                # warm-up
     ts = []
     for _ in range(3):
         t = time.perf_counter()
-        sr.reduce(host, out, B, DType.BFLOAT16)
+        sr.reduce(host, out, B, dtype_id)
         ts.append(time.perf_counter() - t)
     med = statistics.median(ts)
-    # check a 16 MiB window against torch's bf16 left fold on the device
+    # check an 8 MiB window against torch's left fold on the device
     w = 8 << 20
-    acc = host[0][:w].to(dev).view(torch.bfloat16).clone()
+    acc = host[0][:w].to(dev).view(tdt).clone()
     for h in host[1:]:
-        acc.add_(h[:w].to(dev).view(torch.bfloat16))
+        acc.add_(h[:w].to(dev).view(tdt))
     ok = bool(torch.equal(acc.view(torch.uint8).cpu(), out[:w]))
     # bare H2D of the same N*B bytes into one device buffer (reference rate)
     dbuf = torch.empty(chunk, dtype=torch.uint8, device=dev)
@@ -405,7 +420,7 @@ def cfg5(red, dev, N=16, B=256 << 20, chunk=32 << 20):
             dbuf.copy_(h[o:o + chunk], non_blocking=True)
     torch.cuda.synchronize()
     h2d = time.perf_counter() - t
-    emit(config="cfg5", n_workers=N, bucket_bytes=B, total_bytes=N * B, chunk_bytes=chunk,
+    emit(config=name, n_workers=N, bucket_bytes=B, total_bytes=N * B, chunk_bytes=chunk,
          e2e_s=round(med, 4), e2e_gibps=round(N * B / med / GIB, 2),
          h2d_only_gibps=round(N * B / h2d / GIB, 2), e2e_over_h2d=round(h2d / med, 3),
          host_setup_s=round(setup_s, 1), exact_window=ok)
@@ -547,7 +562,7 @@ def cfg1_pipelined(host, N, B, view=False, push_async=False):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--only", default="cfg1,cfg3,sweep,cfg4,cfg5")
+    p.add_argument("--only", default="cfg1,cfg3,sweep,cfg4,cfg5,cfg2e2e")
     p.add_argument("--variants", default="all", help="cfg3: all | blockq")
     a = p.parse_args()
     global VARIANTS
@@ -567,6 +582,8 @@ def main():
         cfg4(red, dev)
     if "cfg5" in todo:
         cfg5(red, dev)
+    if "cfg2e2e" in todo:
+        cfg2_e2e(red, dev)
 
 
 if __name__ == "__main__":
