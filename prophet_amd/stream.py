@@ -10,7 +10,12 @@ one GPU with three HIP streams and a ring of device chunk slots:
     compute stream:  fold(slot) -> out slot           (byteps_reduce_sum_n)
     d2h stream:      out slot -> host result chunk
 
-so PCIe transfers in both directions overlap the fold.  Chunks are multiples
+so PCIe transfers in both directions overlap the fold.  ``zero_copy=True``
+instead runs ONE fold whose loads and stores go straight to the pinned host
+pages over PCIe (device addresses from ``hipHostGetDevicePointer``): no device
+staging and no copy engines, the same PCIe ceiling (config 2's workload: 51.8
+vs 51.0 GiB/s), but the kernel holds the CUs for the whole
+transfer, so it suits a GPU with nothing else to run.  Chunks are multiples
 of 16 bytes and of 8 elements, so the fp16 F16C body/tail split
 (cpu_reducer.cc:103,118) falls exactly where an unchunked call would put it,
 and the result is bit-identical to one ``sum_n`` over the whole bucket.
@@ -23,9 +28,10 @@ from .reducer import GpuReducer, MODE_REFERENCE
 
 class StreamingReducer:
     def __init__(self, n_workers: int, chunk_bytes: int = 32 << 20, depth: int = 3,
-                 device=None, reducer: GpuReducer | None = None):
+                 device=None, reducer: GpuReducer | None = None, zero_copy: bool = False):
         import torch
         self.torch = torch
+        self.zero_copy = zero_copy
         self.dev = torch.device(device if device is not None else "cuda")
         self.n_workers = n_workers
         self.chunk = max(128, (int(chunk_bytes) // 128) * 128)
@@ -51,6 +57,13 @@ class StreamingReducer:
         torch = self.torch
         if len(host_srcs) != self.n_workers:
             raise ValueError("expected one host buffer per worker")
+        if self.zero_copy:
+            srcs = [_Dev(_host_device_ptr(h)) for h in host_srcs]
+            with torch.cuda.stream(self.s_cmp):
+                self.red.sum_n(_Dev(_host_device_ptr(host_dst)), srcs, length, dtype, mode,
+                               stream=self.s_cmp)
+            self.s_cmp.synchronize()
+            return
         es = elem_size(dtype)
         step = self.chunk // (8 * es) * (8 * es)      # whole 8-element groups
         if step == 0:
@@ -80,3 +93,34 @@ class StreamingReducer:
             off += ln
             c += 1
         self.s_d2h.synchronize()
+
+
+class _Dev:
+    """A device address in the shape the reducer takes (``data_ptr()``)."""
+    def __init__(self, p: int):
+        self.p = p
+
+    def data_ptr(self) -> int:
+        return self.p
+
+
+_hip = None
+
+
+def _host_device_ptr(t) -> int:
+    """Device address of a pinned host tensor (hipHostGetDevicePointer); raises
+    for memory the device cannot address (pageable host memory)."""
+    import ctypes
+    from .reducer import EARGS, ReduceError
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+        _hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.c_void_p, ctypes.c_uint]
+    p = ctypes.c_void_p()
+    rc = _hip.hipHostGetDevicePointer(ctypes.byref(p), ctypes.c_void_p(int(t.data_ptr())), 0)
+    if rc != 0 or not p.value:
+        _hip.hipGetLastError()     # do not leave the error for torch's next check
+        raise ReduceError(EARGS, f"zero_copy needs pinned host buffers (hipHostGetDevicePointer "
+                                 f"returned {rc})")
+    return int(p.value)

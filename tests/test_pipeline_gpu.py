@@ -22,7 +22,8 @@ def red():
 @pytest.mark.parametrize("dt", [DType.BFLOAT16, DType.FLOAT16, DType.FLOAT32, DType.INT8],
                          ids=lambda d: DType(d).name)
 @pytest.mark.parametrize("extra", [0, 1, 7])
-def test_streaming_reducer_bit_exact(red, dt, extra):
+@pytest.mark.parametrize("zero_copy", [False, True], ids=["sdma", "zerocopy"])
+def test_streaming_reducer_bit_exact(red, dt, extra, zero_copy):
     from prophet_amd.stream import StreamingReducer
     es = elem_size(dt)
     n = 300_007
@@ -32,11 +33,21 @@ def test_streaming_reducer_bit_exact(red, dt, extra):
            .view(np.uint8)[:L].copy() for k in range(N)]
     host = [torch.from_numpy(x).pin_memory() for x in ins]
     out = torch.zeros(L, dtype=torch.uint8).pin_memory()
-    sr = StreamingReducer(N, chunk_bytes=64 * 1024 + 48, depth=3, reducer=red)
+    sr = StreamingReducer(N, chunk_bytes=64 * 1024 + 48, depth=3, reducer=red,
+                          zero_copy=zero_copy)
     sr.reduce(host, out, L, dt)
     want = np.zeros(L, np.uint8)
     PortReducer(nthreads=4).sum_n(want, ins, L, dt)
     assert_bytes_match(dt, out.numpy(), want, nan_class_f32_f64=False)
+
+
+def test_streaming_zero_copy_rejects_pageable(red):
+    from prophet_amd.reducer import ReduceError
+    from prophet_amd.stream import StreamingReducer
+    sr = StreamingReducer(2, reducer=red, zero_copy=True)
+    host = [torch.zeros(64, dtype=torch.uint8) for _ in range(2)]     # not pinned
+    with pytest.raises(ReduceError):
+        sr.reduce(host, torch.zeros(64, dtype=torch.uint8).pin_memory(), 64, DType.UINT8)
 
 
 def test_sharded_reducer_single_rank(red):
