@@ -162,7 +162,16 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * time.  Table residency as for plans (buffers fixed after InitTensor).  When
  * a block's data lands after the launch, its buffers should not share a 128-B
  * line with an earlier block's (a line read for the earlier block may be
- * cached ahead of the later block's DMA). */
+ * cached ahead of the later block's DMA).
+ *
+ * Live releases need the consumer and the releasing stream on DIFFERENT
+ * hardware queues: HIP multiplexes streams onto a few in-order hardware queues
+ * per process (GPU_MAX_HW_QUEUES, 4 by default), and a release queued behind
+ * the running consumer in a shared queue cannot run until the consumer gives
+ * up (timeout, ETIMEOUT; the grid always drains).  Launch the consumer on a
+ * stream of higher priority than the streams that copy and release
+ * (hipStreamCreateWithPriority): priorities get separate hardware queues.
+ * Releases on the launch stream itself, before the launch, are always safe. */
 typedef struct byteps_reduce_blockq byteps_reduce_blockq;
 int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                                 const int* block_end, int nblocks, int dtype, int mode,

@@ -133,7 +133,9 @@ def test_live_release_after_dma(red, dev, occ):
     tab = Table(dev, dt, blocks)
     q = red.make_blockq(tab.blocks, dt)
     q.config(wg_per_cu=occ, timeout_s=5.0)
-    comp, copy = torch.cuda.Stream(), torch.cuda.Stream()
+    # the consumer on a high-priority stream: its own hardware queue, so the
+    # copy stream's DMA and releases never queue behind it (include/bpsr/reduce.h)
+    comp, copy = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
     for it in range(2):
         pushes, wants = tab.host_inputs(1000 * it + 3)
         torch.cuda.synchronize()
@@ -165,7 +167,7 @@ def test_out_of_order_release_waits_for_prefix(red, dev, shape):
     pushes, wants = tab.host_inputs(55)
     tab.upload(pushes)
     torch.cuda.synchronize()
-    comp, side = torch.cuda.Stream(), torch.cuda.Stream()
+    comp, side = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
     q.launch(comp)
     for b in reversed(range(len(blocks))):
         q.release(b, side)

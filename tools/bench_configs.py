@@ -230,6 +230,11 @@ def cfg3(red, dev, N=8, sets=3):
         bq_variants.append((f"prophet_blockq_{nm}_hipgraph", blockq_graph(occ)))
 
     rel_stream = torch.cuda.Stream()
+    # The live consumer runs on a high-priority stream: a hardware queue of its
+    # own, so the releases on rel_stream never sit behind it in a shared queue
+    # (include/bpsr/reduce.h; under rocprofv3 with both at normal priority the
+    # first live launch of each queue waited out its 5-s timeout).
+    live_stream = torch.cuda.Stream(priority=-100)
 
     def blockq_live(i, occ=0):
         """Consumer launched first on s; the 12 releases follow on another
@@ -240,9 +245,13 @@ def cfg3(red, dev, N=8, sets=3):
         ev = torch.cuda.Event()
         ev.record(s)
         rel_stream.wait_event(ev)
-        bq.launch(s)
+        live_stream.wait_event(ev)
+        bq.launch(live_stream)
         for b in range(len(by_block)):
             bq.release(b, rel_stream)
+        done = torch.cuda.Event()
+        done.record(live_stream)
+        s.wait_event(done)
 
     bq_variants.append(("prophet_blockq_dispatch_live_release", blockq_live))
     bq_variants.append(("prophet_blockq_persistent_live_release",
