@@ -131,6 +131,20 @@ class ShardedReducer:
         if self.owned:
             self.fold(dst, list(recv_slots))
 
+    def reduce_from_host(self, host_pushes, recv_slots, dst) -> None:
+        """Pushes that start in host memory (ps-lite receive buffers / BytePS
+        shm, server.cc:174, shared_memory.cc:28-49) land straight on their
+        owner: each rank copies only ITS slice of every worker's push host ->
+        its own HBM (``recv_slots[k]``, non-blocking from pinned memory) and
+        folds it — no collective, and the node's PCIe links work in parallel,
+        one per GPU (the scatter over xGMI is the fallback for
+        pushes that already sit on one GPU)."""
+        if not self.owned:
+            return
+        for k, h in enumerate(host_pushes):
+            recv_slots[k].copy_(h[self.lo:self.hi], non_blocking=True)
+        self.fold(dst, list(recv_slots))
+
     def reduce_scatter(self, local_full, recv_slots, dst) -> None:
         """Worker local reduce (REDUCE stage, core_loops.cc:184-247): every rank
         holds its own full gradient vector ``local_full`` (n_elems); rank g

@@ -50,6 +50,30 @@ def test_streaming_zero_copy_rejects_pageable(red):
         sr.reduce(host, torch.zeros(64, dtype=torch.uint8).pin_memory(), 64, DType.UINT8)
 
 
+def test_sharded_reduce_from_host_single_rank(red):
+    """reduce_from_host: the owner's slice of pinned host pushes straight to its
+    HBM slots, HIP fold; equal to torch's left fold."""
+    import torch.distributed as dist
+    from prophet_amd.shard import ShardedReducer
+    if not dist.is_initialized():
+        import os
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    n = 200_003
+    sr = ShardedReducer(n)
+    dev = torch.device("cuda:0")
+    host = [torch.randn(n).pin_memory() for _ in range(6)]
+    slots = [torch.empty(sr.owned, device=dev) for _ in range(6)]
+    owned = torch.empty(sr.owned, device=dev)
+    sr.reduce_from_host(host, slots, owned)
+    torch.cuda.synchronize()
+    ref = host[0].clone()
+    for h in host[1:]:
+        ref.add_(h)
+    assert torch.equal(owned.cpu(), ref)
+
+
 def test_sharded_reducer_single_rank(red):
     import torch.distributed as dist
     from prophet_amd.shard import ShardedReducer

@@ -65,7 +65,7 @@ def _oracle_fold():
     return fold
 
 
-def _worker(rank, world, port, n_elems, n_workers, q):
+def _worker(rank, world, port, n_elems, n_workers, q, mode="scatter"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -75,12 +75,15 @@ def _worker(rank, world, port, n_elems, n_workers, q):
         sr = ShardedReducer(n_elems, fold=_oracle_fold())
         root = 0
         pushes = None
-        if rank == root:
+        if rank == root or mode == "host":   # "host": every rank sees the shm pushes
             pushes = [torch.from_numpy(synth.bucket(DType.FLOAT32, n_elems, k, "normal", 77))
                       for k in range(n_workers)]
         slots = [torch.empty(sr.owned, dtype=torch.float32) for _ in range(n_workers)]
         owned = torch.empty(sr.owned, dtype=torch.float32)
-        sr.scatter_reduce(root, pushes, slots, owned)
+        if mode == "host":
+            sr.reduce_from_host(pushes, slots, owned)
+        else:
+            sr.scatter_reduce(root, pushes, slots, owned)
         full = torch.empty(n_elems, dtype=torch.float32)
         sr.allgather(owned, full)
         q.put((rank, full.numpy().tobytes()))
@@ -92,12 +95,16 @@ def _worker(rank, world, port, n_elems, n_workers, q):
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
-def test_scatter_reduce_allgather_gloo(world):
+@pytest.mark.parametrize("mode", ["scatter", "host"])
+def test_scatter_reduce_allgather_gloo(world, mode):
+    """Pushes on rank 0 scattered to owners (scatter_reduce), or read from host
+    memory by every owner directly (reduce_from_host): the gathered result is
+    the unsharded left fold, bit for bit."""
     n_elems, n_workers = 10_007, 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_elems, n_workers, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_elems, n_workers, q, mode))
              for r in range(world)]
     for p in procs:
         p.start()
