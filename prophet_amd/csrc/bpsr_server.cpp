@@ -514,7 +514,11 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
   if (s->cfg.async_mode == 0 && ks->inited && ks->got[worker])
     ks->cv.wait(lk, [&] { return !ks->got[worker]; });
   if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
-  if ((rc = arrive(s, ks, worker))) return rc;  // arrival order = call order
+  if ((rc = arrive(s, ks, worker))) {  // arrival order = call order
+    // the caller gets its buffer back on error: let the queued copy finish first
+    (void)hipEventSynchronize(ks->copied);
+    return rc;
+  }
   Response r{key, ks, nullptr, ctx, nullptr, 0, cb, worker};
   std::lock_guard<std::mutex> g(s->rq_mu);
   s->rq.push_back(r);
