@@ -428,3 +428,16 @@ def test_push_async_init_store_is_last_call(port):
     assert not out.any()
     assert srv.key_info(0)[0] == 1
     srv.close()
+
+
+def test_push_async_error_returns_buffer(port):
+    """A state-machine error (a second init push from one worker) is reported
+    by push_async itself, after its queued copy has finished."""
+    from prophet_amd.reducer import ReduceError
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 1000
+    srv = PSServer(N)
+    srv.push_async(0, 0, data(dt, n, 0, 0, 0), dt)
+    with pytest.raises(ReduceError):
+        srv.push_async(0, 0, data(dt, n, 0, 0, 0), dt)
+    srv.close()
