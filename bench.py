@@ -8,22 +8,36 @@ of one 256 MiB bucket per GPU — the server round of byteps/server/server.cc:
 resident in HBM before the timed region; 3 input sets are rotated so every
 step streams from HBM rather than the 256 MiB Infinity Cache.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
-per GPU; each GPU owns a contiguous slice of the key space and reduces its own
-256 MiB bucket per step (weak scaling, no data-path collective — the sum is
-element-wise).  Barrier + synchronize bracket the timed steps, the max over
-ranks is taken, and value = total gradient bytes aggregated by all ranks / time.
+Multi-GPU: one process per GPU, either launched by the driver
+(``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``:
+RANK/LOCAL_RANK/WORLD_SIZE come from the environment) or by this script
+itself (``python bench.py --gpus N`` with no WORLD_SIZE set: the parent starts
+N rank processes BEFORE it touches the GPU, waits, and exits with their
+status; rank 0 prints the line).  Each GPU owns a contiguous slice of the key
+space and reduces its own 256 MiB bucket per step (weak scaling, no data-path
+collective — the sum is element-wise).  Barrier + synchronize bracket the
+timed steps, the max over ranks is taken, and value = total gradient bytes
+aggregated by all ranks / time.
+
+``scaling`` (every N): BASELINE config 4 — the 8-way fp32 VGG-16 gradient set
+(553,430,176 B per worker) sharded over the N GPUs by the reference's
+reduce-scatter ownership (core_loops.cc:208-247): per-GPU fold time of the
+owned slice (max over ranks), the G=1 time of the whole set measured in the
+same run, strong-scaling speedup/efficiency, and, for N > 1, the RCCL P2P
+scatter from a landing GPU plus the all-gather return leg.
 
 Prints ONE JSON line (rank 0).  Metric: GiB/s = N_workers * B / t / 2^30 per
 step, summed over GPUs.  ``roofline`` prices the dominant kernel at
 (N_workers + 1) * B algorithmic HBM bytes per launch against 8.0 TB/s;
-``cpu_baseline`` times the reference's own CpuReducer (oracle/_ref, the
-reference server round: zero-copy first arrival + (N-1) sums + copy to store)
-on a bounded sample on the host cores.
+``cpu_baseline`` times the clean-room CPU restatement of CpuReducer
+(oracle/bpsr_oracle.c, proven bit-identical to the reference by the golden
+vectors) running the reference server round on the headline 256 MiB bucket
+on the host cores.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import statistics
@@ -35,13 +49,20 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
+METRIC = "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs"
 # --dtype name -> (byteps DataType id, torch dtype name); ids: common.h:52-65 (+ bf16 = 11)
 DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
           "u8": (3, "uint8"), "i32": (4, "int32"), "i8": (5, "int8"), "i64": (6, "int64"),
           "bf16": (11, "bfloat16")}
+# Sources that define the headline kernel and its launch: a committed PMC
+# traffic record is quoted only while their hash matches (bench line
+# roofline.traffic_source).
+KERNEL_SOURCES = ("prophet_amd/csrc/bpsr_kernels_impl.h", "prophet_amd/csrc/bpsr_ops.h",
+                  "prophet_amd/csrc/bpsr_internal.h", "prophet_amd/csrc/bpsr_k_f32.hip",
+                  "prophet_amd/csrc/bpsr_api.cpp")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -55,59 +76,134 @@ def parse():
     p.add_argument("--layout", default="arena", choices=["arena", "separate"],
                    help="worker slots in one skewed HBM arena, or separate allocations")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-scaling", action="store_true",
+                   help="skip the config-4 (VGG-16 sharded) scaling object")
     p.add_argument("--no-scatter", action="store_true",
-                   help="N > 1: skip the config-4 RCCL scatter leg reported beside value")
-    p.add_argument("--cpu-sample-mib", type=float, default=64.0,
-                   help="bucket size of the CPU baseline sample")
-    return p.parse_args()
+                   help="N > 1: skip the RCCL scatter + all-gather leg of `scaling`")
+    p.add_argument("--scaling-elems", type=int, default=0,
+                   help="elements per worker of the config-4 set (0: VGG-16, 138,357,544)")
+    p.add_argument("--cpu-sample-mib", type=float, default=256.0,
+                   help="bucket size of the CPU baseline sample (headline: 256)")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: launcher/plumbing self-test over gloo with torch's CPU add "
+                        "(no HIP; the line is marked and is not a measurement)")
+    return p.parse_args(argv)
+
+
+# --------------------------------------------------------------------------
+# launcher: N rank processes, started before anything touches the GPU
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list[str], timeout_s: float = 1500.0) -> int:
+    """Start ``n`` copies of this script as ranks 0..n-1 (one per GPU) and wait.
+
+    The parent never initialises the GPU: it only spawns children (a child
+    process, never an exec) and relays their status.  Rank 0's stdout is the
+    parent's; the other ranks' stdout goes to stderr so exactly one JSON line
+    reaches stdout.  If a rank fails, the others are terminated (exact PIDs)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=None if r == 0 else sys.stderr.fileno()))
+    t_end = time.monotonic() + timeout_s
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad or time.monotonic() > t_end:
+            rc = bad[0] if bad else 124
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.1)
+    return rc
+
+
+# --------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1 only): the clean-room restatement
 
 
 def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | None:
-    """Reference CpuReducer (or the restatement) on host cores, server-round pattern."""
+    """CpuReducer server round on host cores: zero-copy first arrival, N-1
+    ``sum`` calls (server.cc:127-130 SUM_RECV) and the ``copy`` to the store
+    (server.cc:91 COPY_MERGED), timed with the clean-room restatement
+    (oracle/bpsr_oracle.c, OpenMP like cpu_reducer.cc:85-92; bit-identical to
+    the reference on every golden vector).  Also, as a secondary field only,
+    the reference's own CpuReducer when oracle/_ref was built."""
     import numpy as np
 
     from oracle.oracle import PortReducer, RefReducer
     from prophet_amd import synth
 
     es = {0: 4, 1: 8, 2: 2, 3: 1, 4: 4, 5: 1, 6: 8, 11: 2}[dtype_id]
-    if dtype_id == 11:           # reference has no bf16: time the restatement
-        kinds = [("port", PortReducer)]
-    else:
-        kinds = [("reference", RefReducer)] if RefReducer.available() else [("port", PortReducer)]
-    kind, cls = kinds[0]
     L = int(sample_mib * (1 << 20)) // es * es
     n = L // es
-    ins = [np.ascontiguousarray(synth.bucket(dtype_id, n, k, "normal")).view(np.uint8)
-           for k in range(n_workers)]
+    if dtype_id == 0:
+        # numpy's generator: 256 MiB x N in a second or two (synth's splitmix
+        # Box-Muller stream takes ~10x longer at this size); values N(0,1) alike
+        ins = [np.random.default_rng(1000 + k).standard_normal(n, dtype=np.float32).view(np.uint8)
+               for k in range(n_workers)]
+    else:
+        ins = [np.ascontiguousarray(synth.bucket(dtype_id, n, k, "normal")).view(np.uint8)
+               for k in range(n_workers)]
     store = np.empty(L, np.uint8)
     merged = np.empty(L, np.uint8)
-    out = {}
     ncpu = os.cpu_count() or 1
     try:
         ncpu = len(os.sched_getaffinity(0))
     except Exception:
         pass
-    for label, threads in (("default", 4), ("all", max(1, min(ncpu, 64)))):
-        red = cls(nthreads=threads)
 
+    def leg(red, threads, budget):
         def round_once():
             merged[:] = ins[0]           # stands in for the ps-lite receive buffer
             t0 = time.perf_counter()
-            for s in ins[1:]:            # server.cc:127-130 SUM_RECV jobs
-                red.sum(merged, s, L, dtype_id)
-            red.copy(store, merged, L)   # server.cc:91 COPY_MERGED
+            for s in ins[1:]:
+                assert red.sum(merged, s, L, dtype_id) == 0
+            red.copy(store, merged, L)
             return time.perf_counter() - t0
-
         for _ in range(2):
             round_once()
         ts = []
         t_begin = time.perf_counter()
-        budget = 10.0 if label == "default" else 4.0   # seconds of CPU work per leg
         while len(ts) < 10 or (time.perf_counter() - t_begin < budget and len(ts) < 2000):
             ts.append(round_once())
         med = statistics.median(ts)
-        out[label] = dict(threads=threads, gibps=n_workers * L / med / GIB,
-                          median_s=med, min_s=min(ts), reps=len(ts))
+        return dict(threads=threads, gibps=n_workers * L / med / GIB, median_s=med,
+                    min_s=min(ts), reps=len(ts))
+
+    default = leg(PortReducer(nthreads=4), 4, 10.0)
+    all_threads = max(1, min(ncpu, 64))
+    allc = leg(PortReducer(nthreads=all_threads), all_threads, 4.0)
+    ref = None
+    if dtype_id != 11 and RefReducer.available():
+        r = leg(RefReducer(nthreads=4), 4, 3.0)
+        ref = {"value": round(r["gibps"], 3), "cores": 4, "reps": r["reps"],
+               "what": "the reference's own cpu_reducer.cc built from /root/reference "
+                       "(oracle/_ref), secondary only"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -117,28 +213,185 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
                     break
     except OSError:
         pass
-    d = out["default"]
     return {
-        "value": round(d["gibps"], 3), "unit": "GiB/s", "cores": d["threads"], "kind": kind,
+        "value": round(default["gibps"], 3), "unit": "GiB/s", "cores": default["threads"],
+        "kind": "port",
         "sample": (f"{n_workers}-way server round (zero-copy first arrival, {n_workers - 1} "
-                   f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket, "
-                   f"median of {d['reps']} reps (~10 s of CPU work); "
-                   f"BYTEPS_OMP_THREAD_PER_GPU=4 (reference default)"),
-        "all_cores": {"value": round(out["all"]["gibps"], 3), "cores": out["all"]["threads"],
-                      "reps": out["all"]["reps"]},
+                   f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket (the "
+                   f"headline bucket), clean-room restatement oracle/bpsr_oracle.c, median of "
+                   f"{default['reps']} reps (~10 s of CPU work); 4 OpenMP threads = "
+                   f"BYTEPS_OMP_THREAD_PER_GPU default (cpu_reducer.cc:40-44)"),
+        "all_cores": {"value": round(allc["gibps"], 3), "cores": allc["threads"],
+                      "reps": allc["reps"]},
+        "reference_build": ref,
         "cpu_model": cpu_model, "host_cpus": ncpu,
     }
 
 
+# --------------------------------------------------------------------------
+# folds and timers for the two device kinds
+
+
+def _torch_fold(dst, srcs):
+    """--device cpu plumbing self-test only: torch's own CPU left fold."""
+    dst.copy_(srcs[0])
+    for s in srcs[1:]:
+        dst.add_(s)
+
+
+class _Clock:
+    """Average duration of a block of launches: HIP events on the launch
+    stream (cuda) or wall time (cpu self-test)."""
+
+    def __init__(self, dev):
+        self.cuda = dev.type == "cuda"
+        if self.cuda:
+            import torch
+            self.stream = torch.cuda.current_stream(dev)
+
+    def sync(self):
+        if self.cuda:
+            import torch
+            torch.cuda.synchronize()
+
+    def time(self, fn, reps: int) -> float:
+        """ms per call of fn(i) over reps calls (after the caller's warm-up)."""
+        if self.cuda:
+            import torch
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.stream)
+            for i in range(reps):
+                fn(i)
+            e1.record(self.stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps
+        t0 = time.perf_counter()
+        for i in range(reps):
+            fn(i)
+        return (time.perf_counter() - t0) * 1e3 / reps
+
+
+def _max_over_ranks(dist, dev, vals: list[float]) -> list[float]:
+    import torch
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t]
+
+
+def _all_true(dist, dev, flag: bool) -> bool:
+    import torch
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t[0]) == 1)
+
+
+def _left_fold_equal(out, srcs) -> bool:
+    """out (typed tensor) == torch's own left fold of srcs, bit for bit."""
+    import torch
+    ref = srcs[0].clone()
+    for s in srcs[1:]:
+        ref.add_(s)
+    return bool(torch.equal(ref.view(torch.int32), out.view(torch.int32)))
+
+
+# --------------------------------------------------------------------------
+# config 4: VGG-16 set sharded over the GPUs
+
+
+def scaling_leg(dev, world: int, rank: int, n_workers: int, fold, reps: int = 10,
+                n_elems: int | None = None, sets: int = 2) -> dict:
+    """BASELINE config 4, device-resident part: every worker's fp32 VGG-16
+    gradient vector is cut by the reference's reduce-scatter ownership
+    (``owner_ranges``, core_loops.cc:208-211) and each GPU folds its owned
+    slice of the N pushes (already on their owner, as ``reduce_from_host``
+    leaves them).  Strong scaling: total work fixed, so the per-GPU fold time
+    should fall as 1/G.  The G=1 time of the whole set is measured in the same
+    run on rank 0 (the other ranks wait at a barrier)."""
+    import torch
+    import torch.distributed as dist
+    from prophet_amd.arena import BucketArena
+    from prophet_amd.buckets import vgg16_param_sizes
+    from prophet_amd.shard import owner_ranges
+
+    E = n_elems or sum(vgg16_param_sizes())
+    ranges = owner_ranges(E, world)
+    clock = _Clock(dev)
+    multi = world > 1 and dist.is_initialized()
+    gen = torch.Generator(device=dev)
+
+    def make_sets(m):
+        out = []
+        for s in range(sets):
+            slots = [t.view(torch.float32) for t in BucketArena(n_workers + 1, 4 * m, dev).slots()]
+            for k in range(n_workers):
+                gen.manual_seed(7000 + 97 * rank + 13 * s + k)
+                slots[k].copy_(torch.randn(m, device=dev, generator=gen))
+            out.append((slots[n_workers], slots[:n_workers]))
+        return out
+
+    def time_folds(data) -> float:
+        def step(i):
+            dst, srcs = data[i % len(data)]
+            fold(dst, srcs)
+        for i in range(2):
+            step(i)
+        clock.sync()
+        return clock.time(step, reps)
+
+    res: dict = {}
+    # G = 1: the whole set on one GPU (rank 0), measured in this run
+    t1 = None
+    if rank == 0:
+        whole = make_sets(E)
+        t1 = time_folds(whole)
+        del whole
+    if multi:
+        dist.barrier()
+    lo, hi = ranges[rank]
+    m = hi - lo
+    data = make_sets(m) if m else []
+    if multi:
+        clock.sync()
+        dist.barrier()
+    t_g = time_folds(data) if m else 0.0
+    ok = _left_fold_equal(data[0][0], data[0][1]) if m else True
+    t_g, = _max_over_ranks(dist, dev, [t_g])
+    ok = _all_true(dist, dev, ok)
+    if world == 1:
+        t1 = t_g
+    t1s = _max_over_ranks(dist, dev, [t1 or 0.0])[0]
+    alg_per_gpu = (n_workers + 1) * 4 * max(hi_ - lo_ for lo_, hi_ in ranges)
+    res.update({
+        "workload": (f"config 4: {n_workers}-way fp32 VGG-16 set ({E * 4} B per worker) sharded "
+                     f"over {world} GPU(s) by reduce-scatter ownership (core_loops.cc:208-211); "
+                     f"owned slices device-resident; strong scaling"),
+        "shard_elems": [hi_ - lo_ for lo_, hi_ in ranges],
+        "g1_fold_ms": round(t1s, 4),
+        "per_gpu_fold_ms": round(t_g, 4),
+        "speedup_vs_g1": round(t1s / t_g, 3) if t_g else None,
+        "strong_efficiency": round(t1s / (world * t_g), 3) if t_g else None,
+        "node_GiBps": round(n_workers * E * 4 / (t_g * 1e-3) / GIB, 1) if t_g else None,
+        "per_gpu_frac_of_roofline": round(alg_per_gpu / (t_g * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        if t_g else None,
+        "exact_vs_torch_fold": ok,
+        "reps": reps,
+    })
+    return res
+
+
 def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
                 n_elems: int | None = None, fold=None) -> dict:
-    """BASELINE config 4 on the node the bench runs on (N > 1 only): N workers'
-    fp32 VGG-16 gradient vectors (553,430,176 B each) land on GPU 0; RCCL
-    grouped P2P over xGMI moves each owner its key-space slice
-    (ShardedReducer.scatter_reduce: the only data-path collective, SURVEY.md
-    §8e), the owner folds; then the all-gather return leg (core_loops.cc:
-    249-254).  Reported beside `value`, never as it.  Verified bit-exact on
-    GPU 0 against torch's own left fold of the whole vector."""
+    """BASELINE config 4's exchange (N > 1 only): N workers' fp32 VGG-16
+    gradient vectors (553,430,176 B each) land on GPU 0; RCCL grouped P2P over
+    xGMI moves each owner its key-space slice (ShardedReducer.scatter_reduce:
+    the only data-path collective), the owner folds; then the
+    all-gather return leg (core_loops.cc:249-254).  Verified bit-exact on GPU 0
+    against torch's own left fold of the whole vector."""
     import torch
     import torch.distributed as dist
     from prophet_amd.buckets import vgg16_param_sizes
@@ -176,10 +429,7 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
     t_gather = timed(lambda: sr.allgather(owned, full))
     ok = None
     if rank == root:
-        ref = pushes[0].clone()
-        for p in pushes[1:]:
-            ref.add_(p)
-        ok = bool(torch.equal(ref.view(torch.int32), full.view(torch.int32)))
+        ok = _left_fold_equal(full, pushes)
     lo, hi = sr.ranges[root]
     egress = n_workers * (E - (hi - lo)) * 4
     return {"workload": f"{n_workers} x VGG-16-sized fp32 ({E * 4} B) landed on GPU 0, "
@@ -191,39 +441,81 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
             "exact_vs_torch_fold": ok}
 
 
+# --------------------------------------------------------------------------
+# provenance of roofline.traffic
+
+
+def kernel_build_id(root: str = ROOT) -> str:
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(workload: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary (tools/pmc_traffic.py -> profiles/pmc_traffic.json), if it was
-    collected for this workload."""
+    PMC summary (tools/pmc_traffic.py -> profiles/pmc_traffic.json) — quoted
+    only when it was collected for this workload AND for the kernel sources
+    now in the tree.  Returns (bytes or None, source dict)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, {"status": "no committed PMC record"}
+    src = {"file": "profiles/pmc_traffic.json", "session": d.get("session"),
+           "kernel_build": d.get("kernel_build")}
+    if d.get("workload") != workload:
+        src["status"] = "recorded for another workload: not quoted"
+        return None, src
+    try:
+        now = kernel_build_id()
+    except OSError:
+        now = None
+    if d.get("kernel_build") != now:
+        src["status"] = f"kernel sources changed since the PMC pass (now {now}): not quoted"
+        return None, src
+    src["status"] = "same workload, same kernel sources"
+    return d.get("hbm_bytes_per_launch"), src
 
 
-def main():
-    args = parse()
+# --------------------------------------------------------------------------
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # Parent: start one process per GPU before anything touches the GPU.
+        sys.exit(launch_ranks(args.gpus, argv))
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # Bind this rank's GPU before the process group exists, so RCCL's
-    # communicator (barrier, the max-over-ranks all_reduce) uses it.
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    if world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE",
+              file=sys.stderr)
+    cuda = args.device == "cuda"
+    if cuda:
+        # Bind this rank's GPU before the process group exists, so RCCL's
+        # communicator (barrier, the max-over-ranks all_reduce) uses it.
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if cuda:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        world = dist.get_world_size()
 
     from prophet_amd.arena import BucketArena
     from prophet_amd.dtypes import DType
-    from prophet_amd.reducer import GpuReducer
 
     dtype_id = DType(DTYPES[args.dtype][0])
     tdt = getattr(torch, DTYPES[args.dtype][1])
@@ -232,7 +524,24 @@ def main():
     N = args.workers
     B = int(args.bucket_mib * (1 << 20)) // es * es
     n_elems = B // es
-    red = GpuReducer(device=local_rank)
+    if cuda:
+        from prophet_amd.reducer import GpuReducer
+        red = GpuReducer(device=local_rank)
+        stream = torch.cuda.current_stream(dev)
+
+        def fold_bytes(dst, srcs):
+            red.sum_n(dst, srcs, B, dtype_id, mode=mode, stream=stream)
+
+        def fold_f32(dst, srcs):
+            red.sum_n(dst, srcs, dst.numel() * 4, DType.FLOAT32, stream=stream)
+    else:
+        red = None
+        if mode:
+            raise SystemExit("--device cpu: reference mode only")
+
+        def fold_bytes(dst, srcs):
+            _torch_fold(dst.view(tdt), [s.view(tdt) for s in srcs])
+        fold_f32 = _torch_fold
 
     # Input sets: the server's per-worker receive slots for this GPU's bucket,
     # carved from one HBM arena (prophet_amd/arena.py: skewed slots avoid the
@@ -251,37 +560,28 @@ def main():
             else:
                 t.copy_(torch.randint(0, 256, (B,), dtype=torch.uint8, device=dev))
         sets.append((slots[N], slots[:N]))
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream(dev)
+    clock = _Clock(dev)
+    clock.sync()
 
     def step(i):
         dst, srcs = sets[i % len(sets)]
-        red.sum_n(dst, srcs, B, dtype_id, mode=mode, stream=stream)
+        fold_bytes(dst, srcs)
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    clock.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    clock.sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    kern_ms = clock.time(step, args.steps)   # avg duration per launch, launch stream
+    clock.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    clock.sync()
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps   # avg duration per launch, same stream
     t_step = wall / args.steps
-    if world > 1:
-        tt = torch.tensor([t_step, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step, kern_ms = float(tt[0]), float(tt[1])
+    t_step, kern_ms = _max_over_ranks(dist, dev, [t_step, kern_ms])
 
     # Correctness spot check of the last set against torch's own left fold.
     dst, srcs = sets[(args.steps + args.warmup - 1) % len(sets)]
@@ -289,15 +589,29 @@ def main():
     for s in srcs[1:]:
         chk.add_(s.view(tdt)[: 1 << 20])
     ok = bool(torch.equal(chk.view(torch.uint8), dst[: chk.numel() * es])) if mode == 0 else None
+    ok = _all_true(dist, dev, ok) if ok is not None else None
+    del sets
+
+    devices = [f"{local_rank}"]
+    if cuda:
+        devices = [f"{local_rank}:{torch.cuda.get_device_name(dev)}"]
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, devices[0])
+        devices = gathered
 
     alg_bytes = (N + 1) * B
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     workload = f"{N}-way {args.dtype} left-fold sum of one {B / (1 << 20):.0f} MiB bucket per GPU"
     if mode:
         workload += " (fp32-accumulate mode)"
-    tv, tnt, tgrid, tocc = red.get_tuning()
+    traffic, traffic_src = pmc_traffic(workload)
+    tuning = None
+    if red is not None:
+        tv, tnt, tgrid, tocc = red.get_tuning()
+        tuning = {"vpt": tv, "nt": tnt, "max_grid": tgrid, "wg_per_cu": tocc}
     line = {
-        "metric": "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": round(world * N * B / t_step / GIB, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -312,15 +626,33 @@ def main():
                 f"{args.sets} rotated input sets, layout={args.layout}",
         "config": {"workload": workload, "n_workers": N, "bucket_bytes": B,
                    "parallelism": f"key-space shard x{world}", "kernel": "byteps_reduce_sum_n",
-                   "tuning": {"vpt": tv, "nt": tnt, "max_grid": tgrid,
-                                                 "wg_per_cu": tocc}},
+                   "tuning": tuning, "devices": devices},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(workload),
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 5)},
         "check_vs_torch_fold": ok,
     }
+    if not cuda:
+        line["device"] = "cpu plumbing self-test (torch CPU add, gloo): NOT a measurement"
+
+    def extra_legs():
+        if not args.no_scaling:
+            try:
+                line["scaling_cfg4"] = scaling_leg(dev, world, rank, N, fold_f32,
+                                                   n_elems=args.scaling_elems or None)
+            except Exception as e:  # report, never hide
+                line["scaling_cfg4"] = {"error": repr(e)}
+            if world > 1 and not args.no_scatter:
+                try:
+                    line["scaling_cfg4"]["scatter"] = scatter_leg(
+                        dev, world, rank, N, n_elems=args.scaling_elems or None,
+                        fold=None if cuda else _torch_fold)
+                except Exception as e:  # report, never hide
+                    line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
+
     if world == 1:
+        extra_legs()
         if rank == 0 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)
@@ -328,9 +660,9 @@ def main():
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)
         return
-    # N > 1: the headline line is complete; the config-4 scatter leg runs after
-    # it under a watchdog, so a stuck or failing collective can cost only the
-    # extra field, never the line.
+    # N > 1: the headline line is complete; the config-4 legs run after it
+    # under a watchdog, so a stuck or failing collective can cost only those
+    # fields, never the line.
     import threading
     lock = threading.Lock()
     state = {"printed": False}
@@ -343,18 +675,15 @@ def main():
         if exit_now:
             os._exit(0)
 
-    watchdog = threading.Timer(180.0, lambda: (line.setdefault(
-        "scatter", {"error": "timed out after 180 s"}), emit_and_maybe_exit(True)))
+    watchdog = threading.Timer(240.0, lambda: (line.setdefault(
+        "scaling_cfg4", {}).setdefault("error", "timed out after 240 s"),
+        emit_and_maybe_exit(True)))
     watchdog.daemon = True
     watchdog.start()
-    if not args.no_scatter:
-        try:
-            line["scatter"] = scatter_leg(dev, world, rank, N)
-        except Exception as e:  # report, never hide
-            line["scatter"] = {"error": repr(e)}
+    extra_legs()
     emit_and_maybe_exit(False)
-    dist.destroy_process_group()
     watchdog.cancel()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -49,6 +49,11 @@ typedef struct byteps_server_config {
   int policy;          /* byteps_server_policy                               */
   int async_mode;      /* 1 = asynchronous training (sum into the store)     */
   int device;          /* HIP device ordinal                                 */
+  int enable_schedule; /* BYTEPS_SERVER_ENABLE_SCHEDULE (server.cc:335): each
+                          lane gets an engine thread that issues queued folds
+                          by (fewest counted pushes on the key, oldest) —
+                          queue.h:68-97 — one at a time; 0 = FIFO, issued at
+                          arrival (the reference default)                    */
 } byteps_server_config;
 
 typedef struct byteps_server byteps_server;
@@ -56,7 +61,8 @@ typedef struct byteps_server byteps_server;
 /* Defaults from the environment, as init_global_env (server.cc:310-337) reads
  * them: DMLC_NUM_WORKER, BYTEPS_SERVER_ENGINE_THREAD, BYTEPS_ENABLE_ASYNC
  * (here "1" means asynchronous; the reference reads the flag inverted,
- * server.cc:315), BPSR_SERVER_POLICY (fused|incremental), device 0. */
+ * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
+ * BYTEPS_SERVER_ENABLE_SCHEDULE, device 0. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
@@ -76,9 +82,12 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
  * behind the copies on the device), then acknowledges from the server's
  * responder thread with cb(ctx, key, worker, status) once the bytes are in HBM
  * and `data` may be reused — the point at which the reference answers a push
- * (server.cc:255 SendPushResponse).  Init pushes (round 0) do not wait for the
- * other workers' init pushes.  Like byteps_server_push, a worker's push for the
- * next round issued before the current round finished waits for it. */
+ * (server.cc:255 SendPushResponse).  Init pushes (round 0) are answered only
+ * once every worker's init push has arrived, all together, as the reference
+ * does (server.cc:184-198; workers use that answer as a barrier,
+ * operations.cc:301-302).  Like byteps_server_push, a worker's push issued
+ * while its previous push of the key (init push included) is not folded yet
+ * waits inside the call until it is. */
 typedef void (*byteps_server_push_cb)(void* ctx, uint64_t key, int worker, int status);
 int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
                              size_t len, int dtype, int location, byteps_server_push_cb cb,
@@ -102,8 +111,9 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
  * mirrored as soon as it finishes.  Two mirrors alternate by round, each at a
  * fixed address (register them with the NIC once).  Sync mode: the view stays
  * valid until this worker's next pull of the key returns.  Async mode: each
- * call copies the current store; the view is valid until the next call on the
- * key.  The caller must not write through the view. */
+ * call copies the current store into the next of num_workers + 1 mirrors (a
+ * ring), so a view stays intact for the next num_workers pulls of the key.
+ * The caller must not write through the view. */
 int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** data, size_t* len);
 
 /* Non-blocking pull for a transport's receive thread: the reference's default
@@ -113,9 +123,10 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
  * server-owned responder thread later calls
  *   cb(ctx, key, data, len, status)
  * with data/len = the zero-copy view byteps_server_pull_host_view would give
- * (same validity), status 0, and counts the pull toward the key's re-arm when
- * cb returns — so cb sends (or copies) the response before returning, as
- * SendPullResponse does.  Pulls still waiting at byteps_server_destroy get
+ * (same validity), status 0.  The pull is counted toward the key's re-arm just
+ * BEFORE cb runs (the reference counts it with SendPullResponse under one
+ * lock, server.cc:100-113, 293-298), so cb sends (or copies) the response
+ * before returning, as SendPullResponse does.  Pulls still waiting at byteps_server_destroy get
  * status BYTEPS_REDUCE_ECANCELED and data NULL.  cb must not call back into
  * the server for the same key. */
 typedef void (*byteps_server_pull_cb)(void* ctx, uint64_t key, const void* data, size_t len,
@@ -126,6 +137,13 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
  * rounds, engine lane, and the arrival order of the last completed round. */
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
                            int* last_order, int max_order);
+
+/* Debug/test hook for scheduling (enable_schedule only): pause > 0 holds the
+ * lane's engine queue (nothing is issued; pushes still queue), 0 releases it,
+ * < 0 leaves it; the keys of the jobs the lane issued so far, in issue order,
+ * go to log_keys (up to max_log) and their count to *n_log. */
+int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* log_keys,
+                             int max_log, int* n_log);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,12 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
   }
 }
 
-static Tuning& tuning() {
+// Process-wide tuning, read by every launch (engine lanes and caller threads)
+// and written by byteps_reduce_set_tuning: launches take a snapshot under the
+// lock, so a concurrent set_tuning never tears a launch's geometry.
+static std::mutex g_tuning_mu;
+
+static Tuning& tuning_storage() {
   static Tuning tu = [] {
     // tools/sweep.py, tools/occ_sweep.py, tools/cfg3_probe.py (profiles/)
     Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1, 4, 2};
@@ -106,6 +111,11 @@ static Tuning& tuning() {
     return t;
   }();
   return tu;
+}
+
+static Tuning tuning() {
+  std::lock_guard<std::mutex> g(g_tuning_mu);
+  return tuning_storage();
 }
 
 // Bytes in flight per CU = residency x 256 lanes x n sources x vpt x 16 B.
@@ -371,13 +381,13 @@ int byteps_reduce_dtype_size(int dtype) {
 const char* byteps_reduce_last_error(void) { return g_last_error.c_str(); }
 
 int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ) {
-  Tuning& t = tuning();
-  if (vpt > 0) {
-    if (vpt != 1 && vpt != 2 && vpt != 4)
-      return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2 or 4");
-    t.vpt = vpt;
-  }
+  // validate everything before changing anything
+  if (vpt > 0 && vpt != 1 && vpt != 2 && vpt != 4)
+    return fail(BYTEPS_REDUCE_EARGS, "vpt must be 1, 2 or 4");
   if (occ > 8) return fail(BYTEPS_REDUCE_EARGS, "occ must be 0..8");
+  std::lock_guard<std::mutex> g(g_tuning_mu);
+  Tuning& t = tuning_storage();
+  if (vpt > 0) t.vpt = vpt;
   if (nt >= 0) t.nt = nt ? 1 : 0;
   if (max_grid > 0) t.max_grid = max_grid;
   if (occ >= 0) t.occ = occ;
@@ -385,7 +395,7 @@ int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ) {
 }
 
 int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid, int* occ) {
-  const Tuning& t = tuning();
+  const Tuning t = tuning();
   if (vpt) *vpt = t.vpt;
   if (nt) *nt = t.nt;
   if (max_grid) *max_grid = t.max_grid;

@@ -2,6 +2,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -137,8 +139,14 @@ inline int launch_occ(const Tuning& tu, uint64_t tiles, bool batched) {
   if (tiles >= (batched ? tu.occ_min_tiles_batch : tu.occ_min_tiles)) return 1;
   return batched ? tu.small_occ_batch : tu.small_occ;
 }
-// Allow `kernel` to request up to 160 KiB of dynamic LDS (once per kernel).
-hipError_t allow_full_lds(const void* kernel);
+// Allow `kernel` to request up to `bytes` of dynamic LDS.  hipFuncSetAttribute
+// acts on the calling thread's current device, so it is applied once PER
+// DEVICE: bit d of `done` records device d (a process may drive several GPUs,
+// e.g. one server or shard thread per device).
+struct KernelAttr {
+  std::atomic<uint64_t> done{0};
+};
+hipError_t allow_lds(KernelAttr& once, const void* kernel, int bytes = (int)kLdsPerCU);
 
 int elem_size(int dtype);  // 0 if unsupported
 

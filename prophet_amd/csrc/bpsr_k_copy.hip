@@ -18,8 +18,9 @@ namespace bpsr {
 // torch's (profiles/r01_copy_sweep.jsonl; Tuning::copy_occ / copy_vpt).
 template <int VPT>
 static hipError_t launch_copy_vpt(const FoldArgs& a0, const Tuning& tu, hipStream_t s) {
-  static const hipError_t lds_ok =
-      allow_full_lds(reinterpret_cast<const void*>(&fold_kernel<OpI8, VPT, true, 1>));
+  static KernelAttr attr;
+  const hipError_t lds_ok =
+      allow_lds(attr, reinterpret_cast<const void*>(&fold_kernel<OpI8, VPT, true, 1>));
   if (lds_ok != hipSuccess) return lds_ok;
   FoldArgs a = a0;
   a.grid = (uint32_t)fold_grid(a.g, tu, VPT);
@@ -29,9 +30,15 @@ static hipError_t launch_copy_vpt(const FoldArgs& a0, const Tuning& tu, hipStrea
   return hipGetLastError();
 }
 
-hipError_t allow_full_lds(const void* kernel) {
-  return hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)kLdsPerCU);
+hipError_t allow_lds(KernelAttr& once, const void* kernel, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? (uint64_t{1} << dev) : 0;
+  if (bit && (once.done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+  e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess && bit) once.done.fetch_or(bit, std::memory_order_release);
+  return e;
 }
 
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,

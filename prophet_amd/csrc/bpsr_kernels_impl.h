@@ -567,8 +567,9 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
 
 template <class Op, int VPT, bool NT, int NS>
 static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
-  static const hipError_t lds_ok =
-      allow_full_lds(reinterpret_cast<const void*>(&fold_kernel<Op, VPT, NT, NS>));
+  static KernelAttr attr;
+  const hipError_t lds_ok =
+      allow_lds(attr, reinterpret_cast<const void*>(&fold_kernel<Op, VPT, NT, NS>));
   if (lds_ok != hipSuccess) return lds_ok;
   FoldArgs b = a;
   b.grid = (uint32_t)fold_grid(a.g, tu, VPT);   // the kernel strides by its own grid
@@ -606,10 +607,11 @@ static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_
 
 template <class Op, int VPT>
 static hipError_t launch_batched_vpt(const BatchLaunch& L, const Tuning& tu, hipStream_t s) {
-  static const hipError_t ok_nt =
-      allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, true>));
-  static const hipError_t ok_t =
-      allow_full_lds(reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
+  static KernelAttr attr_nt, attr_t;
+  const hipError_t ok_nt =
+      allow_lds(attr_nt, reinterpret_cast<const void*>(&batched_kernel<Op, VPT, true>));
+  const hipError_t ok_t =
+      allow_lds(attr_t, reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
   if (ok_nt != hipSuccess) return ok_nt;
   if (ok_t != hipSuccess) return ok_t;
   if (L.tiles == 0) return hipSuccess;
@@ -634,17 +636,18 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
 template <class Op, int VPT, bool NT>
 static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated, hipStream_t s) {
   if (gated) {
-    static const hipError_t okg =
-        allow_full_lds(reinterpret_cast<const void*>(&blockq_gate_kernel<Op, VPT, NT>));
+    static KernelAttr attr_g;
+    const hipError_t okg =
+        allow_lds(attr_g, reinterpret_cast<const void*>(&blockq_gate_kernel<Op, VPT, NT>));
     if (okg != hipSuccess) return okg;
     hipLaunchKernelGGL((blockq_gate_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
     return hipGetLastError();
   }
   // the kernel's own static LDS (the record staging words) comes on top of the
   // dynamic residency request, so allow 256 B less than the CU's 160 KiB
-  static const hipError_t ok =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&blockq_kernel<Op, VPT, NT>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCU - 256);
+  static KernelAttr attr_p;
+  const hipError_t ok = allow_lds(attr_p, reinterpret_cast<const void*>(&blockq_kernel<Op, VPT, NT>),
+                                  (int)kLdsPerCU - 256);
   if (ok != hipSuccess) return ok;
   hipLaunchKernelGGL((blockq_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
   return hipGetLastError();

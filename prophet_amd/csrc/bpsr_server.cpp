@@ -8,9 +8,9 @@
 
 #include <algorithm>
 #include <condition_variable>
-#include <deque>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <memory>
 #include <mutex>
@@ -19,6 +19,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "bpsr_engine_queue.h"
 #include "bpsr_internal.h"
 
 namespace bpsr {
@@ -26,11 +27,44 @@ namespace {
 
 constexpr size_t kSlotAlign = 4096;
 constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots
+constexpr int kMaxDebugLog = 4096;
+
+struct KeyState;
+
+// One engine message (server.h:65-75 BytePSEngineMessage): the fold work of
+// one arrival (SUM_RECV), of a finished round (COPY_MERGED, or the fused
+// left fold) or of an async push.
+enum JobKind { kSumRecv = 0, kAsyncSum = 1, kFinishIncremental = 2, kFinishFused = 3 };
+struct FoldJob {
+  KeyState* ks = nullptr;
+  int kind = kSumRecv;
+  int w = -1;              // the arriving worker's slot
+  int acc = -1;            // the accumulator slot (first arrival), incremental policy
+  std::vector<int> order;  // arrival order of the finished round
+};
 
 struct Lane {
   hipStream_t fold = nullptr;  // folds, in round order per key
-  hipStream_t copy = nullptr;  // push/pull copies
-  hipStream_t d2h = nullptr;   // per-round store -> host mirror copies
+  hipStream_t copy = nullptr;  // push copies
+  hipStream_t d2h = nullptr;   // store -> host mirror copies
+  // BYTEPS_SERVER_ENABLE_SCHEDULE: pending jobs and the thread that issues them
+  std::unique_ptr<EngineQueue<FoldJob>> q;
+  std::thread dispatcher;
+  hipEvent_t job_done = nullptr;
+  std::mutex dbg_mu;
+  std::vector<uint64_t> log;  // keys of dispatched jobs, in dispatch order
+};
+
+// A pull ready to be answered, or a push to acknowledge, by the responder.
+struct Response {
+  uint64_t key = 0;
+  KeyState* ks = nullptr;
+  byteps_server_pull_cb cb = nullptr;
+  void* ctx = nullptr;
+  const char* view = nullptr;  // mirror holding the answered round
+  int status = 0;
+  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
+  int worker = -1;
 };
 
 struct KeyState {
@@ -47,23 +81,29 @@ struct KeyState {
   std::vector<char*> slot;
   char* store = nullptr;
   // current round
-  std::vector<char> got;      // worker pushed this round
+  std::vector<char> got;      // worker pushed this round (cleared when the round's fold is issued)
   std::vector<int> order;     // arrival order this round
   int arrived = 0;
   int init_count = 0;
+  std::vector<Response> init_acks;  // non-blocking init pushes, answered together (server.cc:184-198)
+  int pending = 0;            // jobs queued on the lane, not yet issued (scheduling only)
+  int error = 0;              // sticky failure of an issued fold: every later call returns it
+  std::string error_msg;
   // completion / pull gating (server.cc:100-114, 280-306)
   uint64_t rounds = 0;
   bool push_finished = false;
   int pull_cnt = 0;
   std::vector<int> last_order;
-  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the round
+  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the last issued fold
   hipEvent_t copied = nullptr;
   bool has_done = false;
-  // pinned host mirror of the store for zero-copy pull responses
-  // (byteps_server_pull_host_view; server.cc:42-70 responds from the store
-  // itself).  Two buffers by round parity, filled by ONE D2H per round.
-  char* mirror[2] = {nullptr, nullptr};
-  void* mirror_dev[2] = {nullptr, nullptr};  // the same pages as the device sees them
+  // pinned host mirrors of the store for zero-copy pull responses
+  // (server.cc:42-70 responds from the store itself).  Sync mode: two, by
+  // round parity, filled by ONE D2H per round.  Async mode: a ring of
+  // num_workers + 1, one D2H per pull.
+  std::vector<char*> mirror;
+  std::vector<void*> mirror_dev;  // the same pages as the device sees them
+  uint64_t mirror_next = 0;       // async ring position
   hipEvent_t mirrored = nullptr;  // recorded on the lane's d2h stream
   // byteps_server_pull_async requests waiting for this round to finish
   // (the reference's q_pull_reqmeta_, server.cc:304)
@@ -74,29 +114,18 @@ struct KeyState {
   std::vector<Waiting> waiting;
 };
 
-// A pull ready to be answered by the responder thread.
-struct Response {
-  uint64_t key;
-  KeyState* ks;
-  byteps_server_pull_cb cb;
-  void* ctx;
-  const char* view;  // mirror holding the answered round
-  int status;
-  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
-  int worker = -1;
-};
-
 }  // namespace
 }  // namespace bpsr
 
 struct byteps_server {
   byteps_server_config cfg;
-  std::vector<bpsr::Lane> lanes;
+  bool schedule = false;
+  std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
   std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
-  // responder thread for byteps_server_pull_async (the engine threads'
-  // SendPullResponse of queued pulls, server.cc:100-114)
+  // responder thread: SendPullResponse of queued pulls (server.cc:100-114)
+  // and SendPushResponse of non-blocking pushes (server.cc:255)
   std::mutex rq_mu;
   std::condition_variable rq_cv;
   std::deque<bpsr::Response> rq;
@@ -138,6 +167,11 @@ KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
   return p;
 }
 
+int key_error(const KeyState* ks) {
+  return fail(ks->error, "key %llu: an earlier fold failed: %s", (unsigned long long)ks->key,
+              ks->error_msg.c_str());
+}
+
 // Allocate slots + store for a key (caller holds ks->mu).
 int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   if (ks->allocated) {
@@ -173,11 +207,20 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   return 0;
 }
 
+// May worker w's push land in its slot now?  Not while its push of the
+// current round (or its init push) is still unfolded; in async mode with
+// scheduling, not while an earlier async sum of the key is still queued.
+bool can_push(const byteps_server* s, const KeyState* ks, int w) {
+  if (ks->error) return true;  // the caller reports it
+  if (ks->got[w]) return false;
+  return !(s->cfg.async_mode && ks->inited && ks->pending > 0);
+}
+
 // Bring `len` bytes into worker `w`'s slot on the lane's copy stream, after
-// the previous round's fold has consumed the slot; wait for the copy.
+// the last issued fold of the key has consumed the slot.
 int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc,
             bool wait = true) {
-  Lane& L = s->lanes[ks->lane];
+  Lane& L = *s->lanes[ks->lane];
   hipError_t e = hipSuccess;
   if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->done, 0);
   if (e == hipSuccess)
@@ -189,51 +232,69 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
   return e == hipSuccess ? 0 : hip_fail(e, "push copy");
 }
 
-// Queue the D2H of the store into mirror[round & 1] on the lane's d2h stream,
-// behind the round's fold (caller holds ks->mu).  Its own stream, so the copy
-// overlaps the H2D pushes of the lane's other keys (PCIe is full duplex).
-int queue_mirror(byteps_server* s, KeyState* ks, uint64_t round) {
-  Lane& L = s->lanes[ks->lane];
+// Queue the D2H of the store into mirror[idx] on the lane's d2h stream,
+// behind the key's last issued fold (caller holds ks->mu).  Its own stream, so
+// the copy overlaps the H2D pushes of the lane's other keys (PCIe is full duplex).
+int queue_mirror(byteps_server* s, KeyState* ks, size_t idx) {
+  Lane& L = *s->lanes[ks->lane];
   hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
   if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
   // The copy kernel writes the pinned mirror straight over PCIe.  A
   // hipMemcpyAsync D2H queued behind a pending event wait was handed to an SDMA
   // engine that ran at ~13 GB/s beside the H2D pushes (rocprofv3 memory-copy
   // trace); the kernel path runs at the link's rate.
-  int rc = byteps_reduce_copy(ks->mirror_dev[round & 1], ks->store, ks->len,
+  int rc = byteps_reduce_copy(ks->mirror_dev[idx], ks->store, ks->len,
                               reinterpret_cast<void*>(L.d2h));
   if (rc) return rc;
   e = hipEventRecord(ks->mirrored, L.d2h);
   return e == hipSuccess ? 0 : hip_fail(e, "store mirror copy");
 }
 
-// Pin the key's two store mirrors on first use (fixed addresses from then on,
-// as server.cc:60-69 reuses its response buffer to avoid re-registering
-// memory); with queue_now, also mirror the finished current round.  Caller
-// holds ks->mu.
+// Next mirror of an async-mode pull: a ring, so a view stays intact for the
+// next num_workers pulls of the key.
+size_t next_async_mirror(KeyState* ks) { return (size_t)(ks->mirror_next++ % ks->mirror.size()); }
+
+// Pin the key's store mirrors on first use (fixed addresses from then on, as
+// server.cc:60-69 reuses its response buffer to avoid re-registering memory);
+// with queue_now, also mirror the finished current round.  Caller holds ks->mu.
 int ensure_mirror(byteps_server* s, KeyState* ks, bool queue_now) {
-  if (ks->mirror[0]) return 0;
+  if (!ks->mirror.empty()) return 0;
+  const int nm = s->cfg.async_mode ? s->cfg.num_workers + 1 : 2;
   hipError_t e;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < nm; ++i) {
     void* p = nullptr;
     if ((e = hipHostMalloc(&p, ks->len, hipHostMallocDefault)) != hipSuccess)
       return hip_fail(e, "hipHostMalloc(store mirror)");
-    ks->mirror[i] = static_cast<char*>(p);
-    if ((e = hipHostGetDevicePointer(&ks->mirror_dev[i], p, 0)) != hipSuccess)
+    void* d = nullptr;
+    if ((e = hipHostGetDevicePointer(&d, p, 0)) != hipSuccess) {
+      (void)hipHostFree(p);
       return hip_fail(e, "hipHostGetDevicePointer(store mirror)");
+    }
+    ks->mirror.push_back(static_cast<char*>(p));
+    ks->mirror_dev.push_back(d);
   }
   if ((e = hipEventCreateWithFlags(&ks->mirrored, hipEventDisableTiming)) != hipSuccess)
     return hip_fail(e, "hipEventCreate");
-  return queue_now ? queue_mirror(s, ks, ks->rounds) : 0;
+  return queue_now ? queue_mirror(s, ks, ks->rounds & 1) : 0;
 }
 
-// Hand a ready pull of the current round to the responder (caller holds ks->mu).
-void respond_later(byteps_server* s, uint64_t key, KeyState* ks, byteps_server_pull_cb cb,
-                   void* ctx, int status) {
-  Response r{key, ks, cb, ctx, ks->mirror[ks->rounds & 1], status};
+void enqueue_response(byteps_server* s, const Response& r) {
   std::lock_guard<std::mutex> g(s->rq_mu);
   s->rq.push_back(r);
   s->rq_cv.notify_one();
+}
+
+// Hand a pull to the responder (caller holds ks->mu).
+void respond_later(byteps_server* s, KeyState* ks, byteps_server_pull_cb cb, void* ctx,
+                   const char* view, int status) {
+  Response r;
+  r.key = ks->key;
+  r.ks = ks;
+  r.cb = cb;
+  r.ctx = ctx;
+  r.view = view;
+  r.status = status;
+  enqueue_response(s, r);
 }
 
 // Count one answered pull; after NumWorkers the key re-arms (server.cc:105-113).
@@ -244,6 +305,23 @@ void count_pull(byteps_server* s, KeyState* ks) {
     ks->push_finished = false;
     ks->pull_cnt = 0;
   }
+  ks->cv.notify_all();
+}
+
+// A fold of the key failed after its push calls returned: remember it, fail
+// the pulls waiting for the round, wake every waiter.  Caller holds ks->mu.
+void fail_key(byteps_server* s, KeyState* ks, int rc) {
+  if (!ks->error) {
+    ks->error = rc;
+    ks->error_msg = byteps_reduce_last_error();
+  }
+  for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, nullptr, rc);
+  ks->waiting.clear();
+  for (auto& a : ks->init_acks) {
+    a.status = rc;
+    enqueue_response(s, a);
+  }
+  ks->init_acks.clear();
   ks->cv.notify_all();
 }
 
@@ -259,100 +337,198 @@ void responder_main(byteps_server* s) {
       s->rq.pop_front();
     }
     if (r.push_cb) {  // the push's bytes are in HBM: the sender's buffer is free
-      hipError_t e = hipEventSynchronize(r.ks->copied);
-      r.push_cb(r.ctx, r.key, r.worker, e == hipSuccess ? 0 : hip_fail(e, "push copy sync"));
+      int status = r.status;
+      if (status == 0) {
+        hipError_t e = hipEventSynchronize(r.ks->copied);
+        if (e != hipSuccess) status = hip_fail(e, "push copy sync");
+      }
+      r.push_cb(r.ctx, r.key, r.worker, status);
       continue;
     }
     int status = r.status;
     if (status == 0) {
-      // The event still names this round's copy: the next round cannot finish
-      // before this pull is counted below.
+      // The event still names the answered round's copy: the next round
+      // cannot finish before this pull is counted (it needs this worker's
+      // next push, which follows the answer).
       hipError_t e = hipEventSynchronize(r.ks->mirrored);
       if (e != hipSuccess) status = hip_fail(e, "store mirror sync");
     }
-    r.cb(r.ctx, r.key, status == 0 ? r.view : nullptr, status == 0 ? r.ks->len : 0, status);
     if (r.status == 0) {
+      // Count BEFORE answering, under the key lock, as the reference counts
+      // under flag_mu_ in the same step as SendPullResponse
+      // (server.cc:100-113, 293-298): once the worker has its answer it may
+      // push and finish the next round, and a late count would land there.
       std::lock_guard<std::mutex> g(r.ks->mu);
       count_pull(s, r.ks);
     }
+    r.cb(r.ctx, r.key, status == 0 ? r.view : nullptr, status == 0 ? r.ks->len : 0, status);
+  }
+}
+
+// A round's fold is issued: publish it (caller holds ks->mu).
+int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order) {
+  Lane& L = *s->lanes[ks->lane];
+  hipError_t e = hipEventRecord(ks->done, L.fold);
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  ks->has_done = true;
+  int rc = 0;
+  if (!ks->mirror.empty() && (rc = queue_mirror(s, ks, (ks->rounds + 1) & 1))) return rc;
+  ks->last_order = order;
+  std::fill(ks->got.begin(), ks->got.end(), 0);
+  ks->rounds++;
+  ks->push_finished = true;
+  ks->pull_cnt = 0;
+  const char* view = ks->mirror.empty() ? nullptr : ks->mirror[ks->rounds & 1];
+  for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, view, 0);
+  ks->waiting.clear();
+  ks->cv.notify_all();
+  return 0;
+}
+
+// Issue a job's kernels on the lane's fold stream and apply its state
+// changes — the body of the engine thread (server.cc:70-145).  Caller holds
+// ks->mu.
+int execute(byteps_server* s, const FoldJob& j) {
+  KeyState* ks = j.ks;
+  Lane& L = *s->lanes[ks->lane];
+  void* fs = reinterpret_cast<void*>(L.fold);
+  // Folds run behind the slots' H2D copies (byteps_server_push_async returns
+  // before they finish; the copy stream is in order, so the last recorded copy
+  // covers every earlier one) and behind the last mirror D2H of the store.
+  hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
+  if (we == hipSuccess && ks->mirrored) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
+  if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+  int rc = 0;
+  switch (j.kind) {
+    case kSumRecv:  // SUM_RECV (server.cc:117-139): merged (= first arrival's slot) += push
+      return byteps_reduce_sum(ks->slot[j.acc], ks->slot[j.w], ks->len, ks->dtype, fs);
+    case kAsyncSum: {  // server.cc:220-230: every push is summed straight into the store
+      rc = byteps_reduce_sum(ks->store, ks->slot[j.w], ks->len, ks->dtype, fs);
+      if (rc) return rc;
+      hipError_t e = hipEventRecord(ks->done, L.fold);
+      if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+      ks->has_done = true;
+      ks->rounds++;
+      ks->cv.notify_all();
+      return 0;
+    }
+    case kFinishIncremental:  // COPY_MERGED (server.cc:82-115)
+      rc = byteps_reduce_copy(ks->store, ks->slot[j.acc], ks->len, fs);
+      break;
+    default: {  // one fused left fold in arrival order straight into the store
+      const int N = (int)j.order.size();
+      std::vector<const void*> srcs(N);
+      for (int k = 0; k < N; ++k) srcs[k] = ks->slot[j.order[k]];
+      rc = byteps_reduce_sum_n(ks->store, srcs.data(), N, ks->len, ks->dtype,
+                               BYTEPS_REDUCE_MODE_REFERENCE, fs);
+    }
+  }
+  if (rc) return rc;
+  return finish_round(s, ks, j.order);
+}
+
+// Run a job now (reference default: the engine takes messages FIFO and this
+// build issues them to the lane's stream in arrival order), or queue it for
+// the lane's dispatcher (scheduling on).  Caller holds ks->mu.
+int submit(byteps_server* s, KeyState* ks, FoldJob&& j) {
+  if (!s->schedule) return execute(s, j);
+  ks->pending++;
+  s->lanes[ks->lane]->q->push(ks->key, std::move(j));
+  return 0;
+}
+
+// BYTEPS_SERVER_ENABLE_SCHEDULE: the lane's engine thread.  Pops by
+// (fewest counted pushes, oldest) and, like the reference engine thread that
+// runs each message to completion before the next pop (server.cc:70-145),
+// waits for each job's kernels before popping again — which is what lets
+// later arrivals overtake queued ones.
+void dispatcher_main(byteps_server* s, int lane) {
+  (void)hipSetDevice(s->cfg.device);
+  Lane& L = *s->lanes[lane];
+  FoldJob j;
+  uint64_t key = 0;
+  while (L.q->wait_pop(&j, &key)) {
+    {
+      std::lock_guard<std::mutex> dl(L.dbg_mu);
+      if (L.log.size() < (size_t)kMaxDebugLog) L.log.push_back(key);
+    }
+    KeyState* ks = j.ks;
+    {
+      std::lock_guard<std::mutex> g(ks->mu);
+      ks->pending--;
+      if (!ks->error) {
+        const int rc = execute(s, j);
+        if (rc) fail_key(s, ks, rc);
+      }
+      if (hipEventRecord(L.job_done, L.fold) != hipSuccess) fail_key(s, ks, BYTEPS_REDUCE_EHIP);
+      ks->cv.notify_all();
+    }
+    (void)hipEventSynchronize(L.job_done);
   }
 }
 
 // A push's bytes are in slot w: advance the state machine (caller holds ks->mu).
 int arrive(byteps_server* s, KeyState* ks, int w) {
+  if (ks->error) return key_error(ks);
   const int N = s->cfg.num_workers;
-  Lane& L = s->lanes[ks->lane];
-  void* fold_stream = reinterpret_cast<void*>(L.fold);
-  int rc = 0;
-  // Folds run behind the slots' H2D copies (byteps_server_push_async returns
-  // before they finish; the copy stream is in order, so the last recorded copy
-  // covers every earlier one) and behind the last mirror D2H of the store.
-  hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
-  if (we == hipSuccess && ks->mirror[0]) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
-  if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+  Lane& L = *s->lanes[ks->lane];
   if (!ks->inited) {
     // Round 0: server.cc:175-199 — after all NumWorkers init pushes the store
-    // is initialised by copying the LAST arrived push.
+    // is initialised by copying the LAST arrived push, in the handler itself.
     if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d sent two init pushes", w);
     ks->got[w] = 1;
     if (++ks->init_count < N) return 0;
-    rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, fold_stream);
+    hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
+    if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+    int rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, reinterpret_cast<void*>(L.fold));
     if (rc) return rc;
     hipError_t e = hipEventRecord(ks->done, L.fold);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
     ks->has_done = true;
     ks->inited = true;
     std::fill(ks->got.begin(), ks->got.end(), 0);
+    // server.cc:196-198: every held init push is answered now
+    for (auto& a : ks->init_acks) enqueue_response(s, a);
+    ks->init_acks.clear();
     ks->cv.notify_all();
     return 0;
   }
+  EngineQueue<FoldJob>* q = s->schedule ? L.q.get() : nullptr;
   if (s->cfg.async_mode) {
-    // server.cc:220-230: every push is summed straight into the store.
-    rc = byteps_reduce_sum(ks->store, ks->slot[w], ks->len, ks->dtype, fold_stream);
-    if (rc) return rc;
-    hipError_t e = hipEventRecord(ks->done, L.fold);
-    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-    ks->has_done = true;
-    ks->rounds++;
-    ks->cv.notify_all();
-    return 0;
+    FoldJob j;
+    j.ks = ks;
+    j.kind = kAsyncSum;
+    j.w = w;
+    const int rc = submit(s, ks, std::move(j));
+    if (q) q->clear_counter(ks->key);  // server.cc:277
+    return rc;
   }
   if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d pushed twice in one round", w);
   ks->got[w] = 1;
   ks->order.push_back(w);
   ks->arrived++;
-  if (s->cfg.policy == BYTEPS_SERVER_INCREMENTAL && ks->arrived > 1) {
-    // SUM_RECV (server.cc:117-139): merged (= first arrival's slot) += this push
-    rc = byteps_reduce_sum(ks->slot[ks->order[0]], ks->slot[w], ks->len, ks->dtype, fold_stream);
+  if (ks->arrived > 1 && s->cfg.policy == BYTEPS_SERVER_INCREMENTAL) {
+    FoldJob j;  // SUM_RECV (server.cc:245-251)
+    j.ks = ks;
+    j.kind = kSumRecv;
+    j.w = w;
+    j.acc = ks->order[0];
+    const int rc = submit(s, ks, std::move(j));
     if (rc) return rc;
+  } else if (ks->arrived > 1 && ks->arrived < N && q) {
+    q->count(ks->key);  // the SUM_RECV the reference would have queued
   }
   if (ks->arrived < N) return 0;
-  if (s->cfg.policy == BYTEPS_SERVER_INCREMENTAL) {
-    // COPY_MERGED (server.cc:82-115)
-    rc = byteps_reduce_copy(ks->store, ks->slot[ks->order[0]], ks->len, fold_stream);
-  } else {
-    // one fused left fold in arrival order straight into the store
-    std::vector<const void*> srcs(N);
-    for (int k = 0; k < N; ++k) srcs[k] = ks->slot[ks->order[k]];
-    rc = byteps_reduce_sum_n(ks->store, srcs.data(), N, ks->len, ks->dtype,
-                             BYTEPS_REDUCE_MODE_REFERENCE, fold_stream);
-  }
-  if (rc) return rc;
-  hipError_t e = hipEventRecord(ks->done, L.fold);
-  if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
-  ks->has_done = true;
-  if (ks->mirror[0] && (rc = queue_mirror(s, ks, ks->rounds + 1))) return rc;
-  ks->last_order = ks->order;
+  FoldJob j;
+  j.ks = ks;
+  j.kind = s->cfg.policy == BYTEPS_SERVER_INCREMENTAL ? kFinishIncremental : kFinishFused;
+  j.acc = ks->order[0];
+  j.order = ks->order;
   ks->order.clear();
   ks->arrived = 0;
-  std::fill(ks->got.begin(), ks->got.end(), 0);
-  ks->rounds++;
-  ks->push_finished = true;
-  ks->pull_cnt = 0;
-  for (auto& wp : ks->waiting) respond_later(s, ks->key, ks, wp.cb, wp.ctx, 0);
-  ks->waiting.clear();
-  ks->cv.notify_all();
-  return 0;
+  const int rc = submit(s, ks, std::move(j));
+  if (q) q->clear_counter(ks->key);  // server.cc:269-271
+  return rc;
 }
 
 // Init pushes block until every worker's init push has arrived and the store
@@ -361,20 +537,43 @@ int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock
   const bool init_round = !ks->inited;
   int rc = arrive(s, ks, w);
   if (rc || !init_round) return rc;
-  ks->cv.wait(lk, [&] { return ks->inited; });
-  return 0;
+  ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
+  return ks->error ? key_error(ks) : 0;
 }
 
-// Per-thread stream for pull copies (a pull blocks only on its own copy).
-hipStream_t pull_stream(int device) {
-  thread_local hipStream_t st = nullptr;
-  thread_local int dev = -1;
-  if (st && dev == device) return st;
-  if (st) (void)hipStreamDestroy(st);
-  st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) st = nullptr;
-  dev = device;
-  return st;
+// Per-thread stream and event for pull copies (a pull blocks only on its own copy).
+struct PullCtx {
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;
+  int dev = -1;
+};
+PullCtx* pull_ctx(int device) {
+  thread_local PullCtx c;
+  if (c.st && c.dev == device) return &c;
+  if (c.st) (void)hipStreamDestroy(c.st);
+  if (c.ev) (void)hipEventDestroy(c.ev);
+  c.st = nullptr;
+  c.ev = nullptr;
+  c.dev = device;
+  if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c.ev, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  return &c;
+}
+
+KeyState* key_for_pull(byteps_server* s, uint64_t key) {
+  KeyState* ks = get_key(s, key, false);
+  if (!ks || !ks->allocated)  // server.cc:282-283
+    fail(BYTEPS_REDUCE_EARGS, "Processing pull request when the key %llu has not been inited yet",
+         (unsigned long long)key);
+  return ks && ks->allocated ? ks : nullptr;
+}
+
+void destroy_lanes(byteps_server* s) {
+  for (auto& Lp : s->lanes)
+    if (Lp && Lp->q) Lp->q->stop();
+  for (auto& Lp : s->lanes)
+    if (Lp && Lp->dispatcher.joinable()) Lp->dispatcher.join();
 }
 
 }  // namespace
@@ -395,6 +594,8 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   cfg->policy = (p && std::string(p) == "incremental") ? BYTEPS_SERVER_INCREMENTAL
                                                        : BYTEPS_SERVER_FUSED;
   cfg->device = 0;
+  const char* sc = getenv("BYTEPS_SERVER_ENABLE_SCHEDULE");  // server.cc:335
+  cfg->enable_schedule = (sc && atoi(sc) != 0) ? 1 : 0;
   return BYTEPS_REDUCE_OK;
 }
 
@@ -408,24 +609,32 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
     return fail(BYTEPS_REDUCE_EARGS, "unknown policy %d", cfg->policy);
   auto s = std::make_unique<byteps_server>();
   s->cfg = *cfg;
+  s->schedule = cfg->enable_schedule != 0;
   int rc = set_device(s.get());
   if (rc) return rc;
-  s->lanes.resize(cfg->engine_lanes);
   s->acc_load.assign(cfg->engine_lanes, 0);
-  for (auto& L : s->lanes) {
+  for (int i = 0; i < cfg->engine_lanes; ++i) {
+    s->lanes.push_back(std::make_unique<Lane>());
+    Lane& L = *s->lanes.back();
     hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
+    if (e == hipSuccess && s->schedule)
+      e = hipEventCreateWithFlags(&L.job_done, hipEventDisableTiming);
     if (e != hipSuccess) {
       byteps_server_destroy(s.release());
       return hip_fail(e, "hipStreamCreate");
     }
+    if (s->schedule) L.q = std::make_unique<EngineQueue<FoldJob>>(true);
   }
   try {
+    if (s->schedule)
+      for (int i = 0; i < cfg->engine_lanes; ++i)
+        s->lanes[i]->dispatcher = std::thread(dispatcher_main, s.get(), i);
     s->responder = std::thread(responder_main, s.get());
   } catch (...) {
     byteps_server_destroy(s.release());
-    return fail(BYTEPS_REDUCE_EARGS, "cannot start the pull responder thread");
+    return fail(BYTEPS_REDUCE_EARGS, "cannot start the server's threads");
   }
   *out = s.release();
   return BYTEPS_REDUCE_OK;
@@ -434,13 +643,19 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
 int byteps_server_destroy(byteps_server* s) {
   if (!s) return BYTEPS_REDUCE_OK;
   (void)hipSetDevice(s->cfg.device);
+  destroy_lanes(s);  // queued jobs are issued first (the dispatchers drain)
   if (s->responder.joinable()) {
     for (auto& kv : s->keys) {  // pulls whose round never finished: cancelled
       KeyState* ks = kv.second.get();
       std::lock_guard<std::mutex> g(ks->mu);
       for (auto& wp : ks->waiting)
-        respond_later(s, kv.first, ks, wp.cb, wp.ctx, BYTEPS_REDUCE_ECANCELED);
+        respond_later(s, ks, wp.cb, wp.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
       ks->waiting.clear();
+      for (auto& a : ks->init_acks) {  // init pushes whose round never completed
+        a.status = BYTEPS_REDUCE_ECANCELED;
+        enqueue_response(s, a);
+      }
+      ks->init_acks.clear();
     }
     {
       std::lock_guard<std::mutex> g(s->rq_mu);
@@ -449,24 +664,24 @@ int byteps_server_destroy(byteps_server* s) {
     s->rq_cv.notify_all();
     s->responder.join();
   }
-  for (auto& L : s->lanes) {
-    if (L.fold) (void)hipStreamSynchronize(L.fold);
-    if (L.copy) (void)hipStreamSynchronize(L.copy);
-    if (L.d2h) (void)hipStreamSynchronize(L.d2h);
+  for (auto& Lp : s->lanes) {
+    if (Lp->fold) (void)hipStreamSynchronize(Lp->fold);
+    if (Lp->copy) (void)hipStreamSynchronize(Lp->copy);
+    if (Lp->d2h) (void)hipStreamSynchronize(Lp->d2h);
   }
   for (auto& kv : s->keys) {
     KeyState* ks = kv.second.get();
     if (ks->done) (void)hipEventDestroy(ks->done);
     if (ks->copied) (void)hipEventDestroy(ks->copied);
     if (ks->mirrored) (void)hipEventDestroy(ks->mirrored);
-    for (char* m : ks->mirror)
-      if (m) (void)hipHostFree(m);
+    for (char* m : ks->mirror) (void)hipHostFree(m);
     if (ks->arena) (void)hipFree(ks->arena);
   }
-  for (auto& L : s->lanes) {
-    if (L.fold) (void)hipStreamDestroy(L.fold);
-    if (L.copy) (void)hipStreamDestroy(L.copy);
-    if (L.d2h) (void)hipStreamDestroy(L.d2h);
+  for (auto& Lp : s->lanes) {
+    if (Lp->fold) (void)hipStreamDestroy(Lp->fold);
+    if (Lp->copy) (void)hipStreamDestroy(Lp->copy);
+    if (Lp->d2h) (void)hipStreamDestroy(Lp->d2h);
+    if (Lp->job_done) (void)hipEventDestroy(Lp->job_done);
   }
   delete s;
   return BYTEPS_REDUCE_OK;
@@ -491,11 +706,10 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   KeyState* ks = get_key(s, key, true);
   std::unique_lock<std::mutex> lk(ks->mu);
   if ((rc = allocate(s, ks, len, dtype))) return rc;
-  if (s->cfg.async_mode == 0 && ks->inited && ks->got[worker]) {
-    // A worker's next-round push may arrive while the key still waits for the
-    // other workers' pulls of this round; hold it until the key re-arms.
-    ks->cv.wait(lk, [&] { return !ks->got[worker]; });
-  }
+  // A worker's next push may arrive while its previous one (of this round, or
+  // its init push) is not folded yet: hold it until the slot is free.
+  ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
+  if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
   return arrive_and_wait_init(s, ks, worker, lk);
 }
@@ -511,18 +725,28 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
   KeyState* ks = get_key(s, key, true);
   std::unique_lock<std::mutex> lk(ks->mu);
   if ((rc = allocate(s, ks, len, dtype))) return rc;
-  if (s->cfg.async_mode == 0 && ks->inited && ks->got[worker])
-    ks->cv.wait(lk, [&] { return !ks->got[worker]; });
+  ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
+  if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
+  const bool init_push = !ks->inited;
   if ((rc = arrive(s, ks, worker))) {  // arrival order = call order
     // the caller gets its buffer back on error: let the queued copy finish first
     (void)hipEventSynchronize(ks->copied);
     return rc;
   }
-  Response r{key, ks, nullptr, ctx, nullptr, 0, cb, worker};
-  std::lock_guard<std::mutex> g(s->rq_mu);
-  s->rq.push_back(r);
-  s->rq_cv.notify_one();
+  Response r;
+  r.key = key;
+  r.ks = ks;
+  r.ctx = ctx;
+  r.push_cb = cb;
+  r.worker = worker;
+  if (init_push && !ks->inited) {
+    // server.cc:184-185: an init push is answered only once all NumWorkers
+    // init pushes are in (workers use it as a barrier, operations.cc:301-302)
+    ks->init_acks.push_back(r);
+    return BYTEPS_REDUCE_OK;
+  }
+  enqueue_response(s, r);
   return BYTEPS_REDUCE_OK;
 }
 
@@ -534,8 +758,10 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
   if (!ks || !ks->allocated)
     return fail(BYTEPS_REDUCE_EARGS, "key %llu not initialised (byteps_server_init_key)",
                 (unsigned long long)key);
-  std::lock_guard<std::mutex> g(ks->mu);
-  if (ks->has_done) {  // the slot may be read by the last queued fold
+  std::unique_lock<std::mutex> lk(ks->mu);
+  ks->cv.wait(lk, [&] { return ks->pending == 0 || ks->error; });  // every fold issued
+  if (ks->error) return key_error(ks);
+  if (ks->has_done) {  // the slot may be read by the last issued fold
     hipError_t e = hipEventSynchronize(ks->done);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   }
@@ -552,6 +778,7 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   KeyState* ks = get_key(s, key, false);
   if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
   std::unique_lock<std::mutex> lk(ks->mu);
+  ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   return arrive_and_wait_init(s, ks, worker, lk);
 }
 
@@ -559,37 +786,36 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (!s || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   int rc = set_device(s);
   if (rc) return rc;
-  KeyState* ks = get_key(s, key, false);
-  if (!ks || !ks->allocated)  // server.cc:282-283
-    return fail(BYTEPS_REDUCE_EARGS,
-                "Processing pull request when the key %llu has not been inited yet",
-                (unsigned long long)key);
+  KeyState* ks = key_for_pull(s, key);
+  if (!ks) return BYTEPS_REDUCE_EARGS;
   std::unique_lock<std::mutex> lk(ks->mu);
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
-  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished; });
-  hipStream_t cs = pull_stream(s->cfg.device);
-  if (!cs) return fail(BYTEPS_REDUCE_EHIP, "cannot create the pull stream");
-  // Order the copy after the round's fold while still holding the key lock
-  // (async mode keeps adding into the store); the copy itself runs unlocked.
-  hipError_t e = ks->has_done ? hipStreamWaitEvent(cs, ks->done, 0) : hipSuccess;
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  if (ks->error) return key_error(ks);
+  PullCtx* pc = pull_ctx(s->cfg.device);
+  if (!pc) return fail(BYTEPS_REDUCE_EHIP, "cannot create the pull stream");
+  const hipMemcpyKind kind =
+      location == BYTEPS_SERVER_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  // Order the copy after the key's last issued fold while still holding the key lock.
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(pc->st, ks->done, 0) : hipSuccess;
+  if (s->cfg.async_mode) {
+    // Async mode keeps adding into the store: queue the copy under the lock
+    // and make the lane's later folds wait for it, so none lands mid-copy.
+    if (e == hipSuccess) e = hipMemcpyAsync(out, ks->store, len, kind, pc->st);
+    if (e == hipSuccess) e = hipEventRecord(pc->ev, pc->st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->lanes[ks->lane]->fold, pc->ev, 0);
+    lk.unlock();
+    if (e == hipSuccess) e = hipEventSynchronize(pc->ev);
+    return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "pull copy");
+  }
   lk.unlock();
   // In sync mode the store cannot change while this pull is outstanding: the
   // next round needs this worker's next push, which follows the pull.
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(out, ks->store, len,
-                       location == BYTEPS_SERVER_HOST ? hipMemcpyDeviceToHost
-                                                      : hipMemcpyDeviceToDevice, cs);
-  if (e == hipSuccess) e = hipStreamSynchronize(cs);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, ks->store, len, kind, pc->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(pc->st);
   if (e != hipSuccess) return hip_fail(e, "pull copy");
   lk.lock();
-  if (!s->cfg.async_mode) {
-    // server.cc:105-113: after NumWorkers pulls the key re-arms
-    if (++ks->pull_cnt == s->cfg.num_workers) {
-      ks->push_finished = false;
-      ks->pull_cnt = 0;
-    }
-    ks->cv.notify_all();
-  }
+  count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   return BYTEPS_REDUCE_OK;
 }
 
@@ -600,23 +826,24 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   if (len) *len = 0;
   int rc = set_device(s);
   if (rc) return rc;
-  KeyState* ks = get_key(s, key, false);
-  if (!ks || !ks->allocated)  // server.cc:282-283
-    return fail(BYTEPS_REDUCE_EARGS,
-                "Processing pull request when the key %llu has not been inited yet",
-                (unsigned long long)key);
+  KeyState* ks = key_for_pull(s, key);
+  if (!ks) return BYTEPS_REDUCE_EARGS;
   std::unique_lock<std::mutex> lk(ks->mu);
-  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished; });
-  hipError_t e = hipSuccess;
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  if (ks->error) return key_error(ks);
   if ((rc = ensure_mirror(s, ks, !s->cfg.async_mode))) return rc;
-  // async mode: the store changes with every push, so each view is a fresh D2H
-  if (s->cfg.async_mode && (rc = queue_mirror(s, ks, ks->rounds))) return rc;
-  const char* view = ks->mirror[ks->rounds & 1];
+  size_t idx = ks->rounds & 1;
+  if (s->cfg.async_mode) {  // the store changes with every push: a fresh D2H per view
+    idx = next_async_mirror(ks);
+    if ((rc = queue_mirror(s, ks, idx))) return rc;
+  }
+  const char* view = ks->mirror[idx];
   hipEvent_t ev = ks->mirrored;
   lk.unlock();
   // The event still names this round's copy: the next round cannot finish
   // before this pull is counted below.
-  if ((e = hipEventSynchronize(ev)) != hipSuccess) return hip_fail(e, "store mirror sync");
+  hipError_t e = hipEventSynchronize(ev);
+  if (e != hipSuccess) return hip_fail(e, "store mirror sync");
   lk.lock();
   count_pull(s, ks);
   *data = view;
@@ -629,20 +856,20 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
   if (!s || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   int rc = set_device(s);
   if (rc) return rc;
-  KeyState* ks = get_key(s, key, false);
-  if (!ks || !ks->allocated)  // server.cc:282-283
-    return fail(BYTEPS_REDUCE_EARGS,
-                "Processing pull request when the key %llu has not been inited yet",
-                (unsigned long long)key);
+  KeyState* ks = key_for_pull(s, key);
+  if (!ks) return BYTEPS_REDUCE_EARGS;
   std::lock_guard<std::mutex> g(ks->mu);
+  if (ks->error) return key_error(ks);
   if (s->cfg.async_mode) {  // answered at once from a fresh copy of the store
-    if ((rc = ensure_mirror(s, ks, false)) || (rc = queue_mirror(s, ks, ks->rounds))) return rc;
-    respond_later(s, key, ks, cb, ctx, 0);
+    if ((rc = ensure_mirror(s, ks, false))) return rc;
+    const size_t idx = next_async_mirror(ks);
+    if ((rc = queue_mirror(s, ks, idx))) return rc;
+    respond_later(s, ks, cb, ctx, ks->mirror[idx], 0);
     return BYTEPS_REDUCE_OK;
   }
   if ((rc = ensure_mirror(s, ks, ks->push_finished))) return rc;
   if (ks->push_finished)  // server.cc:293-301: push already finished
-    respond_later(s, key, ks, cb, ctx, 0);
+    respond_later(s, ks, cb, ctx, ks->mirror[ks->rounds & 1], 0);
   else                    // server.cc:303-304: queued until the round finishes
     ks->waiting.push_back({cb, ctx});
   return BYTEPS_REDUCE_OK;
@@ -659,6 +886,23 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
   if (last_order)
     for (int i = 0; i < max_order && i < (int)ks->last_order.size(); ++i)
       last_order[i] = ks->last_order[i];
+  return ks->error ? key_error(ks) : BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* log_keys,
+                             int max_log, int* n_log) {
+  if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
+  if (lane < 0 || lane >= (int)s->lanes.size())
+    return fail(BYTEPS_REDUCE_EARGS, "lane %d outside [0, %zu)", lane, s->lanes.size());
+  Lane& L = *s->lanes[lane];
+  if (pause >= 0) {
+    if (!L.q) return fail(BYTEPS_REDUCE_EARGS, "lane pause needs enable_schedule (no dispatcher)");
+    L.q->hold(pause > 0);
+  }
+  std::lock_guard<std::mutex> g(L.dbg_mu);
+  if (n_log) *n_log = (int)L.log.size();
+  if (log_keys)
+    for (int i = 0; i < max_log && i < (int)L.log.size(); ++i) log_keys[i] = L.log[i];
   return BYTEPS_REDUCE_OK;
 }
 

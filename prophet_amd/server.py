@@ -22,6 +22,7 @@ SERVER_EXPORTS = (
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
+    "byteps_server_debug_lane",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -33,7 +34,7 @@ PUSH_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _int, _int)
 
 class ServerConfig(ctypes.Structure):
     _fields_ = [("num_workers", _int), ("engine_lanes", _int), ("policy", _int),
-                ("async_mode", _int), ("device", _int)]
+                ("async_mode", _int), ("device", _int), ("enable_schedule", _int)]
 
 
 def _lib():
@@ -54,6 +55,8 @@ def _lib():
                                                _vp]
         L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
                                              ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
+        L.byteps_server_debug_lane.argtypes = [_vp, _int, _int, ctypes.POINTER(_u64), _int,
+                                               ctypes.POINTER(_int)]
         L._server_bound = True
     return L
 
@@ -77,9 +80,10 @@ def config_from_env() -> ServerConfig:
 
 class PSServer:
     def __init__(self, num_workers: int, engine_lanes: int = 4, policy: int = FUSED,
-                 async_mode: bool = False, device: int = 0):
+                 async_mode: bool = False, device: int = 0, enable_schedule: bool = False):
         self.lib = _lib()
-        self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device)
+        self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device,
+                                int(enable_schedule))
         self.handle = _vp()
         self._pending = {}
         _check(self.lib.byteps_server_create(ctypes.byref(self.cfg), ctypes.byref(self.handle)))
@@ -132,7 +136,8 @@ class PSServer:
     def pull_view(self, key: int) -> memoryview:
         """Zero-copy pull response (server.cc:42-70): a read-only memoryview of
         the pinned host mirror the server fills with one D2H per round.  Valid
-        until this worker's next pull of the key returns (sync mode)."""
+        until this worker's next pull of the key returns (sync mode), or for the
+        next num_workers pulls of the key (async mode)."""
         p, n = _vp(), _sz()
         _check(self.lib.byteps_server_pull_host_view(self.handle, key, ctypes.byref(p),
                                                      ctypes.byref(n)))
@@ -143,8 +148,8 @@ class PSServer:
         """Non-blocking pull (byteps_server_pull_async; server.cc:286-305 queues
         it until the round finishes).  ``callback(key, view, status)`` runs on the
         server's responder thread with ``view`` a read-only memoryview of the
-        round's host mirror (None unless status == 0); the pull counts toward
-        the key's re-arm when the callback returns."""
+        round's host mirror (None unless status == 0); the pull is counted
+        toward the key's re-arm just before the callback runs."""
         def tramp(_ctx, k, data, n, status):
             try:
                 view = None
@@ -168,6 +173,15 @@ class PSServer:
         _check(self.lib.byteps_server_key_info(self.handle, key, ctypes.byref(rounds),
                                                ctypes.byref(lane), order, self.cfg.num_workers))
         return int(rounds.value), int(lane.value), list(order)
+
+    def debug_lane(self, lane: int, pause: int = -1, max_log: int = 4096) -> list[int]:
+        """Scheduling test hook (byteps_server_debug_lane): pause (1) / release
+        (0) the lane's engine queue; returns the keys it issued so far, in order."""
+        keys = (_u64 * max_log)()
+        n = _int()
+        _check(self.lib.byteps_server_debug_lane(self.handle, lane, pause, keys, max_log,
+                                                 ctypes.byref(n)))
+        return [int(keys[i]) for i in range(min(n.value, max_log))]
 
     def close(self) -> None:
         if self.handle:

@@ -1,0 +1,76 @@
+"""bench.py's multi-rank launcher and its config-4 scaling object, on CPU.
+
+``python bench.py --gpus N`` with no WORLD_SIZE starts N rank processes itself
+(before anything touches a GPU) and exactly one JSON line comes back with
+``n_gpus == N``.  ``--device cpu`` swaps the HIP fold for torch's CPU add and
+RCCL for gloo, so the launcher, the barrier / max-over-ranks timing, the
+config-4 sharded fold and the scatter + all-gather leg all run here; the line
+says it is not a measurement."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(n, extra=()):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", str(n),
+           "--steps", "2", "--warmup", "1", "--workers", "3", "--bucket-mib", "0.0625",
+           "--sets", "2", "--no-cpu-baseline", "--scaling-elems", "10007", *extra]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_launcher_one_line_n_ranks(n):
+    line = _run_bench(n)
+    assert line["n_gpus"] == n
+    assert line["config"]["parallelism"] == f"key-space shard x{n}"
+    assert len(line["config"]["devices"]) == n
+    assert line["check_vs_torch_fold"] is True
+    assert "NOT a measurement" in line["device"]
+    sc = line["scaling_cfg4"]
+    assert sc["exact_vs_torch_fold"] is True
+    assert len(sc["shard_elems"]) == n and sum(sc["shard_elems"]) == 10007
+    assert sc["per_gpu_fold_ms"] > 0 and sc["g1_fold_ms"] > 0
+    assert sc["strong_efficiency"] is not None
+    if n == 1:
+        assert sc["g1_fold_ms"] == sc["per_gpu_fold_ms"] and "scatter" not in sc
+    else:
+        assert sc["scatter"]["exact_vs_torch_fold"] is True
+        assert sc["scatter"]["scatter_fold_ms"] > 0
+
+
+def test_launcher_failing_rank_fails_the_run():
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+           "--mode", "accum", "--no-cpu-baseline"]   # cpu self-test refuses accum mode
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_traffic_quoted_only_for_same_kernel_sources(tmp_path, monkeypatch):
+    import bench
+    bid = bench.kernel_build_id()
+    wl = "8-way f32 left-fold sum of one 256 MiB bucket per GPU"
+    rec = {"workload": wl, "kernel_build": bid, "session": "sX", "hbm_bytes_per_launch": 123.0}
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    t, src = bench.pmc_traffic(wl)
+    assert t == 123.0 and src["session"] == "sX"
+    rec["kernel_build"] = "0" * 16
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
+    t, src = bench.pmc_traffic(wl)
+    assert t is None and "changed" in src["status"]
+    t, src = bench.pmc_traffic("other workload")
+    assert t is None

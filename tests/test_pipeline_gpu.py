@@ -106,3 +106,45 @@ def test_arena_slots_are_skewed_and_disjoint():
     assert all(b - a_ == a.stride for a_, b in zip(ptrs, ptrs[1:]))
     assert a.stride % (1 << 20) != 0
     assert all(s.numel() == 1 << 20 for s in a.slots())
+
+
+@pytest.mark.timeout(600)
+def test_cfg5_full_size_streamed_bf16(red):
+    """BASELINE config 5 at its own size: 16 workers x 256 MiB bf16 (4 GiB of
+    pinned host pushes) streamed H2D -> fold -> D2H by StreamingReducer.  The
+    whole 256 MiB result equals torch's own bf16 left fold (per-step RNE, the
+    build's bf16 rule), and a strided set of windows equals the CPU
+    restatement (parity for bf16 is pinned by the restatement only: the
+    reference has no bf16)."""
+    from prophet_amd.stream import StreamingReducer
+    N, B = 16, 256 << 20
+    n = B // 2
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    host = []
+    for k in range(N):
+        gen.manual_seed(5000 + k)
+        t = torch.empty(B, dtype=torch.uint8).pin_memory()
+        t.view(torch.bfloat16).copy_(torch.randn(n, device=dev, generator=gen)
+                                     .to(torch.bfloat16))
+        host.append(t)
+    out = torch.empty(B, dtype=torch.uint8).pin_memory()
+    StreamingReducer(N, reducer=red).reduce(host, out, B, DType.BFLOAT16)
+    # whole result vs torch's left fold on the device, chunk by chunk
+    step = 32 << 20
+    for o in range(0, n, step):
+        e = min(n, o + step)
+        acc = host[0].view(torch.bfloat16)[o:e].to(dev)
+        for h in host[1:]:
+            acc.add_(h.view(torch.bfloat16)[o:e].to(dev))
+        assert torch.equal(acc.view(torch.int16).cpu(),
+                           out.view(torch.bfloat16)[o:e].view(torch.int16)), f"chunk at {o}"
+    # strided windows vs the restatement
+    port = PortReducer(nthreads=4)
+    W = 65_536
+    for i in range(16):
+        o = (i * (n - W)) // 15
+        ins = [h.numpy()[2 * o: 2 * (o + W)].copy() for h in host]
+        want = np.zeros(2 * W, np.uint8)
+        port.sum_n(want, ins, 2 * W, DType.BFLOAT16)
+        assert np.array_equal(out.numpy()[2 * o: 2 * (o + W)], want), f"window at {o}"

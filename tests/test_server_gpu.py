@@ -29,14 +29,17 @@ def data(dt, n, worker, rnd, key):
         .view(np.uint8)
 
 
+@pytest.mark.parametrize("schedule", [False, True], ids=["fifo", "schedule"])
 @pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
 @pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
-def test_sync_rounds_concurrent_workers(port, policy, dt):
+def test_sync_rounds_concurrent_workers(port, policy, dt, schedule):
+    """... also with BYTEPS_SERVER_ENABLE_SCHEDULE (engine threads issuing
+    queued folds by priority, queue.h:68-97): same bits."""
     from prophet_amd.server import PSServer
     N, R = 8, 3
     sizes = [1, 7, 1000, 65_536 + 3, 1_000_003]    # elements per key
     es = elem_size(dt)
-    srv = PSServer(N, engine_lanes=4, policy=policy)
+    srv = PSServer(N, engine_lanes=4, policy=policy, enable_schedule=schedule)
     bar = threading.Barrier(N + 1)
     errors = []
     results = {}
@@ -430,14 +433,251 @@ def test_push_async_init_store_is_last_call(port):
     srv.close()
 
 
-def test_push_async_error_returns_buffer(port):
-    """A state-machine error (a second init push from one worker) is reported
-    by push_async itself, after its queued copy has finished."""
-    from prophet_amd.reducer import ReduceError
+def test_push_async_init_acks_wait_for_all_init_pushes(port):
+    """server.cc:184-198: init pushes are answered only once all NumWorkers
+    init pushes are in (a barrier for the workers, operations.cc:301-302).
+    A worker that pushes its round-1 push before the other init pushes
+    arrived waits inside the call (its slot still holds the init push), and
+    the round is then folded normally."""
     from prophet_amd.server import PSServer
-    dt, N, n = DType.FLOAT32, 2, 1000
+    dt, N, n = DType.FLOAT32, 2, 100_003
     srv = PSServer(N)
-    srv.push_async(0, 0, data(dt, n, 0, 0, 0), dt)
-    with pytest.raises(ReduceError):
-        srv.push_async(0, 0, data(dt, n, 0, 0, 0), dt)
+    acks = []
+    got = threading.Semaphore(0)
+
+    def ack(k, w, st, tag):
+        acks.append((tag, w, st))
+        got.release()
+    srv.push_async(0, 0, data(dt, n, 0, 0, 0), dt, lambda k, w, st: ack(k, w, st, "init"))
+    time.sleep(0.3)
+    assert acks == []                      # worker 1's init push is missing
+    early = threading.Thread(target=srv.push_async,
+                             args=(0, 0, data(dt, n, 0, 1, 0), dt,
+                                   lambda k, w, st: ack(k, w, st, "r1")))
+    early.start()
+    time.sleep(0.3)
+    assert early.is_alive() and acks == []   # held: its slot still holds the init push
+    srv.push_async(0, 1, data(dt, n, 1, 0, 0), dt, lambda k, w, st: ack(k, w, st, "init"))
+    early.join(timeout=30)
+    assert not early.is_alive()
+    for _ in range(3):
+        assert got.acquire(timeout=30)
+    assert sorted(acks[:2]) == [("init", 0, 0), ("init", 1, 0)]
+    assert acks[2] == ("r1", 0, 0)
+    srv.push(0, 1, data(dt, n, 1, 1, 0), dt)
+    out = np.zeros(n * 4, np.uint8)
+    srv.pull(0, out)
+    assert srv.key_info(0)[2] == [0, 1]
+    want = np.zeros(n * 4, np.uint8)
+    port.sum_n(want, [data(dt, n, w, 1, 0) for w in (0, 1)], n * 4, dt)
+    assert np.array_equal(out, want)
+    srv.close()
+
+
+def test_pull_answer_then_immediate_next_round_push():
+    """The responder counts a pull BEFORE calling back (server.cc:100-113
+    counts under the lock that sends the answer).  Each worker pushes the next
+    round the moment its answers arrive, so a round can complete right after
+    the last answer; a count made after the callback would then land on the
+    new round, re-arm the key one pull early and leave a worker's pull
+    unanswered.  Pulls of a round are issued once every worker has pushed it
+    (after that barrier every earlier answer, hence every earlier count, is
+    done)."""
+    from prophet_amd.server import PSServer
+    N, n, R, keys = 3, 4099, 40, 2
+    dt = DType.INT32
+    srv = PSServer(N, engine_lanes=2)
+    for j in range(keys):
+        ts = [threading.Thread(target=srv.push, args=(j, w, np.zeros(n, np.int32), dt))
+              for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    errors, results = [], {}
+    bar = threading.Barrier(N)
+
+    def worker(w):
+        try:
+            for r in range(1, R + 1):
+                for j in range(keys):
+                    srv.push_async(j, w, np.full(n, 100 * r + w, np.int32), dt)
+                bar.wait(timeout=60)
+                evs = []
+                for j in range(keys):
+                    ev = threading.Event()
+                    box = {}
+
+                    def cb(k, view, st, box=box, ev=ev):
+                        box["v"] = None if view is None else np.frombuffer(view, np.int32).copy()
+                        box["st"] = st
+                        ev.set()
+                    srv.pull_async(j, cb)
+                    evs.append((j, ev, box))
+                for j, ev, box in evs:
+                    assert ev.wait(30), f"worker {w} round {r} key {j}: no answer"
+                    assert box["st"] == 0
+                    results[(w, r, j)] = box["v"]
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=150)
+    assert not any(t.is_alive() for t in ts), "deadlock"
+    assert not errors, errors[:3]
+    assert len(results) == N * R * keys
+    for (w, r, j), v in results.items():
+        assert (v == sum(100 * r + k for k in range(N))).all(), (w, r, j)
+    srv.close()
+
+
+def test_schedule_issue_order():
+    """BYTEPS_SERVER_ENABLE_SCHEDULE (queue.h:68-97): with the lane held, queued
+    SUM_RECV / COPY_MERGED jobs leave by (fewest counted pushes on the key,
+    oldest) — a key whose round is complete (ClearCounter, server.cc:269-271)
+    first — and the results stay the arrival-order folds."""
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.INT32, 3, 10_000
+    srv = PSServer(N, engine_lanes=1, policy=1, enable_schedule=True)
+    for j in range(3):
+        ts = [threading.Thread(target=srv.push, args=(j, w, np.zeros(n, np.int32), dt))
+              for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert srv.debug_lane(0) == []                  # the init round is not queued
+    srv.debug_lane(0, pause=1)
+    val = lambda j, w: np.full(n, 1 + 10 * j + 100 * w, np.int32)   # noqa: E731
+    srv.push(0, 0, val(0, 0), dt)                   # first arrival: accumulator, no job
+    srv.push(0, 1, val(0, 1), dt)                   # job a: SUM_RECV key 0 (count 1)
+    srv.push(1, 0, val(1, 0), dt)
+    srv.push(1, 1, val(1, 1), dt)                   # job b: key 1
+    srv.push(1, 2, val(1, 2), dt)                   # jobs c, d: SUM_RECV + COPY_MERGED, cleared
+    srv.push(2, 0, val(2, 0), dt)
+    srv.push(2, 1, val(2, 1), dt)                   # job e: key 2 (count 1)
+    assert srv.debug_lane(0) == []                  # held: nothing issued yet
+    srv.debug_lane(0, pause=0)
+    out = np.zeros(n, np.int32)
+    srv.pull(1, out)                                # key 1's round finished
+    assert (out == sum(1 + 10 + 100 * w for w in range(N))).all()
+    for j in (0, 2):
+        srv.push(j, 2, val(j, 2), dt)
+    for j in (0, 2):
+        srv.pull(j, out)
+        assert (out == sum(1 + 10 * j + 100 * w for w in range(N))).all()
+    log = srv.debug_lane(0)
+    assert log[:5] == [1, 1, 1, 0, 2], log
+    srv.close()
+
+
+def test_async_mode_pulls_never_torn(port):
+    """Async mode: a blocking pull's copy is ordered before the lane's later
+    folds (no fold lands mid-copy), and views come from a ring of
+    num_workers + 1 mirrors, so the last num_workers views stay intact."""
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.INT32, 3, 8 << 20
+    srv = PSServer(N, async_mode=True, engine_lanes=1)
+    ts = [threading.Thread(target=srv.push, args=(0, w, np.zeros(n, np.int32), dt))
+          for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ones = np.ones(n, np.int32)
+    stop = threading.Event()
+    pushes = []
+
+    def pusher():
+        while not stop.is_set():
+            srv.push(0, len(pushes) % N, ones, dt)
+            pushes.append(1)
+    t = threading.Thread(target=pusher)
+    t.start()
+    try:
+        out = np.zeros(n, np.int32)
+        seen = []
+        for _ in range(12):
+            srv.pull(0, out)
+            assert (out == out[0]).all(), "torn pull"
+            seen.append(int(out[0]))
+        assert seen == sorted(seen)
+        views = []
+        for _ in range(N):
+            v = np.frombuffer(srv.pull_view(0), np.int32)
+            assert (v == v[0]).all(), "torn view"
+            views.append((v, int(v[0])))
+        for v, first in views:                 # the ring kept every one of them
+            assert (v == first).all()
+    finally:
+        stop.set()
+        t.join()
+    srv.close()
+
+
+def _fast_bucket(n, seed):
+    return np.random.default_rng(seed).standard_normal(n, dtype=np.float32).view(np.uint8)
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+@pytest.mark.parametrize("layout", ["1key", "17keys"])
+def test_cfg1_two_workers_64mib(port, policy, layout):
+    """BASELINE config 1 at its own workload: 2 workers push fp32 64 MiB each
+    (host buffers), as ONE key, or split into BytePS's 4,096,000-B partitions
+    (17 keys, global.cc:128-135) on 4 engine lanes; each worker pushes then
+    pulls every key from its own thread; 2 rounds after init.  Every pulled
+    byte equals the oracle's left fold in the recorded arrival order
+    (server.cc:147-308)."""
+    from prophet_amd.server import PSServer
+    dt, N, B, R = DType.FLOAT32, 2, 64 << 20, 2
+    parts = [(0, B)] if layout == "1key" else \
+        [(o, min(4_096_000, B - o)) for o in range(0, B, 4_096_000)]
+    assert len(parts) == (1 if layout == "1key" else 17)
+    srv = PSServer(N, engine_lanes=4, policy=policy)
+    ins = {(w, r): _fast_bucket(B // 4, 1000 + 10 * r + w) for w in range(N) for r in range(R + 1)}
+    outs = {(w, r): np.zeros(B, np.uint8) for w in range(N) for r in range(1, R + 1)}
+    orders = {}
+    errors = []
+    bar = threading.Barrier(N + 1)
+
+    def worker(w):
+        try:
+            for r in range(R + 1):
+                for j, (o, ln) in enumerate(parts):
+                    srv.push(j, w, ins[(w, r)][o:o + ln], dt)
+                bar.wait()
+                bar.wait()
+                if r == 0:
+                    continue
+                for j, (o, ln) in enumerate(parts):
+                    srv.pull(j, outs[(w, r)][o:o + ln])
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for r in range(R + 1):
+        bar.wait()
+        for j in range(len(parts)):
+            rounds, _, order = srv.key_info(j)
+            assert rounds == r
+            orders[(r, j)] = order
+        bar.wait()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    for r in range(1, R + 1):
+        want = np.zeros(B, np.uint8)
+        for j, (o, ln) in enumerate(parts):
+            order = orders[(r, j)]
+            assert sorted(order) == [0, 1]
+            port.sum_n(want[o:o + ln], [ins[(w, r)][o:o + ln] for w in order], ln, dt)
+        for w in range(N):
+            assert np.array_equal(outs[(w, r)], want), (r, w)
     srv.close()
