@@ -150,16 +150,26 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  *   release(q, b, s)       mark block b released once the work queued before it
  *                          on stream s (e.g. the block's H2D pushes) has
  *                          completed; b < 0 releases every block;
+ *   release_range(q, f, c, s)  the same for blocks [f, f + c) in ONE kernel
+ *                          (a Prophet release group spanning several blocks);
  *   status(q, s)           synchronise s and report whether a launch gave up:
  *                          a workgroup that waits longer than the timeout
  *                          (default 2 s) for a release sets a sticky error, every
  *                          workgroup then stops and status returns
  *                          BYTEPS_REDUCE_ETIMEOUT (and clears it).
  *
- * Every block must be released in every iteration; the launch's last workgroup
- * clears the releases, so releases for the next iteration must be ordered
- * after this launch (same stream, or an event).  One launch of a queue at a
- * time.  Table residency as for plans (buffers fixed after InitTensor).  When
+ * Iterations are numbered by epochs (host call order): launch k waits for the
+ * k-th release of every block (its release word >= k), so nothing is re-armed
+ * between iterations, a block may be released before or after its
+ * iteration's launch, and later iterations can be enqueued at once (the
+ * caller keeps iteration k + 1's data from landing before launch k consumed
+ * the buffers).  Every block must be released once per iteration.  After
+ * ETIMEOUT, status() counts the abandoned iteration's missing releases as
+ * given.  A launch captured into a hipGraph replays with its epoch fixed, so a
+ * capture must release every block before the launch (EARGS otherwise).  One
+ * launch of a queue at a time.  Launch and release may be called from
+ * different threads.  Table residency as for plans (buffers fixed after
+ * InitTensor).  When
  * a block's data lands after the launch, its buffers should not share a 128-B
  * line with an earlier block's (a line read for the earlier block may be
  * cached ahead of the later block's DMA).
@@ -177,12 +187,14 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                                 const int* block_end, int nblocks, int dtype, int mode,
                                 byteps_reduce_blockq** q);
 /* Consumer shape: wg_per_cu = 0 (default) dispatch-ordered — one workgroup
- * per tile, each gated on the released-tile mark the release kernel raises;
+ * per tile, each gated on the release words of the blocks up to its own;
  * 1..8 persistent workgroups per CU sweeping the table; < 0 keeps.  Release
  * timeout in seconds (<= 0 keeps). */
 int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s);
 int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream);
 int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* stream);
+int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int count,
+                                       void* stream);
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream);
 int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
 

@@ -572,6 +572,12 @@ struct byteps_reduce_blockq {
   BlockqCtl* ctl = nullptr;
   uint32_t* host_err = nullptr;  // pinned word for blockq_status
   TableInfo ti;
+  // Epochs (host call order): launch k consumes epoch k; the k-th release of
+  // block b carries epoch k.  Guarded: launches and releases may come from
+  // different threads (a transport's receive threads release blocks).
+  std::mutex mu;
+  uint32_t launch_epoch = 0;
+  std::vector<uint32_t> rel_epoch;  // per block: epoch of its latest release
 };
 
 static void blockq_free(byteps_reduce_blockq* q) {
@@ -619,6 +625,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   q->nblocks = nblocks;
   q->gate_occ = gate_occ;
   q->ti = ti;
+  q->rel_epoch.assign((size_t)nblocks, 0u);
   int khz = 0;
   hipError_t e = hipGetDevice(&q->device);
   if (e == hipSuccess)
@@ -637,6 +644,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                   hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->ctl), sizeof(BlockqCtl));
   if (e == hipSuccess) e = hipMemset(q->ctl, 0, sizeof(BlockqCtl));
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // words zeroed before any stream uses them
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&q->host_err), sizeof(uint32_t));
   if (e != hipSuccess) {
@@ -657,6 +665,21 @@ int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double t
 
 int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  hipStream_t s = to_stream(stream);
+  std::lock_guard<std::mutex> g(q->mu);
+  const uint32_t epoch = q->launch_epoch + 1;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+    // A captured launch keeps this epoch in every replay: only iterations
+    // whose releases are captured before it (same graph, stream order) replay
+    // correctly, so that is what a capture must hold.
+    for (int b = 0; b < q->nblocks; ++b)
+      if (!epoch_reached(q->rel_epoch[b], epoch))
+        return fail(BYTEPS_REDUCE_EARGS,
+                    "captured block-queue launch: release every block before the launch "
+                    "(block %d is not; epochs are fixed at capture)", b);
+  }
+  q->launch_epoch = epoch;
   if (q->ti.tiles == 0) return BYTEPS_REDUCE_OK;
   BlockqLaunch Q;
   Q.L = batch_launch(q->dev_table, q->ti);
@@ -665,9 +688,9 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.ctl = q->ctl;
   Q.nblocks = (uint32_t)q->nblocks;
   Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
-  Q.pad[0] = Q.pad[1] = 0;
+  Q.epoch = epoch;
+  Q.pad = 0;
   const Tuning tu = tuning_for_n(q->ti.nmax);
-  hipStream_t s = to_stream(stream);
   const bool gated = q->occ == 0;
   size_t lds;
   if (gated) {
@@ -687,23 +710,41 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     lds = ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255;
   }
   hipError_t e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, s);
-  if (e == hipSuccess && gated)  // re-arm behind the launch, as the persistent kernel's last workgroup does
-    e = launch_blockq_rearm(q->flags, (uint32_t)q->nblocks, q->ctl, s);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
+}
+
+int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int count,
+                                       void* stream) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (first < 0 || count < 0 || first > q->nblocks || count > q->nblocks - first)
+    return fail(BYTEPS_REDUCE_EARGS, "blocks [%d, %d+%d) outside [0, %d)", first, first, count,
+                q->nblocks);
+  hipStream_t s = to_stream(stream);
+  std::lock_guard<std::mutex> g(q->mu);
+  // Each block's release carries its own next epoch; a range whose blocks are
+  // at different epochs (a block released ahead) goes out as one kernel per
+  // run of equal epochs.  A one-wave kernel raises the words at system scope:
+  // a hipMemset node was not seen by the consumer's polls under graph replay,
+  // and hipStreamWriteValue32 measured slower for per-block releases.
+  int b = first;
+  const int end = first + count;
+  while (b < end) {
+    const uint32_t ep = q->rel_epoch[b] + 1;
+    int run = b + 1;
+    while (run < end && q->rel_epoch[run] + 1 == ep) ++run;
+    hipError_t e = launch_blockq_release(q->flags, (uint32_t)b, (uint32_t)(run - b), ep, s);
+    if (e != hipSuccess) return hip_fail(e, "block release");
+    for (int k = b; k < run; ++k) q->rel_epoch[k] = ep;
+    b = run;
+  }
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* stream) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
   if (block >= q->nblocks) return fail(BYTEPS_REDUCE_EARGS, "block %d >= %d", block, q->nblocks);
-  hipStream_t s = to_stream(stream);
-  // A one-wave kernel storing the words at system scope (write-through); a
-  // hipMemset node was not seen by the consumer's polls under graph replay, and
-  // hipStreamWriteValue32 measured slower for per-block releases.
-  const uint32_t first = block < 0 ? 0u : (uint32_t)block;
-  const uint32_t count = block < 0 ? (uint32_t)q->nblocks : 1u;
-  hipError_t e = launch_blockq_release(q->flags, first, count, (uint32_t)q->nblocks,
-                                       q->flags + q->nblocks, q->ctl, s);
-  return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block release");
+  return block < 0 ? byteps_reduce_blockq_release_range(q, 0, q->nblocks, stream)
+                   : byteps_reduce_blockq_release_range(q, block, 1, stream);
 }
 
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
@@ -717,6 +758,13 @@ int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
   e = hipMemsetAsync(&q->ctl->err, 0, sizeof(uint32_t), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "block queue status reset");
+  {
+    // The abandoned iteration's missing releases will not come: count them as
+    // given, so the next iteration's releases carry the next launch's epoch.
+    std::lock_guard<std::mutex> g(q->mu);
+    for (auto& r : q->rel_epoch)
+      if (!epoch_reached(r, q->launch_epoch)) r = q->launch_epoch;
+  }
   return fail(BYTEPS_REDUCE_ETIMEOUT,
               "block queue: a block was not released within %.3f s; the launch stopped early",
               q->timeout_s);

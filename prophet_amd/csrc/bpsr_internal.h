@@ -84,28 +84,31 @@ struct BatchLaunch {
   uint32_t tiles;
 };
 
-// Persistent block consumer (byteps_reduce_blockq_*).  One launch folds the
-// whole table; resident workgroups sweep the tiles in table order, and a
-// workgroup starts a tile only once the tile's block and every block before it
-// have been released (flags[b] != 0, written stream-ordered by
-// byteps_reduce_blockq_release).
-// The launch's last workgroup re-arms the queue (flags, done counter).
+// Block consumer (byteps_reduce_blockq_*).  One launch folds the whole table;
+// a workgroup starts a tile only once the tile's block and every block before
+// it have been released for this launch's EPOCH.  Epochs (launch k consumes
+// epoch k; the k-th release of block b carries epoch k) replace a re-arm step:
+// flags[b] holds the latest epoch block b was released for, so block b is
+// released for launch k iff flags[b] >= k, and nothing is ever cleared.
 struct BlockqCtl {
-  uint32_t released;  // tiles [0, released) are in released blocks (release kernel)
-  uint32_t done;  // workgroups finished in this launch
   uint32_t err;   // sticky: a workgroup gave up waiting for a release
-  uint32_t pad;
+  uint32_t pad[3];
 };
 struct BlockqLaunch {
   BatchLaunch L;
-  uint32_t* flags;              // one word per block, != 0 = released
+  uint32_t* flags;              // one word per block: the latest epoch it was released for
   const uint32_t* block_first;  // first tile of each block, [nblocks] = tiles
   BlockqCtl* ctl;
   uint32_t nblocks;
   uint32_t grid;            // launched (persistent) workgroups
   uint64_t timeout_ticks;   // wall_clock64() ticks a workgroup waits for a release
-  uint32_t pad[2];
+  uint32_t epoch;           // this launch's epoch (>= 1)
+  uint32_t pad;
 };
+// Released for epoch e: the block's word holds e or a later epoch (wrap-safe).
+__host__ __device__ inline bool epoch_reached(uint32_t have, uint32_t e) {
+  return (int32_t)(have - e) >= 0;
+}
 
 struct Tuning {
   int vpt;       // 16-B vectors per thread per tile (1, 2, 4)
@@ -196,10 +199,8 @@ hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, co
                           hipStream_t s);
 hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, bool gated,
                          int dtype, int mode, hipStream_t s);
-hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count,
-                                 uint32_t nblocks, const uint32_t* block_first, BlockqCtl* ctl,
+hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s);
-hipError_t launch_blockq_rearm(uint32_t* flags, uint32_t nblocks, BlockqCtl* ctl, hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.

@@ -93,59 +93,22 @@ hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, co
   }
 }
 
-// Block-queue release (one wave): flags[first .. first+count) = 1 by
-// system-scope atomic stores, so the consumer's system-scope polls see them
-// whatever cache the writer ran behind (a hipMemset node inside a replayed
-// hipGraph was not seen); then, behind a seq_cst fence (two releases racing on
-// two streams must not both miss the other's flag), the released prefix of
-// blocks is recomputed and ctl->released raised to its first tile.
-__device__ __forceinline__ uint32_t ld_sys32(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
+// Block-queue release (one wave) of blocks [first, first + count) for
+// `epoch`: each block's word is raised to the epoch by a system-scope atomic
+// max — the consumers poll at system scope whatever cache the writer ran
+// behind (a hipMemset node inside a replayed hipGraph was not seen), and max,
+// not store, because releases of consecutive epochs may run on different
+// streams out of order.  Nothing is cleared between iterations: launch k
+// waits for words >= k.
 __global__ void blockq_release_kernel(uint32_t* flags, uint32_t first, uint32_t count,
-                                      uint32_t nblocks, const uint32_t* block_first,
-                                      BlockqCtl* ctl) {
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t i = lane; i < count; i += 64)
-    __hip_atomic_store(flags + first + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  uint32_t r = 0;
-  for (;;) {
-    const uint32_t b = r + lane;
-    const bool rel = b >= nblocks || ld_sys32(flags + b) != 0;
-    const uint64_t pending = __ballot(!rel);
-    if (pending != 0) {
-      r += (uint32_t)__builtin_ctzll(pending);
-      break;
-    }
-    r = r + 64 < nblocks ? r + 64 : nblocks;
-    if (r >= nblocks) break;
-  }
-  if (lane == 0)
-    __hip_atomic_fetch_max(&ctl->released, block_first[r], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+                                      uint32_t epoch) {
+  for (uint32_t i = threadIdx.x; i < count; i += 64)
+    __hip_atomic_fetch_max(flags + first + i, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Re-arm behind a dispatch-ordered launch (same stream): releases and the
-// released mark back to 0, system-scope stores.
-__global__ void blockq_rearm_kernel(uint32_t* flags, uint32_t nblocks, BlockqCtl* ctl) {
-  for (uint32_t i = threadIdx.x; i < nblocks; i += 64)
-    __hip_atomic_store(flags + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&ctl->released, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count,
-                                 uint32_t nblocks, const uint32_t* block_first, BlockqCtl* ctl,
+hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s) {
-  hipLaunchKernelGGL(blockq_release_kernel, dim3(1), dim3(64), 0, s, flags, first, count,
-                     nblocks, block_first, ctl);
-  return hipGetLastError();
-}
-
-hipError_t launch_blockq_rearm(uint32_t* flags, uint32_t nblocks, BlockqCtl* ctl, hipStream_t s) {
-  hipLaunchKernelGGL(blockq_rearm_kernel, dim3(1), dim3(64), 0, s, flags, nblocks, ctl);
+  hipLaunchKernelGGL(blockq_release_kernel, dim3(1), dim3(64), 0, s, flags, first, count, epoch);
   return hipGetLastError();
 }
 

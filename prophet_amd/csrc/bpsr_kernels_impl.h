@@ -437,15 +437,16 @@ __global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
 // at the top of every iteration — the returned-atomic register's write-after-
 // write guard — and so an HBM write round trip per tile.)
 // Blocks are consumed in table order: a workgroup may start tile t once every
-// block up to t's is released.  It keeps the first tile past the released
+// block up to t's is released for this launch's epoch.  It keeps the first tile past the released
 // prefix it last saw (`ready_tiles`), so a tile costs one compare unless it
 // crosses that mark; then wave 0 scans the flags 64 at a time (one load per
 // lane), sleeping between polls, and the workgroup acquires at system scope
 // (the data may have landed by DMA or from another queue).  Every wave reaches
 // the exit: all its tiles done, or a release that does not come within
 // Q.timeout_ticks sets the sticky ctl->err, which every waiting workgroup sees
-// on its next poll.  The last workgroup to finish re-arms the queue.  Every
-// access to the flags is a system-scope atomic (releases: blockq_release_kernel).
+// on its next poll.  Nothing is re-armed: the next launch waits for the next
+// epoch.  Every access to the flags is a system-scope atomic (releases:
+// blockq_release_kernel).
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
         const uint64_t t0 = wall_clock64();
         for (;;) {
           const uint32_t b = r + lane;
-          const bool rel = b >= Q.nblocks || ld_sys(Q.flags + b) != 0;
+          const bool rel = b >= Q.nblocks || epoch_reached(ld_sys(Q.flags + b), Q.epoch);
           const uint64_t pending = __ballot(!rel);
           const uint32_t r2 = pending == 0 ? (r + 64 < Q.nblocks ? r + 64 : Q.nblocks)
                                            : r + (uint32_t)__builtin_ctzll(pending);
@@ -517,40 +518,44 @@ __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
                             Q.L.entries, mid);
     __syncthreads();
   }
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (atomicAdd(&Q.ctl->done, 1u) == Q.grid - 1) {
-      // every other workgroup has finished: re-arm
-      for (uint32_t b = 0; b < Q.nblocks; ++b)
-        __hip_atomic_store(Q.flags + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&Q.ctl->released, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&Q.ctl->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // Dispatch-ordered block consumer (the block queue's default mode): one tile
 // record per workgroup, grid = tiles, like batched_kernel — hardware dispatch
-// in tile order keeps the sweep as tight as one batched launch — and each
-// workgroup first checks the released-tile mark that the release kernel
-// publishes (ctl->released, system-scope, raised monotonically).  A workgroup
-// whose tile is not yet released polls the mark (per wave, `s_sleep` between
-// polls, bounded by the timeout) and acquires before its loads; one whose
-// tile is released reads data no workgroup of this launch has touched since
-// the launch's own acquire (blocks do not share lines), so it needs none.
+// in tile order keeps the sweep as tight as one batched launch.  Each wave
+// loads the release words of the first 64 blocks (one system-scope load per
+// lane) together with its record's scalar loads — no extra round trip — and
+// its tile may start once every block up to the tile's own holds this
+// launch's epoch or a later one.  A wave whose tile is not yet released polls
+// the words (`s_sleep` between polls, bounded by the timeout) and acquires
+// before its loads; one whose tile is released reads data no workgroup of
+// this launch has touched since the launch's own acquire (blocks do not share
+// lines), so it needs none.
 template <class Op, int VPT, bool NT>
 __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
   const uint32_t t = blockIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
   const unsigned char* rec = Q.L.recs + (uint64_t)t * Q.L.rec_stride;
-  // the mark (vector load) and the record (scalar loads) travel together
-  const uint32_t relv = ld_sys(&Q.ctl->released);
+  // the words (vector load) and the record (scalar loads) travel together
+  uint32_t w = lane < Q.nblocks ? ld_sys(Q.flags + lane) : Q.epoch;
   const RecRegs r = load_record(rec);
-  const uint32_t rel = __builtin_amdgcn_readfirstlane(relv);
-  if (t >= rel) {
+  const uint32_t blk = reinterpret_cast<const TileHead*>(rec)->block;
+  // every block b <= blk released for this epoch (blocks past 64: rare, more loads)
+  auto released = [&](uint32_t w0) __attribute__((always_inline)) {
+    if (__ballot(lane <= blk && !epoch_reached(w0, Q.epoch)) != 0) return false;
+    for (uint32_t base = 64; base <= blk; base += 64) {
+      const uint32_t b = base + lane;
+      const uint32_t wb = b <= blk ? ld_sys(Q.flags + b) : Q.epoch;
+      if (__ballot(!epoch_reached(wb, Q.epoch)) != 0) return false;
+    }
+    return true;
+  };
+  if (!released(w)) {
     const uint64_t t0 = wall_clock64();
     for (;;) {
       __builtin_amdgcn_s_sleep(4);
-      if (__builtin_amdgcn_readfirstlane(ld_sys(&Q.ctl->released)) > t) break;
+      w = lane < Q.nblocks ? ld_sys(Q.flags + lane) : Q.epoch;
+      if (released(w)) break;
       if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
       if (wall_clock64() - t0 > Q.timeout_ticks) {
         __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

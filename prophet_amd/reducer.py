@@ -50,6 +50,7 @@ EXPORTS = (
     "byteps_reduce_plan_create", "byteps_reduce_plan_launch", "byteps_reduce_plan_destroy",
     "byteps_reduce_blockq_create", "byteps_reduce_blockq_config", "byteps_reduce_blockq_launch",
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
+    "byteps_reduce_blockq_release_range",
 )
 
 
@@ -100,6 +101,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_config.argtypes = [_vp, _int, ctypes.c_double]
     L.byteps_reduce_blockq_launch.argtypes = [_vp, _vp]
     L.byteps_reduce_blockq_release.argtypes = [_vp, _int, _vp]
+    L.byteps_reduce_blockq_release_range.argtypes = [_vp, _int, _int, _vp]
     L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     _LIB = L
@@ -253,9 +255,10 @@ class Plan:
 class BlockQueue:
     """``byteps_reduce_blockq``: a persistent consumer over an iteration's blocks.
 
-    Per iteration: ``launch()`` once, then ``release(b)`` for every block (in
-    any stream order; a block is consumed once it and all earlier blocks are
-    released), ``status()`` to learn whether the launch gave up waiting."""
+    Per iteration: ``launch()`` once and ``release(b)`` for every block, in
+    either order (epochs pair the k-th launch with the k-th release of each
+    block; a block is consumed once it and all earlier blocks are released),
+    ``status()`` to learn whether the launch gave up waiting."""
 
     def __init__(self, lib, blocks, dtype, mode):
         self.lib = lib
@@ -285,6 +288,11 @@ class BlockQueue:
     def release(self, block: int = -1, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_release(self.handle, int(block),
                                                      _stream_of(self.first, stream)))
+
+    def release_range(self, first: int, count: int, stream=None) -> None:
+        """Release blocks [first, first + count) with one kernel."""
+        _check(self.lib.byteps_reduce_blockq_release_range(self.handle, int(first), int(count),
+                                                           _stream_of(self.first, stream)))
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))

@@ -258,3 +258,75 @@ def test_bad_tables_rejected(red, dev):
         rc = red.lib.byteps_reduce_blockq_create(descs, 1, arr, len(ends), 0, 0, ctypes.byref(h))
         assert rc == EARGS
     assert red.lib.byteps_reduce_blockq_release(None, 0, None) == EARGS
+
+
+@SHAPES
+def test_epochs_back_to_back_iterations(red, dev, shape):
+    """Epoch-numbered releases: three iterations enqueued without a host
+    sync — consumer k on a high-priority stream, its releases on a side stream,
+    the next iteration's launch queued right behind — every launch folds its
+    own iteration's data (each iteration rewrites the inputs by a device copy
+    ordered after the previous launch and before its releases)."""
+    dt = DType.FLOAT32
+    blocks = [[(150_000 + 31 * b, 8, "normal"), (4099, 8, "normal")] for b in range(5)]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=shape, timeout_s=5.0)
+    comp, side = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
+    staged, wants, outs = [], [], []
+    for it in range(3):
+        pushes, w = tab.host_inputs(300 + it)
+        staged.append([[p.to(dev) for p in ps] for ps in pushes])
+        wants.append(w)
+    torch.cuda.synchronize()
+    for it in range(3):
+        q.launch(comp)
+        done = torch.cuda.Event()
+        k = 0
+        with torch.cuda.stream(side):
+            for b, blk in enumerate(tab.blocks):
+                for dst, srcs, L in blk:
+                    for s, p in zip(srcs, staged[it][k]):
+                        s.copy_(p, non_blocking=True)
+                    k += 1
+                q.release(b, side)
+        done.record(comp)
+        side.wait_event(done)            # next iteration's data after this consumer
+        with torch.cuda.stream(comp):
+            outs.append([v[0].clone() for v in tab.views])
+    torch.cuda.synchronize()
+    q.status(comp)
+    for it in range(3):
+        for i, (o, w) in enumerate(zip(outs[it], wants[it])):
+            assert np.array_equal(o.cpu().numpy(), w), (it, i)
+    q.close()
+
+
+def test_release_range_and_capture_rule(red, dev):
+    """release_range releases several blocks with one kernel; a captured launch
+    must have every block released before it (its epoch is fixed at capture)."""
+    from prophet_amd.reducer import EARGS, ReduceError
+    dt = DType.FLOAT16
+    blocks = [[(70_000 + b, 8, "normal")] for b in range(7)]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    pushes, wants = tab.host_inputs(9)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    comp, side = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
+    q.launch(comp)
+    q.release_range(4, 3, side)          # out of order, in ranges
+    q.release_range(0, 4, side)
+    comp.synchronize()
+    q.status(comp)
+    tab.check(wants)
+    with pytest.raises(ReduceError):
+        q.release_range(5, 3, side)      # past the last block
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with pytest.raises(ReduceError) as ei:
+        with torch.cuda.graph(g, stream=s):
+            q.launch(s)                  # nothing released for this epoch
+    assert ei.value.code == EARGS
+    torch.cuda.synchronize()
+    q.close()

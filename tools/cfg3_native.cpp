@@ -1,0 +1,227 @@
+// Config 3 from native code (not product code): the block queue
+// (byteps_reduce_blockq_*) driven through its C ABI with no Python in the
+// loop, to measure the device-side bound of live Prophet block releases.
+// ResNet-50 fp16, 8 workers, 165 partitions in 12 Prophet blocks
+// (tools/cfg3_resnet50_table.txt from tools/cfg3_table.py), 3 rotated input
+// sets.  One JSON line per variant: per-iteration ms (median / min / max of
+// `reps` timed runs of `iters` iterations), fraction of the 8 TB/s roofline at
+// (N+1) x bytes per iteration, run-to-run spread, and exactness against one
+// plan over all partitions.
+//   hipcc -O2 -std=c++17 -Iinclude -o tools/cfg3_native tools/cfg3_native.cpp \
+//         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd'
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "bpsr/reduce.h"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(2);                                                                  \
+    }                                                                           \
+  } while (0)
+#define CKR(x)                                                                           \
+  do {                                                                                   \
+    int r_ = (x);                                                                        \
+    if (r_ != 0) {                                                                       \
+      fprintf(stderr, "%s:%d rc=%d %s\n", __FILE__, __LINE__, r_, byteps_reduce_last_error()); \
+      exit(3);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+namespace {
+constexpr int N = 8;
+constexpr int kSets = 3;
+
+struct Table {
+  size_t total = 0;
+  std::vector<std::pair<size_t, size_t>> parts;  // (offset, len) in block order
+  std::vector<int> block_end;
+};
+
+Table read_table(const char* path) {
+  Table t;
+  FILE* f = fopen(path, "r");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path);
+    exit(2);
+  }
+  int np = 0, nb = 0;
+  if (fscanf(f, "%zu %d %d", &t.total, &np, &nb) != 3) exit(2);
+  for (int i = 0; i < np; ++i) {
+    size_t o, l;
+    if (fscanf(f, "%zu %zu", &o, &l) != 2) exit(2);
+    t.parts.push_back({o, l});
+  }
+  for (int i = 0; i < nb; ++i) {
+    int e;
+    if (fscanf(f, "%d", &e) != 1) exit(2);
+    t.block_end.push_back(e);
+  }
+  fclose(f);
+  return t;
+}
+
+struct Set {
+  std::vector<char*> in;
+  char* out = nullptr;
+  char* ref = nullptr;
+  byteps_reduce_blockq* q = nullptr;
+  byteps_reduce_plan* plan_blocks = nullptr;  // all partitions, no block boundaries (bound)
+  byteps_reduce_plan* plan_ref = nullptr;     // the same into ref (exactness check)
+};
+
+std::vector<byteps_bucket_desc> descs(const Table& t, const Set& s, char* dst) {
+  std::vector<byteps_bucket_desc> d(t.parts.size());
+  for (size_t i = 0; i < t.parts.size(); ++i) {
+    std::memset(&d[i], 0, sizeof(d[i]));
+    d[i].dst = dst + t.parts[i].first;
+    for (int k = 0; k < N; ++k) d[i].srcs[k] = s.in[k] + t.parts[i].first;
+    d[i].len = t.parts[i].second;
+    d[i].n = N;
+  }
+  return d;
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  const char* path = argc > 1 ? argv[1] : "tools/cfg3_resnet50_table.txt";
+  const int iters = argc > 2 ? atoi(argv[2]) : 200;
+  const int reps = argc > 3 ? atoi(argv[3]) : 7;
+  const Table t = read_table(path);
+  const int nb = (int)t.block_end.size();
+  CKR(byteps_reduce_init(0));
+  // fp16 inputs: random signs and mantissas, exponents around 1 (finite)
+  std::vector<uint16_t> host(t.total / 2);
+  uint32_t x = 12345u;
+  std::vector<Set> sets(kSets);
+  for (auto& s : sets) {
+    for (int k = 0; k < N; ++k) {
+      for (auto& h : host) {
+        x = x * 1664525u + 1013904223u;
+        h = (uint16_t)(((x >> 16) & 0x83ffu) | (((x >> 8) & 1u) ? 0x3800u : 0x3c00u));
+      }
+      char* p = nullptr;
+      CK(hipMalloc(&p, t.total));
+      CK(hipMemcpy(p, host.data(), t.total, hipMemcpyHostToDevice));
+      s.in.push_back(p);
+    }
+    CK(hipMalloc(&s.out, t.total));
+    CK(hipMalloc(&s.ref, t.total));
+    auto d = descs(t, s, s.out);
+    CKR(byteps_reduce_blockq_create(d.data(), (int)d.size(), t.block_end.data(), nb,
+                                    BYTEPS_REDUCE_FLOAT16, BYTEPS_REDUCE_MODE_REFERENCE, &s.q));
+    CKR(byteps_reduce_blockq_config(s.q, 0, 5.0));
+    CKR(byteps_reduce_plan_create(d.data(), (int)d.size(), BYTEPS_REDUCE_FLOAT16,
+                                  BYTEPS_REDUCE_MODE_REFERENCE, &s.plan_blocks));
+    auto r = descs(t, s, s.ref);
+    CKR(byteps_reduce_plan_create(r.data(), (int)r.size(), BYTEPS_REDUCE_FLOAT16,
+                                  BYTEPS_REDUCE_MODE_REFERENCE, &s.plan_ref));
+  }
+  int lo = 0, hi = 0;
+  CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  hipStream_t cons, rel[2];
+  CK(hipStreamCreateWithPriority(&cons, hipStreamNonBlocking, hi));  // own hardware queue
+  CK(hipStreamCreateWithFlags(&rel[0], hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&rel[1], hipStreamNonBlocking));
+  for (auto& s : sets) CKR(byteps_reduce_plan_launch(s.plan_ref, cons));
+  CK(hipDeviceSynchronize());
+
+  using Fn = std::function<void(int)>;
+  const Fn pre_released = [&](int i) {
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_release(s.q, -1, cons));
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+  };
+  const Fn live = [&](int i) {  // one release per block, behind the launch, on a second stream
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+    for (int b = 0; b < nb; ++b) CKR(byteps_reduce_blockq_release(s.q, b, rel[0]));
+  };
+  const Fn live_2streams = [&](int i) {  // releases alternate between two streams
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+    for (int b = 0; b < nb; ++b) CKR(byteps_reduce_blockq_release(s.q, b, rel[b & 1]));
+  };
+  const Fn live_ranges = [&](int i) {  // release groups of 4 blocks, one kernel each
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+    for (int b = 0; b < nb; b += 4)
+      CKR(byteps_reduce_blockq_release_range(s.q, b, std::min(4, nb - b), rel[0]));
+  };
+  const Fn release_first = [&](int i) {  // releases issued before the launch, other stream
+    Set& s = sets[i % kSets];
+    for (int b = 0; b < nb; ++b) CKR(byteps_reduce_blockq_release(s.q, b, rel[0]));
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+  };
+  const Fn plan_no_blocks = [&](int i) {
+    CKR(byteps_reduce_plan_launch(sets[i % kSets].plan_blocks, cons));
+  };
+  struct V {
+    const char* name;
+    const Fn* fn;
+  };
+  const V variants[] = {{"plan_all_partitions_no_blocks", &plan_no_blocks},
+                        {"blockq_pre_released", &pre_released},
+                        {"blockq_live_release", &live},
+                        {"blockq_live_release_2streams", &live_2streams},
+                        {"blockq_live_release_ranges4", &live_ranges},
+                        {"blockq_releases_first_other_stream", &release_first}};
+  const double alg = (double)(N + 1) * (double)t.total;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (const V& v : variants) {
+    for (int i = 0; i < 30; ++i) (*v.fn)(i);
+    CK(hipDeviceSynchronize());
+    std::vector<double> ms;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0, cons));
+      for (int i = 0; i < iters; ++i) (*v.fn)(i);
+      CK(hipEventRecord(e1, cons));
+      CK(hipDeviceSynchronize());
+      float el = 0;
+      CK(hipEventElapsedTime(&el, e0, e1));
+      ms.push_back(el / iters);
+    }
+    int status = 0;
+    for (auto& s : sets) status |= byteps_reduce_blockq_status(s.q, cons);
+    bool exact = true;
+    std::vector<char> a(t.total), b(t.total);
+    for (auto& s : sets) {
+      CK(hipMemcpy(a.data(), s.out, t.total, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(b.data(), s.ref, t.total, hipMemcpyDeviceToHost));
+      exact = exact && std::memcmp(a.data(), b.data(), t.total) == 0;
+      CK(hipMemset(s.out, 0, t.total));  // the next variant must write it again
+    }
+    std::sort(ms.begin(), ms.end());
+    const double med = ms[ms.size() / 2];
+    printf("{\"config\": \"cfg3\", \"driver\": \"native C++ (tools/cfg3_native.cpp)\", "
+           "\"variant\": \"%s\", \"n_workers\": %d, \"partitions\": %zu, \"blocks\": %d, "
+           "\"bytes_per_worker\": %zu, \"iters\": %d, \"reps\": %d, \"ms\": %.5f, "
+           "\"min_ms\": %.5f, \"max_ms\": %.5f, \"spread\": %.4f, \"hbm_frac\": %.4f, "
+           "\"status\": %d, \"exact_vs_plan\": %s}\n",
+           v.name, N, t.parts.size(), nb, t.total, iters, reps, med, ms.front(), ms.back(),
+           (ms.back() - ms.front()) / med, alg / (med * 1e-3) / 8e12, status,
+           exact ? "true" : "false");
+    fflush(stdout);
+  }
+  for (auto& s : sets) {
+    byteps_reduce_blockq_destroy(s.q);
+    byteps_reduce_plan_destroy(s.plan_blocks);
+    byteps_reduce_plan_destroy(s.plan_ref);
+    for (char* p : s.in) CK(hipFree(p));
+    CK(hipFree(s.out));
+    CK(hipFree(s.ref));
+  }
+  return 0;
+}

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-2 GPU session steps.  Each GPU step has its own time limit; the script
+# stops at the first step that ends in anything other than success or an
+# ordinary test failure (fault, abort, segfault, timeout).
+#   usage: tools/gpu_r02.sh <tag> <steps...>
+set -u
+TAG=${1:-r02}; shift || true
+STEPS=${*:-"gputest"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -3 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)" | tee -a "$OUT/steps.log"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    gputest) run gputest 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    blockq) run blockq 400 python -u -m pytest tests/test_blockq_gpu.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    server) run server 400 python -u -m pytest tests/test_server_gpu.py -x -v -p no:cacheprovider --timeout 200 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    cfg3n) run cfg3_native 300 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 7 ;;
+    cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
+    cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
+    cfg1trace) run cfg1_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+             -d "$OUT/cfg1trace" -o cfg1 -- ./tools/cfg1_native 4 6 ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-scaling ;;
+    pmc)   run pmc 900 python tools/pmc_traffic.py --out "$OUT/pmc" ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "done"
