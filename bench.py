@@ -195,9 +195,22 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
         return dict(threads=threads, gibps=n_workers * L / med / GIB, median_s=med,
                     min_s=min(ts), reps=len(ts))
 
-    default = leg(PortReducer(nthreads=4), 4, 10.0)
+    class _Baseline:
+        """The restatement in the reference's loop shape (bpsr_oracle_sum_simd:
+        `omp parallel for simd`, AVX) where it has one; else its bit-level form."""
+        def __init__(self, threads):
+            self.p = PortReducer(nthreads=threads)
+            self.simd = dtype_id in (0, 1, 3, 4, 5, 6)
+
+        def sum(self, d, s, n, dt):
+            return self.p.sum_simd(d, s, n, dt) if self.simd else self.p.sum(d, s, n, dt)
+
+        def copy(self, d, s, n):
+            return self.p.copy(d, s, n)
+
+    default = leg(_Baseline(4), 4, 10.0)
     all_threads = max(1, min(ncpu, 64))
-    allc = leg(PortReducer(nthreads=all_threads), all_threads, 4.0)
+    allc = leg(_Baseline(all_threads), all_threads, 4.0)
     ref = None
     if dtype_id != 11 and RefReducer.available():
         r = leg(RefReducer(nthreads=4), 4, 3.0)
@@ -218,7 +231,8 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
         "kind": "port",
         "sample": (f"{n_workers}-way server round (zero-copy first arrival, {n_workers - 1} "
                    f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket (the "
-                   f"headline bucket), clean-room restatement oracle/bpsr_oracle.c, median of "
+                   f"headline bucket), clean-room restatement oracle/bpsr_oracle.c in the "
+                   f"reference's omp-simd loop shape (bpsr_oracle_sum_simd), median of "
                    f"{default['reps']} reps (~10 s of CPU work); 4 OpenMP threads = "
                    f"BYTEPS_OMP_THREAD_PER_GPU default (cpu_reducer.cc:40-44)"),
         "all_cores": {"value": round(allc["gibps"], 3), "cores": allc["threads"],

@@ -211,6 +211,59 @@ int bpsr_oracle_copy(void* dst, const void* src, size_t len, int nthreads) {
   return 0;
 }
 
+/* CPU-baseline form of sum (bench.py's cpu_baseline leg; still test
+ * infrastructure): the reference's own loop shape, cpu_reducer.cc:85-92
+ * `#pragma omp parallel for simd` over storage-type adds, built for AVX like
+ * the reference (setup.py:171-172).  Same bits as bpsr_oracle_sum for every
+ * non-NaN input (IEEE add in the storage type; integers wrap); which payload
+ * a NaN+NaN keeps follows the compiler's operand order, as in the reference
+ * (tests compare those by class).  fp16/bf16 are not vectorised here: -1, and
+ * the caller uses bpsr_oracle_sum. */
+__attribute__((target("avx")))
+int bpsr_oracle_sum_simd(void* dst, const void* src, size_t len, int dtype, int nthreads) {
+  long long i;
+  switch (dtype) {
+    case ORC_FLOAT32: {
+      long long n = (long long)(len / 4);
+      float* o = (float*)dst; const float* x = (const float*)src;
+#pragma omp parallel for simd num_threads(NT(nthreads))
+      for (i = 0; i < n; ++i) o[i] = o[i] + x[i];
+      return 0;
+    }
+    case ORC_FLOAT64: {
+      long long n = (long long)(len / 8);
+      double* o = (double*)dst; const double* x = (const double*)src;
+#pragma omp parallel for simd num_threads(NT(nthreads))
+      for (i = 0; i < n; ++i) o[i] = o[i] + x[i];
+      return 0;
+    }
+    case ORC_UINT8:
+    case ORC_INT8: {
+      long long n = (long long)len;
+      uint8_t* o = (uint8_t*)dst; const uint8_t* x = (const uint8_t*)src;
+#pragma omp parallel for simd num_threads(NT(nthreads))
+      for (i = 0; i < n; ++i) o[i] = (uint8_t)(o[i] + x[i]);
+      return 0;
+    }
+    case ORC_INT32: {
+      long long n = (long long)(len / 4);
+      uint32_t* o = (uint32_t*)dst; const uint32_t* x = (const uint32_t*)src;
+#pragma omp parallel for simd num_threads(NT(nthreads))
+      for (i = 0; i < n; ++i) o[i] = o[i] + x[i];
+      return 0;
+    }
+    case ORC_INT64: {
+      long long n = (long long)(len / 8);
+      uint64_t* o = (uint64_t*)dst; const uint64_t* x = (const uint64_t*)src;
+#pragma omp parallel for simd num_threads(NT(nthreads))
+      for (i = 0; i < n; ++i) o[i] = o[i] + x[i];
+      return 0;
+    }
+    default:
+      return -1;
+  }
+}
+
 int bpsr_oracle_sum_n(void* dst, const void* const* srcs, int n, size_t len, int dtype,
                       int nthreads) {
   if (n < 1 || !dst || !srcs) return -2;

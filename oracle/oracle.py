@@ -49,6 +49,7 @@ class PortReducer:
         L = self.lib
         L.bpsr_oracle_sum.argtypes = [_vp, _vp, _sz, _int, _int]
         L.bpsr_oracle_sum3.argtypes = [_vp, _vp, _vp, _sz, _int, _int]
+        L.bpsr_oracle_sum_simd.argtypes = [_vp, _vp, _sz, _int, _int]
         L.bpsr_oracle_copy.argtypes = [_vp, _vp, _sz, _int]
         L.bpsr_oracle_sum_n.argtypes = [_vp, ctypes.POINTER(_vp), _int, _sz, _int, _int]
         L.bpsr_oracle_half_to_float.argtypes = [ctypes.c_uint16]
@@ -59,6 +60,11 @@ class PortReducer:
 
     def sum(self, dst, src, length: int, dtype: int) -> int:
         return self.lib.bpsr_oracle_sum(_ptr(dst), _ptr(src), length, int(dtype), self.nthreads)
+
+    def sum_simd(self, dst, src, length: int, dtype: int) -> int:
+        """The vectorised CPU-baseline form (fp32/fp64/ints; -1 otherwise)."""
+        return self.lib.bpsr_oracle_sum_simd(_ptr(dst), _ptr(src), length, int(dtype),
+                                             self.nthreads)
 
     def sum3(self, dst, a, b, length: int, dtype: int) -> int:
         return self.lib.bpsr_oracle_sum3(_ptr(dst), _ptr(a), _ptr(b), length, int(dtype),

@@ -132,3 +132,28 @@ def test_port_vs_reference_copy_and_sum3(port):
         ref.sum3(x, a, b, L, dt)
         port.sum3(y, a, b, L, dt)
         assert_bytes_match(dt, y, x, what=f"sum3 {DType(dt).name}")
+
+
+SIMD_DTYPES = {int(d) for d in (DType.FLOAT32, DType.FLOAT64, DType.INT32, DType.INT64,
+                                DType.INT8, DType.UINT8)}
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["op"] == "fold"
+                                  and c["dtype"] in SIMD_DTYPES], ids=case_id)
+def test_simd_baseline_form_matches_golden(port, case):
+    """bench.py's CPU baseline times bpsr_oracle_sum_simd (the reference's
+    `omp parallel for simd` loop shape): same bits as the reference on every
+    golden fold; NaN+NaN positions by class, as for the reference itself."""
+    ins = inputs(case)
+    L = case["len_bytes"]
+    dst = np.full(L, 0x5A, dtype=np.uint8)
+    assert port.copy(dst, ins[0], L) == 0
+    for s in ins[1:]:
+        assert port.sum_simd(dst, s, L, case["dtype"]) == 0
+    assert_bytes_match(case["dtype"], dst, expected(case), what=case_id(case))
+
+
+def test_simd_baseline_refuses_half_types(port):
+    a = np.zeros(16, np.uint8)
+    assert port.sum_simd(a, a.copy(), 16, DType.FLOAT16) == -1
+    assert port.sum_simd(a, a.copy(), 16, DType.BFLOAT16) == -1

@@ -36,6 +36,7 @@ for s in $STEPS; do
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
+    cfg1q8) run cfg1_native_hwq8 300 env GPU_MAX_HW_QUEUES=8 ./tools/cfg1_native 4 20 ;;
     cfg1trace) run cfg1_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
              -d "$OUT/cfg1trace" -o cfg1 -- ./tools/cfg1_native 4 6 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
