@@ -209,7 +209,13 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
             return self.p.copy(d, s, n)
 
     default = leg(_Baseline(4), 4, 10.0)
-    all_threads = max(1, min(ncpu, 64))
+    # the host share this process may use: OMP_NUM_THREADS when the box sets it
+    # (16 per GPU on the GPU pool, whose affinity mask shows every host CPU)
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        share = 0
+    all_threads = max(1, min(share or ncpu, 64))
     allc = leg(_Baseline(all_threads), all_threads, 4.0)
     ref = None
     if dtype_id != 11 and RefReducer.available():

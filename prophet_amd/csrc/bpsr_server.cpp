@@ -96,6 +96,7 @@ struct KeyState {
   std::vector<int> last_order;
   hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the last issued fold
   hipEvent_t copied = nullptr;
+  hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
   bool has_done = false;
   // pinned host mirrors of the store for zero-copy pull responses
   // (server.cc:42-70 responds from the store itself).  Sync mode: two, by
@@ -196,6 +197,8 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   if ((e = hipEventCreateWithFlags(&ks->done, hipEventDisableTiming)) != hipSuccess)
     return hip_fail(e, "hipEventCreate");
   if ((e = hipEventCreateWithFlags(&ks->copied, hipEventDisableTiming)) != hipSuccess)
+    return hip_fail(e, "hipEventCreate");
+  if ((e = hipEventCreateWithFlags(&ks->pulled, hipEventDisableTiming)) != hipSuccess)
     return hip_fail(e, "hipEventCreate");
   ks->len = len;
   ks->dtype = dtype;
@@ -541,24 +544,22 @@ int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock
   return ks->error ? key_error(ks) : 0;
 }
 
-// Per-thread stream and event for pull copies (a pull blocks only on its own copy).
-struct PullCtx {
-  hipStream_t st = nullptr;
-  hipEvent_t ev = nullptr;
-  int dev = -1;
-};
-PullCtx* pull_ctx(int device) {
-  thread_local PullCtx c;
-  if (c.st && c.dev == device) return &c;
-  if (c.st) (void)hipStreamDestroy(c.st);
-  if (c.ev) (void)hipEventDestroy(c.ev);
-  c.st = nullptr;
-  c.ev = nullptr;
-  c.dev = device;
-  if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c.ev, hipEventDisableTiming) != hipSuccess)
-    return nullptr;
-  return &c;
+// The pull destination as the device addresses it: device memory itself, or
+// pinned host memory mapped for the device; nullptr for pageable memory.
+void* device_view(void* out, int location) {
+  if (location == BYTEPS_SERVER_DEVICE) return out;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, out, 0) == hipSuccess && d) return d;
+  (void)hipGetLastError();  // pageable: not an error, just not addressable
+  return nullptr;
+}
+
+bool pull_by_kernel() {
+  static const bool on = [] {
+    const char* v = getenv("BPSR_SERVER_PULL_COPY");
+    return !(v && std::string(v) == "memcpy");
+  }();
+  return on;
 }
 
 KeyState* key_for_pull(byteps_server* s, uint64_t key) {
@@ -613,12 +614,20 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  const char* pv = getenv("BPSR_SERVER_D2H_PRIORITY");
+  const int d2h_prio = (pv && std::string(pv) == "normal") ? prio_lo : prio_hi;
   for (int i = 0; i < cfg->engine_lanes; ++i) {
     s->lanes.push_back(std::make_unique<Lane>());
     Lane& L = *s->lanes.back();
     hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
+    // d2h streams (mirror copies, copying pulls) at the highest priority: a
+    // hardware queue of their own, so a pull's copy never waits behind another
+    // lane's fold that is still waiting for its H2D pushes (HIP multiplexes a
+    // process's streams onto a few in-order hardware queues).
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.d2h, hipStreamNonBlocking, d2h_prio);
     if (e == hipSuccess && s->schedule)
       e = hipEventCreateWithFlags(&L.job_done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -673,6 +682,7 @@ int byteps_server_destroy(byteps_server* s) {
     KeyState* ks = kv.second.get();
     if (ks->done) (void)hipEventDestroy(ks->done);
     if (ks->copied) (void)hipEventDestroy(ks->copied);
+    if (ks->pulled) (void)hipEventDestroy(ks->pulled);
     if (ks->mirrored) (void)hipEventDestroy(ks->mirrored);
     for (char* m : ks->mirror) (void)hipHostFree(m);
     if (ks->arena) (void)hipFree(ks->arena);
@@ -792,28 +802,36 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
   if (ks->error) return key_error(ks);
-  PullCtx* pc = pull_ctx(s->cfg.device);
-  if (!pc) return fail(BYTEPS_REDUCE_EHIP, "cannot create the pull stream");
-  const hipMemcpyKind kind =
-      location == BYTEPS_SERVER_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-  // Order the copy after the key's last issued fold while still holding the key lock.
-  hipError_t e = ks->has_done ? hipStreamWaitEvent(pc->st, ks->done, 0) : hipSuccess;
-  if (s->cfg.async_mode) {
-    // Async mode keeps adding into the store: queue the copy under the lock
-    // and make the lane's later folds wait for it, so none lands mid-copy.
-    if (e == hipSuccess) e = hipMemcpyAsync(out, ks->store, len, kind, pc->st);
-    if (e == hipSuccess) e = hipEventRecord(pc->ev, pc->st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s->lanes[ks->lane]->fold, pc->ev, 0);
-    lk.unlock();
-    if (e == hipSuccess) e = hipEventSynchronize(pc->ev);
-    return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "pull copy");
+  // The copy runs on the lane's d2h stream behind the key's last issued fold,
+  // queued under the key lock.  Device or pinned destinations are written by
+  // the library's copy kernel (the store mirror's path, link rate whatever is
+  // queued beside it); pageable ones by hipMemcpyAsync.  No per-thread
+  // streams: a transport's pull threads come and go, and a stream per thread
+  // (round 1) cost a stream creation per new thread and multiplied the
+  // streams sharing the process's few hardware queues.
+  Lane& L = *s->lanes[ks->lane];
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
+  if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+  void* dv = pull_by_kernel() ? device_view(out, location) : nullptr;
+  if (dv) {
+    if ((rc = byteps_reduce_copy(dv, ks->store, len, L.d2h))) return rc;
+  } else {
+    e = hipMemcpyAsync(out, ks->store, len,
+                       location == BYTEPS_SERVER_HOST ? hipMemcpyDeviceToHost
+                                                      : hipMemcpyDeviceToDevice, L.d2h);
   }
-  lk.unlock();
-  // In sync mode the store cannot change while this pull is outstanding: the
-  // next round needs this worker's next push, which follows the pull.
-  if (e == hipSuccess) e = hipMemcpyAsync(out, ks->store, len, kind, pc->st);
-  if (e == hipSuccess) e = hipStreamSynchronize(pc->st);
+  if (e == hipSuccess) e = hipEventRecord(ks->pulled, L.d2h);
+  // Async mode keeps adding into the store: the lane's later folds wait for
+  // this copy, so none lands mid-copy.  (Sync mode: the store cannot change
+  // while the pull is outstanding — the next round needs this worker's next
+  // push, which follows the pull.)
+  if (e == hipSuccess && s->cfg.async_mode) e = hipStreamWaitEvent(L.fold, ks->pulled, 0);
   if (e != hipSuccess) return hip_fail(e, "pull copy");
+  hipEvent_t ev = ks->pulled;  // a later pull may re-record it: it then covers this copy too
+  lk.unlock();
+  e = hipEventSynchronize(ev);
+  if (e != hipSuccess) return hip_fail(e, "pull copy");
+  if (s->cfg.async_mode) return BYTEPS_REDUCE_OK;
   lk.lock();
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   return BYTEPS_REDUCE_OK;

@@ -36,12 +36,15 @@ for s in $STEPS; do
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
+    cfg1memcpy) run cfg1_native_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy ./tools/cfg1_native 4 20 ;;
+    cfg1prio) run cfg1_native_d2h_normal 300 env BPSR_SERVER_D2H_PRIORITY=normal ./tools/cfg1_native 4 20 ;;
+    cfg1q16) run cfg1_native_hwq16 300 env GPU_MAX_HW_QUEUES=16 BPSR_SERVER_D2H_PRIORITY=normal ./tools/cfg1_native 4 20 ;;
     cfg1q8) run cfg1_native_hwq8 300 env GPU_MAX_HW_QUEUES=8 ./tools/cfg1_native 4 20 ;;
     cfg1trace) run cfg1_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
              -d "$OUT/cfg1trace" -o cfg1 -- ./tools/cfg1_native 4 6 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-scaling ;;
-    pmc)   run pmc 900 python tools/pmc_traffic.py --out "$OUT/pmc" ;;
+    pmc)   run pmc 900 python tools/pmc_traffic.py --out "$OUT/pmc" --session "$TAG" ;;
     *) echo "unknown step $s" ;;
   esac
 done

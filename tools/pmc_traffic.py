@@ -60,6 +60,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     p.add_argument("--commit", action="store_true")
+    p.add_argument("--session", default=os.environ.get("BPSR_SESSION", ""),
+                   help="session tag recorded with the numbers (bench line traffic_source)")
     p.add_argument("bench_args", nargs="*",
                    default=["--steps", "12", "--warmup", "2", "--no-cpu-baseline"])
     a = p.parse_args()
@@ -67,8 +69,12 @@ def main():
     fetch, bl = run_pass("FETCH_SIZE", a.out, a.bench_args)
     write, _ = run_pass("WRITE_SIZE", a.out, a.bench_args)
     cfg = bl.get("config", {})
+    sys.path.insert(0, ROOT)
+    import bench
     res = {
         "workload": cfg.get("workload"),
+        "session": a.session or None,
+        "kernel_build": bench.kernel_build_id(),
         "kernel": KERNEL_KEY,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": statistics.median(fetch) if fetch else None,
