@@ -58,8 +58,11 @@ DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
 # traffic record is quoted only while their hash matches (bench line
 # roofline.traffic_source).
 KERNEL_SOURCES = ("prophet_amd/csrc/bpsr_kernels_impl.h", "prophet_amd/csrc/bpsr_ops.h",
-                  "prophet_amd/csrc/bpsr_internal.h", "prophet_amd/csrc/bpsr_k_f32.hip",
-                  "prophet_amd/csrc/bpsr_api.cpp")
+                  "prophet_amd/csrc/bpsr_internal.h", "prophet_amd/csrc/bpsr_k_f32.hip")
+# ... plus the launch-geometry rules of the C ABI (tuning defaults, residency by
+# source count): this span of bpsr_api.cpp, not the whole file
+KERNEL_SOURCE_SPANS = (("prophet_amd/csrc/bpsr_api.cpp", "static Tuning& tuning_storage()",
+                        "static inline hipStream_t to_stream"),)
 
 
 def parse(argv=None):
@@ -75,6 +78,9 @@ def parse(argv=None):
     p.add_argument("--sets", type=int, default=3, help="rotated input sets")
     p.add_argument("--layout", default="arena", choices=["arena", "separate"],
                    help="worker slots in one skewed HBM arena, or separate allocations")
+    p.add_argument("--skew", type=int, default=-1,
+                   help="arena: bytes between consecutive slots beyond the 4 KiB-rounded "
+                        "bucket (default: prophet_amd.arena.DEFAULT_SKEW)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-scaling", action="store_true",
                    help="skip the config-4 (VGG-16 sharded) scaling object")
@@ -466,10 +472,16 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
 
 
 def kernel_build_id(root: str = ROOT) -> str:
+    """Hash of what decides the headline kernel's code and launch geometry."""
     h = hashlib.sha256()
     for rel in KERNEL_SOURCES:
         with open(os.path.join(root, rel), "rb") as f:
             h.update(rel.encode() + b"\0" + f.read())
+    for rel, a, b in KERNEL_SOURCE_SPANS:
+        with open(os.path.join(root, rel)) as f:
+            text = f.read()
+        i = text.index(a)
+        h.update(rel.encode() + b"\0" + text[i:text.index(b, i)].encode())
     return h.hexdigest()[:16]
 
 
@@ -571,7 +583,8 @@ def main(argv=None):
     sets = []
     for s in range(args.sets):
         if args.layout == "arena":
-            slots = BucketArena(N + 1, B, dev).slots()
+            slots = (BucketArena(N + 1, B, dev) if args.skew < 0 else
+                     BucketArena(N + 1, B, dev, skew=args.skew)).slots()
         else:
             slots = [torch.empty(B, dtype=torch.uint8, device=dev) for _ in range(N + 1)]
         for t in slots[:N]:
@@ -643,7 +656,8 @@ def main(argv=None):
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (torch.randn on device, seeded per rank), resident in HBM, "
-                f"{args.sets} rotated input sets, layout={args.layout}",
+                f"{args.sets} rotated input sets, layout={args.layout}"
+                + (f", skew={args.skew}" if args.skew >= 0 else ""),
         "config": {"workload": workload, "n_workers": N, "bucket_bytes": B,
                    "parallelism": f"key-space shard x{world}", "kernel": "byteps_reduce_sum_n",
                    "tuning": tuning, "devices": devices},
