@@ -35,6 +35,7 @@ for s in $STEPS; do
     cfg3n) run cfg3_native 300 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 7 ;;
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
+    cfg3py) run cfg3_python 600 python tools/bench_configs.py --only cfg3 ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
     cfg1memcpy) run cfg1_native_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy ./tools/cfg1_native 4 20 ;;
     cfg1prio) run cfg1_native_d2h_normal 300 env BPSR_SERVER_D2H_PRIORITY=normal ./tools/cfg1_native 4 20 ;;
