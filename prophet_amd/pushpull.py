@@ -1,0 +1,192 @@
+"""End-to-end push_pull of whole gradient tensors over the GPU-resident PS server.
+
+The worker side of byteps/common/operations.cc and the server side of
+byteps/server/server.cc, with an in-process transport:
+
+* ``declare`` — every worker registers its tensors in the same order; the
+  position is the tensor's declared key (BytePSGlobal's declared-tensor list);
+* ``init_tensor`` — ``InitTensor`` (operations.cc:219-316): the key list is
+  ``(declared_key << 16) + i`` for the partitions of ``size`` bytes under the
+  partition bound (global.cc:128-135, aligned down to 8 * local_size), and
+  each partition is pushed once, blocking — the store's init round and the
+  workers' global barrier (operations.cc:301-302);
+* ``push_pull`` — ``EnqueueTensor`` (operations.cc:138-217) with
+  ``PartitionTensor`` (:99-136): the tensor is cut into the same partitions,
+  each one is pushed under its key and pulled back, and the aggregate lands at
+  its offset of the output — optionally in the order the Prophet PUSH
+  scheduler releases partitions (scheduled_queue.cc:217-296,
+  ``prophet_amd.prophet.ProphetPushQueue``);
+* the server front end decodes the request word like ``BytePSHandler``
+  (``DepairDataHandleType``, server.h:77-88, of ``GetCommandType``'s Cantor
+  pairing, common.cc:99-102) and hands the bytes to ``PSServer``.
+
+Buffers may be host (numpy / CPU tensors) or device tensors; every byte of
+arithmetic is the server's HIP fold.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+
+from .buckets import DEFAULT_PARTITION_BYTES, cantor_command, depair_command, partition_bound
+from .dtypes import DType, elem_size
+
+K_DEFAULT_PUSH_PULL = 0     # RequestType::kDefaultPushPull (common.h:68-71)
+
+
+class ServerFrontend:
+    """The handler in front of the GPU-resident server: decodes the request
+    word, checks one key per request (server.cc:150-171) and forwards."""
+
+    def __init__(self, server):
+        self.server = server
+
+    def push(self, cmd: int, key: int, worker: int, data, nbytes: int) -> None:
+        req, dtype = depair_command(cmd)
+        if req != K_DEFAULT_PUSH_PULL:       # server.cc:151 CHECK_EQ(type.requestType, ...)
+            raise ValueError(f"request type {req} is not kDefaultPushPull")
+        self.server.push(key, worker, data, dtype, nbytes=nbytes)
+
+    def pull(self, key: int, out, nbytes: int) -> None:
+        self.server.pull(key, out, nbytes=nbytes)
+
+
+@dataclass
+class Context:
+    """BPSContext (common.h): one declared tensor's keys and partitions."""
+    name: str
+    declared_key: int
+    size: int = 0
+    dtype: int = 0
+    key_list: list = field(default_factory=list)
+    parts: list = field(default_factory=list)      # (key, offset, len) in bytes
+    initialized: bool = False
+    init_lock: threading.Lock = field(default_factory=threading.Lock)
+
+
+class Worker:
+    """One BytePS worker (its root device) talking to the server front end."""
+
+    def __init__(self, rank: int, frontend: ServerFrontend,
+                 partition_bytes: int = DEFAULT_PARTITION_BYTES, local_size: int = 1):
+        self.rank = rank
+        self.frontend = frontend
+        self.bound = partition_bound(partition_bytes, local_size)
+        if self.bound <= 0:
+            raise ValueError("partition bound must be positive")
+        self.contexts: dict[str, Context] = {}
+        self._declared: list[str] = []
+
+    # ------------------------------------------------------------ declare/init
+    def declare(self, name: str) -> int:
+        """Register a tensor; its position is its declared key."""
+        if name not in self.contexts:
+            self.contexts[name] = Context(name, len(self._declared))
+            self._declared.append(name)
+        return self.contexts[name].declared_key
+
+    def _partition(self, size: int):
+        """PartitionTensor (operations.cc:99-136): [offset, len) under the bound."""
+        out, acc = [], 0
+        while acc < size:
+            ln = min(self.bound, size - acc)
+            out.append((acc, ln))
+            acc += ln
+        return out
+
+    def init_tensor(self, name: str, data, dtype: int) -> Context:
+        """InitTensor (operations.cc:219-316): keys, then one blocking init push
+        per partition (every worker's init push of a key returns only once all
+        of them arrived: the global barrier)."""
+        self.declare(name)
+        ctx = self.contexts[name]
+        size = _nbytes(data)
+        with ctx.init_lock:
+            if ctx.initialized:
+                return ctx
+            if size <= 0:
+                raise ValueError("init tensor size not larger than 0")      # operations.cc:229
+            ctx.size, ctx.dtype = size, int(dtype)
+            start = ctx.declared_key << 16
+            ctx.parts = [(start + i, off, ln) for i, (off, ln) in enumerate(self._partition(size))]
+            ctx.key_list = [k for k, _, _ in ctx.parts]
+            assert len(ctx.key_list) == (size + self.bound - 1) // self.bound   # :257-259
+            cmd = cantor_command(K_DEFAULT_PUSH_PULL, ctx.dtype)
+            for key, off, ln in ctx.parts:
+                self.frontend.push(cmd, key, self.rank, _slice(data, off, ln), ln)
+            ctx.initialized = True
+        return ctx
+
+    # ---------------------------------------------------------------- push_pull
+    def push_pull(self, name: str, tensor, output=None, order=None) -> None:
+        """EnqueueTensor + the PUSH/PULL stages for one tensor: push every
+        partition (in ``order`` — a list of partition indices — if given), then
+        pull every partition into ``output`` (default: ``tensor`` itself, in
+        place, as byteps_push_pull does)."""
+        ctx = self.contexts[name]
+        if not ctx.initialized:
+            raise RuntimeError(f"{name}: init_tensor first")
+        if _nbytes(tensor) != ctx.size:
+            raise ValueError(f"{name}: {_nbytes(tensor)} bytes, declared {ctx.size}")
+        out = tensor if output is None else output
+        if _nbytes(out) != ctx.size:
+            raise ValueError(f"{name}: output tensor size does not match")   # operations.cc:151
+        cmd = cantor_command(K_DEFAULT_PUSH_PULL, ctx.dtype)
+        idx = range(len(ctx.parts)) if order is None else order
+        for i in idx:
+            key, off, ln = ctx.parts[i]
+            self.frontend.push(cmd, key, self.rank, _slice(tensor, off, ln), ln)
+        for key, off, ln in ctx.parts:
+            self.frontend.pull(key, _slice(out, off, ln), ln)
+
+    def push_pull_iteration(self, tensors: dict, scheduler=None) -> list:
+        """One training iteration: every declared tensor, gradients arriving in
+        backward order (highest declared index first).  With a Prophet
+        ``scheduler`` (``ProphetPushQueue``) the partitions are pushed in the
+        groups it releases; then every partition is pulled back in place.
+        Returns the release groups as lists of (declared key, partition)."""
+        from .prophet import PushTask, release_groups
+        ctxs = [self.contexts[n] for n in self._declared if n in tensors]
+        arrivals = []
+        for c in sorted(ctxs, key=lambda c: -c.declared_key):
+            for i, (key, off, ln) in enumerate(c.parts):
+                arrivals.append(PushTask(c.declared_key, i, ln, len(c.parts), key))
+        if scheduler is None:
+            groups = [arrivals]
+        else:
+            scheduler.reset()
+            groups = release_groups(scheduler, arrivals)
+        by_key = {c.declared_key: c for c in ctxs}
+        for g in groups:
+            for t in g:
+                c = by_key[t.grad]
+                key, off, ln = c.parts[t.part]
+                self.frontend.push(cantor_command(K_DEFAULT_PUSH_PULL, c.dtype), key, self.rank,
+                                   _slice(tensors[c.name], off, ln), ln)
+        for c in ctxs:
+            for key, off, ln in c.parts:
+                self.frontend.pull(key, _slice(tensors[c.name], off, ln), ln)
+        return [[(t.grad, t.part) for t in g] for g in groups]
+
+
+def _nbytes(x) -> int:
+    if hasattr(x, "nbytes") and not hasattr(x, "data_ptr"):
+        return int(x.nbytes)                               # numpy
+    return int(x.numel() * x.element_size())               # torch
+
+
+def _slice(x, off: int, ln: int):
+    """Byte range [off, off+ln) of a contiguous buffer, as a view of the same
+    kind (pulls write through it, so a copy would lose the result)."""
+    if hasattr(x, "data_ptr"):                             # torch
+        import torch
+        if not x.is_contiguous():
+            raise ValueError("push_pull needs contiguous tensors")
+        return x.reshape(-1).view(torch.uint8)[off:off + ln]
+    import numpy as np
+    if not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("push_pull needs contiguous arrays")
+    return x.reshape(-1).view(np.uint8)[off:off + ln]
+
+
+__all__ = ["ServerFrontend", "Worker", "Context", "K_DEFAULT_PUSH_PULL", "DType", "elem_size"]
