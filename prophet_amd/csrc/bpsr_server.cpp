@@ -554,10 +554,14 @@ void* device_view(void* out, int location) {
   return nullptr;
 }
 
+// Copying pulls: hipMemcpyAsync (SDMA) by default — measured 2-6 % faster
+// than the copy kernel for blocking pulls and equal behind non-blocking
+// pushes (profiles/r02_cfg1_*); BPSR_SERVER_PULL_COPY=kernel writes device or
+// pinned destinations with the library's copy kernel instead.
 bool pull_by_kernel() {
   static const bool on = [] {
     const char* v = getenv("BPSR_SERVER_PULL_COPY");
-    return !(v && std::string(v) == "memcpy");
+    return v && std::string(v) == "kernel";
   }();
   return on;
 }
@@ -616,18 +620,20 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   s->acc_load.assign(cfg->engine_lanes, 0);
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  (void)prio_lo;
   const char* pv = getenv("BPSR_SERVER_D2H_PRIORITY");
-  const int d2h_prio = (pv && std::string(pv) == "normal") ? prio_lo : prio_hi;
+  const bool d2h_high = pv && std::string(pv) == "high";
   for (int i = 0; i < cfg->engine_lanes; ++i) {
     s->lanes.push_back(std::make_unique<Lane>());
     Lane& L = *s->lanes.back();
     hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
-    // d2h streams (mirror copies, copying pulls) at the highest priority: a
-    // hardware queue of their own, so a pull's copy never waits behind another
-    // lane's fold that is still waiting for its H2D pushes (HIP multiplexes a
-    // process's streams onto a few in-order hardware queues).
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&L.d2h, hipStreamNonBlocking, d2h_prio);
+    // d2h streams (mirror copies, copying pulls): normal priority by default;
+    // BPSR_SERVER_D2H_PRIORITY=high puts them on a hardware queue of their own
+    // (measured: no gain for copying pulls).
+    if (e == hipSuccess)
+      e = d2h_high ? hipStreamCreateWithPriority(&L.d2h, hipStreamNonBlocking, prio_hi)
+                   : hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
     if (e == hipSuccess && s->schedule)
       e = hipEventCreateWithFlags(&L.job_done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -803,9 +809,8 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
   if (ks->error) return key_error(ks);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
-  // queued under the key lock.  Device or pinned destinations are written by
-  // the library's copy kernel (the store mirror's path, link rate whatever is
-  // queued beside it); pageable ones by hipMemcpyAsync.  No per-thread
+  // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
+  // pull_by_kernel).  No per-thread
   // streams: a transport's pull threads come and go, and a stream per thread
   // (round 1) cost a stream creation per new thread and multiplied the
   // streams sharing the process's few hardware queues.
