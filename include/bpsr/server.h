@@ -138,6 +138,23 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
                            int* last_order, int max_order);
 
+/* Batched calls for a transport that delivers many keys at once (co-located
+ * workers, an in-process transport; ps-lite sends one key per request,
+ * server.cc:153).  Each is equivalent to n single calls in array order, the
+ * same worker for every key, except that the work is issued per engine lane
+ * in one launch: the device copies of push_many (device sources), the folds
+ * of every round the call completes (fused policy), and the device copies of
+ * pull_many.  A call never blocks while holding rounds it completed: it issues
+ * them first.  Host sources / destinations are copied per key.
+ *   push_ready_many  byteps_server_push_ready for keys[0..n)
+ *   push_many        byteps_server_push (blocking) for keys[i] with datas[i], lens[i]
+ *   pull_many        byteps_server_pull into outs[i] (lens[i] bytes)           */
+int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n, int worker);
+int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* const* datas,
+                            const size_t* lens, int n, int worker, int dtype, int location);
+int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const* outs,
+                            const size_t* lens, int n, int location);
+
 /* Debug/test hook for scheduling (enable_schedule only): pause > 0 holds the
  * lane's engine queue (nothing is issued; pushes still queue), 0 releases it,
  * < 0 leaves it; the keys of the jobs the lane issued so far, in issue order,

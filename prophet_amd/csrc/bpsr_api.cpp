@@ -179,6 +179,7 @@ constexpr int kRing = 8;
 struct StageRing {
   StageSlot slots[kRing];
   int next = 0;
+  std::vector<char> table;  // host copy of the table being built
   ~StageRing() {
     for (auto& s : slots) {
       if (s.pending && s.done) (void)hipEventSynchronize(s.done);
@@ -190,12 +191,15 @@ struct StageRing {
 };
 static thread_local StageRing g_ring;
 
-static int stage_acquire(size_t bytes, StageSlot** out) {
+StageRing* stage_ring_create() { return new StageRing(); }
+void stage_ring_destroy(StageRing* r) { delete r; }
+
+static int stage_acquire(StageRing& ring, size_t bytes, StageSlot** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
-  StageSlot& s = g_ring.slots[g_ring.next];
-  g_ring.next = (g_ring.next + 1) % kRing;
+  StageSlot& s = ring.slots[ring.next];
+  ring.next = (ring.next + 1) % kRing;
   if (s.pending) {
     e = hipEventSynchronize(s.done);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(stage)");
@@ -363,7 +367,29 @@ static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti) {
   return L;
 }
 
-static thread_local std::vector<char> g_table;
+
+int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype, int mode,
+                      hipStream_t s, StageRing* ring) {
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (nbuckets < 0 || (nbuckets > 0 && !buckets))
+    return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
+  if (nbuckets == 0) return BYTEPS_REDUCE_OK;
+  TableInfo ti;
+  if ((rc = build_table(buckets, nbuckets, dtype, ring->table, &ti))) return rc;
+  if (ti.tiles == 0) return BYTEPS_REDUCE_OK;
+  StageSlot* slot = nullptr;
+  if ((rc = stage_acquire(*ring, ti.bytes, &slot))) return rc;
+  std::memcpy(slot->host, ring->table.data(), ti.bytes);
+  hipError_t e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
+  e = launch_batched(batch_launch(slot->dev, ti), ti.vpt, dtype, mode, tuning_for_n(ti.nmax), s);
+  if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
+  e = hipEventRecord(slot->done, s);
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
+  slot->pending = true;
+  return BYTEPS_REDUCE_OK;
+}
 
 }  // namespace bpsr
 
@@ -479,26 +505,9 @@ int byteps_reduce_sum_n(void* dst, const void* const* srcs, int n, size_t len, i
 
 int byteps_reduce_sum_batched(const byteps_bucket_desc* buckets, int nbuckets, int dtype,
                               int mode, void* stream) {
-  int rc = check_common(dtype, mode);
-  if (rc) return rc;
-  if (nbuckets < 0 || (nbuckets > 0 && !buckets))
-    return fail(BYTEPS_REDUCE_EARGS, "bad bucket table");
-  if (nbuckets == 0) return BYTEPS_REDUCE_OK;
-  TableInfo ti;
-  if ((rc = build_table(buckets, nbuckets, dtype, g_table, &ti))) return rc;
-  if (ti.tiles == 0) return BYTEPS_REDUCE_OK;
-  StageSlot* slot = nullptr;
-  if ((rc = stage_acquire(ti.bytes, &slot))) return rc;
-  std::memcpy(slot->host, g_table.data(), ti.bytes);
-  hipStream_t s = to_stream(stream);
-  hipError_t e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
-  e = launch_batched(batch_launch(slot->dev, ti), ti.vpt, dtype, mode, tuning_for_n(ti.nmax), s);
-  if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
-  e = hipEventRecord(slot->done, s);
-  if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
-  slot->pending = true;
-  return BYTEPS_REDUCE_OK;
+  // the calling thread's staging ring (pinned table + device copy, reused
+  // once the kernel that read a slot has completed)
+  return batched_with_ring(buckets, nbuckets, dtype, mode, to_stream(stream), &g_ring);
 }
 
 struct byteps_reduce_plan {

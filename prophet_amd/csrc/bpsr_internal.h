@@ -153,6 +153,17 @@ hipError_t allow_lds(KernelAttr& once, const void* kernel, int bytes = (int)kLds
 
 int elem_size(int dtype);  // 0 if unsupported
 
+// Staging for batched launches: a ring of pinned host + device descriptor
+// tables, each reused once the kernel that read it completed.  The public
+// byteps_reduce_sum_batched uses one per calling thread; the PS server owns
+// one per engine lane (transport threads come and go).  Not thread-safe: one
+// user at a time.
+struct StageRing;
+StageRing* stage_ring_create();
+void stage_ring_destroy(StageRing* r);
+int batched_with_ring(const struct byteps_bucket_desc* buckets, int nbuckets, int dtype,
+                      int mode, hipStream_t s, StageRing* ring);
+
 // Thread-local error reporting shared by every C-ABI entry point
 // (byteps_reduce_last_error): returns `code`.
 int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));

@@ -28,6 +28,9 @@ namespace {
 constexpr size_t kSlotAlign = 4096;
 constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots
 constexpr int kMaxDebugLog = 4096;
+// pull_many issues the copies of the rounds found finished once this many
+// bytes are ready and it must wait for another round (else at the end)
+constexpr size_t kPullFlushBytes = 8u << 20;
 
 struct KeyState;
 
@@ -53,6 +56,15 @@ struct Lane {
   hipEvent_t job_done = nullptr;
   std::mutex dbg_mu;
   std::vector<uint64_t> log;  // keys of dispatched jobs, in dispatch order
+  // batched calls (push_many / push_ready_many / pull_many): one batched
+  // launch per lane for many keys, staged through the lane's own ring
+  std::mutex batch_mu;
+  StageRing* ring = nullptr;
+  // Lane-wide marks: the latest work issued on each stream (a later record on
+  // an in-order stream covers every earlier one).  Folds wait for copy_mark
+  // (every push copy of the lane so far); batched calls wait for fold_mark /
+  // d2h_mark once per lane instead of one event per key.
+  hipEvent_t copy_mark = nullptr, fold_mark = nullptr, d2h_mark = nullptr;
 };
 
 // A pull ready to be answered, or a push to acknowledge, by the responder.
@@ -94,7 +106,11 @@ struct KeyState {
   bool push_finished = false;
   int pull_cnt = 0;
   std::vector<int> last_order;
-  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after the last issued fold
+  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after a single fold
+  // What to wait for to see the key's last issued fold complete: `done`, or —
+  // after a batched issue (flush_folds), which records no per-key event — the
+  // lane's fold mark (a later record of it covers this fold too).
+  hipEvent_t fold_ev = nullptr;
   hipEvent_t copied = nullptr;
   hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
   bool has_done = false;
@@ -225,12 +241,13 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
             bool wait = true) {
   Lane& L = *s->lanes[ks->lane];
   hipError_t e = hipSuccess;
-  if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->done, 0);
+  if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ks->slot[w], data, len,
                        loc == BYTEPS_SERVER_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
                        L.copy);
   if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
+  if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
   if (e == hipSuccess && wait) e = hipEventSynchronize(ks->copied);
   return e == hipSuccess ? 0 : hip_fail(e, "push copy");
 }
@@ -240,7 +257,7 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
 // the copy overlaps the H2D pushes of the lane's other keys (PCIe is full duplex).
 int queue_mirror(byteps_server* s, KeyState* ks, size_t idx) {
   Lane& L = *s->lanes[ks->lane];
-  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->fold_ev, 0) : hipSuccess;
   if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
   // The copy kernel writes the pinned mirror straight over PCIe.  A
   // hipMemcpyAsync D2H queued behind a pending event wait was handed to an SDMA
@@ -368,11 +385,19 @@ void responder_main(byteps_server* s) {
   }
 }
 
-// A round's fold is issued: publish it (caller holds ks->mu).
-int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order) {
+// A round's fold is issued: publish it (caller holds ks->mu).  `mark`: also
+// raise the lane's fold mark (a batched issue raises it once, before).
+int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
+                 bool mark = true) {
   Lane& L = *s->lanes[ks->lane];
-  hipError_t e = hipEventRecord(ks->done, L.fold);
-  if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+  if (mark) {  // a single fold: its own event, and the lane's mark
+    hipError_t e = hipEventRecord(ks->done, L.fold);
+    if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
+    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    ks->fold_ev = ks->done;
+  } else {     // batched: the mark raised behind the batch stands for it
+    ks->fold_ev = L.fold_mark;
+  }
   ks->has_done = true;
   int rc = 0;
   if (!ks->mirror.empty() && (rc = queue_mirror(s, ks, (ks->rounds + 1) & 1))) return rc;
@@ -395,10 +420,11 @@ int execute(byteps_server* s, const FoldJob& j) {
   KeyState* ks = j.ks;
   Lane& L = *s->lanes[ks->lane];
   void* fs = reinterpret_cast<void*>(L.fold);
-  // Folds run behind the slots' H2D copies (byteps_server_push_async returns
-  // before they finish; the copy stream is in order, so the last recorded copy
-  // covers every earlier one) and behind the last mirror D2H of the store.
-  hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
+  // Folds run behind the slots' copies (byteps_server_push_async returns
+  // before they finish; the copy stream is in order, so the lane's copy mark
+  // covers every copy issued so far, batched ones included) and behind the
+  // last mirror D2H of the store.
+  hipError_t we = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
   if (we == hipSuccess && ks->mirrored) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
   if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
   int rc = 0;
@@ -409,7 +435,9 @@ int execute(byteps_server* s, const FoldJob& j) {
       rc = byteps_reduce_sum(ks->store, ks->slot[j.w], ks->len, ks->dtype, fs);
       if (rc) return rc;
       hipError_t e = hipEventRecord(ks->done, L.fold);
+      if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
       if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+      ks->fold_ev = ks->done;
       ks->has_done = true;
       ks->rounds++;
       ks->cv.notify_all();
@@ -471,7 +499,10 @@ void dispatcher_main(byteps_server* s, int lane) {
 }
 
 // A push's bytes are in slot w: advance the state machine (caller holds ks->mu).
-int arrive(byteps_server* s, KeyState* ks, int w) {
+// With `defer` (a batched call, no scheduling), a round's fused fold is not
+// issued here but handed back, to go out with the call's other keys in one
+// batched launch per lane (flush_folds); the key counts it as pending.
+int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = nullptr) {
   if (ks->error) return key_error(ks);
   const int N = s->cfg.num_workers;
   Lane& L = *s->lanes[ks->lane];
@@ -481,12 +512,14 @@ int arrive(byteps_server* s, KeyState* ks, int w) {
     if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d sent two init pushes", w);
     ks->got[w] = 1;
     if (++ks->init_count < N) return 0;
-    hipError_t we = hipStreamWaitEvent(L.fold, ks->copied, 0);
+    hipError_t we = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
     if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
     int rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, reinterpret_cast<void*>(L.fold));
     if (rc) return rc;
     hipError_t e = hipEventRecord(ks->done, L.fold);
+    if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    ks->fold_ev = ks->done;
     ks->has_done = true;
     ks->inited = true;
     std::fill(ks->got.begin(), ks->got.end(), 0);
@@ -529,9 +562,70 @@ int arrive(byteps_server* s, KeyState* ks, int w) {
   j.order = ks->order;
   ks->order.clear();
   ks->arrived = 0;
+  if (defer && !q && j.kind == kFinishFused && N <= kMaxSrcs) {
+    ks->pending++;
+    defer->push_back(std::move(j));
+    return 0;
+  }
   const int rc = submit(s, ks, std::move(j));
   if (q) q->clear_counter(ks->key);  // server.cc:269-271
   return rc;
+}
+
+// Issue deferred fused folds: per (lane, dtype) ONE batched launch whose
+// buckets are the keys' rounds (dst = store, sources = slots in arrival order),
+// then each key's round is published.  Returns the first error.
+int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
+  if (jobs.empty()) return 0;
+  std::stable_sort(jobs.begin(), jobs.end(), [](const FoldJob& a, const FoldJob& b) {
+    return a.ks->lane != b.ks->lane ? a.ks->lane < b.ks->lane : a.ks->dtype < b.ks->dtype;
+  });
+  int first_rc = 0;
+  size_t i = 0;
+  while (i < jobs.size()) {
+    size_t e = i + 1;
+    while (e < jobs.size() && jobs[e].ks->lane == jobs[i].ks->lane &&
+           jobs[e].ks->dtype == jobs[i].ks->dtype)
+      ++e;
+    Lane& L = *s->lanes[jobs[i].ks->lane];
+    std::lock_guard<std::mutex> bg(L.batch_mu);
+    std::vector<byteps_bucket_desc> d(e - i);
+    hipError_t we0 = hipStreamWaitEvent(L.fold, L.copy_mark, 0);  // every copy of the lane
+    int rc = we0 == hipSuccess ? 0 : hip_fail(we0, "hipStreamWaitEvent");
+    for (size_t k = i; k < e; ++k) {
+      KeyState* ks = jobs[k].ks;
+      std::lock_guard<std::mutex> g(ks->mu);
+      if (ks->mirrored) {
+        hipError_t we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
+        if (we != hipSuccess && !rc) rc = hip_fail(we, "hipStreamWaitEvent");
+      }
+      byteps_bucket_desc& b = d[k - i];
+      std::memset(&b, 0, sizeof(b));
+      b.dst = ks->store;
+      for (size_t m = 0; m < jobs[k].order.size(); ++m) b.srcs[m] = ks->slot[jobs[k].order[m]];
+      b.len = ks->len;
+      b.n = (int)jobs[k].order.size();
+    }
+    if (!rc)
+      rc = batched_with_ring(d.data(), (int)d.size(), jobs[i].ks->dtype,
+                             BYTEPS_REDUCE_MODE_REFERENCE, L.fold, L.ring);
+    if (!rc) {  // raised before any round is published: a pull that sees one waits past it
+      hipError_t me = hipEventRecord(L.fold_mark, L.fold);
+      if (me != hipSuccess) rc = hip_fail(me, "hipEventRecord");
+    }
+    for (size_t k = i; k < e; ++k) {
+      KeyState* ks = jobs[k].ks;
+      std::lock_guard<std::mutex> g(ks->mu);
+      ks->pending--;
+      const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false);
+      if (r2) fail_key(s, ks, r2);
+      ks->cv.notify_all();
+    }
+    if (rc && !first_rc) first_rc = rc;
+    i = e;
+  }
+  jobs.clear();
+  return first_rc;
 }
 
 // Init pushes block until every worker's init push has arrived and the store
@@ -641,6 +735,18 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
       return hip_fail(e, "hipStreamCreate");
     }
     if (s->schedule) L.q = std::make_unique<EngineQueue<FoldJob>>(true);
+    L.ring = stage_ring_create();
+    for (hipEvent_t* m : {&L.copy_mark, &L.fold_mark, &L.d2h_mark})
+      if (e == hipSuccess) e = hipEventCreateWithFlags(m, hipEventDisableTiming);
+    // recorded once on their (empty) streams: waiting on them is a no-op until
+    // the lane issues work
+    if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
+    if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
+    if (e == hipSuccess) e = hipEventRecord(L.d2h_mark, L.d2h);
+    if (e != hipSuccess) {
+      byteps_server_destroy(s.release());
+      return hip_fail(e, "lane events");
+    }
   }
   try {
     if (s->schedule)
@@ -698,6 +804,9 @@ int byteps_server_destroy(byteps_server* s) {
     if (Lp->copy) (void)hipStreamDestroy(Lp->copy);
     if (Lp->d2h) (void)hipStreamDestroy(Lp->d2h);
     if (Lp->job_done) (void)hipEventDestroy(Lp->job_done);
+    if (Lp->ring) stage_ring_destroy(Lp->ring);
+    for (hipEvent_t m : {Lp->copy_mark, Lp->fold_mark, Lp->d2h_mark})
+      if (m) (void)hipEventDestroy(m);
   }
   delete s;
   return BYTEPS_REDUCE_OK;
@@ -778,7 +887,7 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
   ks->cv.wait(lk, [&] { return ks->pending == 0 || ks->error; });  // every fold issued
   if (ks->error) return key_error(ks);
   if (ks->has_done) {  // the slot may be read by the last issued fold
-    hipError_t e = hipEventSynchronize(ks->done);
+    hipError_t e = hipEventSynchronize(ks->fold_ev);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   }
   *slot = ks->slot[worker];
@@ -815,7 +924,7 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   // (round 1) cost a stream creation per new thread and multiplied the
   // streams sharing the process's few hardware queues.
   Lane& L = *s->lanes[ks->lane];
-  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->done, 0) : hipSuccess;
+  hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->fold_ev, 0) : hipSuccess;
   if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
   void* dv = pull_by_kernel() ? device_view(out, location) : nullptr;
   if (dv) {
@@ -910,6 +1019,234 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
     for (int i = 0; i < max_order && i < (int)ks->last_order.size(); ++i)
       last_order[i] = ks->last_order[i];
   return ks->error ? key_error(ks) : BYTEPS_REDUCE_OK;
+}
+
+// ------------------------------------------------------- batched calls --
+
+int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n, int worker) {
+  if (!s || (n > 0 && !keys) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  int rc = set_device(s);
+  if (rc) return rc;
+  std::vector<FoldJob> defer;
+  for (int i = 0; i < n; ++i) {
+    KeyState* ks = get_key(s, keys[i], false);
+    if (!ks || !ks->allocated) {
+      (void)flush_folds(s, defer);
+      return fail(BYTEPS_REDUCE_EARGS, "key %llu not initialised", (unsigned long long)keys[i]);
+    }
+    std::unique_lock<std::mutex> lk(ks->mu);
+    if (!can_push(s, ks, worker)) {
+      // never block while holding deferred rounds: others may wait on them
+      lk.unlock();
+      if ((rc = flush_folds(s, defer))) return rc;
+      lk.lock();
+      ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
+    }
+    if (ks->error) {
+      lk.unlock();
+      (void)flush_folds(s, defer);
+      return key_error(ks);
+    }
+    const bool init_round = !ks->inited;
+    if ((rc = arrive(s, ks, worker, &defer))) {
+      lk.unlock();
+      (void)flush_folds(s, defer);
+      return rc;
+    }
+    if (init_round && !ks->inited) {
+      lk.unlock();
+      if ((rc = flush_folds(s, defer))) return rc;
+      lk.lock();
+      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
+      if (ks->error) return key_error(ks);
+    }
+  }
+  return flush_folds(s, defer);
+}
+
+int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* const* datas,
+                            const size_t* lens, int n, int worker, int dtype, int location) {
+  if (!s || n < 0 || (n > 0 && (!keys || !datas || !lens)))
+    return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (worker < 0 || worker >= s->cfg.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  int rc = set_device(s);
+  if (rc) return rc;
+  // 1. every slot free (its previous round folded), then the copies: per lane
+  //    ONE wait for the lane's folds so far, then one batched copy (device
+  //    sources) or a hipMemcpyAsync per key (host sources), then the lane's
+  //    copy mark, which every later fold of the lane waits for
+  std::vector<KeyState*> ks_of(n);
+  std::vector<std::vector<int>> by_lane(s->lanes.size());
+  for (int i = 0; i < n; ++i) {
+    if (!datas[i]) return fail(BYTEPS_REDUCE_EARGS, "null data for key %d", i);
+    KeyState* ks = get_key(s, keys[i], true);
+    ks_of[i] = ks;
+    std::unique_lock<std::mutex> lk(ks->mu);
+    if ((rc = allocate(s, ks, lens[i], dtype))) return rc;
+    ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
+    if (ks->error) return key_error(ks);
+    by_lane[ks->lane].push_back(i);
+  }
+  for (size_t l = 0; l < by_lane.size(); ++l) {
+    if (by_lane[l].empty()) continue;
+    Lane& L = *s->lanes[l];
+    std::lock_guard<std::mutex> bg(L.batch_mu);
+    hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    if (location == BYTEPS_SERVER_HOST) {
+      for (int i : by_lane[l]) {
+        e = hipMemcpyAsync(ks_of[i]->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice,
+                           L.copy);
+        if (e != hipSuccess) return hip_fail(e, "push copy");
+      }
+    } else {
+      std::vector<byteps_bucket_desc> d(by_lane[l].size());
+      for (size_t k = 0; k < by_lane[l].size(); ++k) {
+        const int i = by_lane[l][k];
+        std::memset(&d[k], 0, sizeof(d[k]));
+        d[k].dst = ks_of[i]->slot[worker];
+        d[k].srcs[0] = datas[i];
+        d[k].len = lens[i];
+        d[k].n = 1;
+      }
+      if ((rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
+                                  BYTEPS_REDUCE_MODE_REFERENCE, L.copy, L.ring)))
+        return rc;
+    }
+    if ((e = hipEventRecord(L.copy_mark, L.copy)) != hipSuccess)
+      return hip_fail(e, "hipEventRecord");
+  }
+  // 2. arrivals, with the rounds they complete folded per lane in one launch
+  std::vector<FoldJob> defer;
+  for (int i = 0; i < n; ++i) {
+    KeyState* ks = ks_of[i];
+    std::unique_lock<std::mutex> lk(ks->mu);
+    const bool init_round = !ks->inited;
+    if ((rc = arrive(s, ks, worker, &defer))) {
+      lk.unlock();
+      (void)flush_folds(s, defer);
+      return rc;
+    }
+    if (init_round && !ks->inited) {
+      lk.unlock();
+      if ((rc = flush_folds(s, defer))) return rc;
+      lk.lock();
+      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
+      if (ks->error) return key_error(ks);
+    }
+  }
+  if ((rc = flush_folds(s, defer))) return rc;
+  // 3. blocking contract: every source may be reused once the call returns
+  //    (a lane's copy mark, re-recorded since, covers this call's copies too)
+  for (size_t l = 0; l < by_lane.size(); ++l) {
+    if (by_lane[l].empty()) continue;
+    hipError_t e = hipEventSynchronize(s->lanes[l]->copy_mark);
+    if (e != hipSuccess) return hip_fail(e, "push copy");
+  }
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const* outs,
+                            const size_t* lens, int n, int location) {
+  if (!s || n < 0 || (n > 0 && (!keys || !outs || !lens)))
+    return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  if (s->cfg.async_mode) {
+    // every fold changes the store: each pull keeps the single call's
+    // ordering (copy queued under the key lock, later folds wait for it)
+    for (int i = 0; i < n; ++i)
+      if ((rc = byteps_server_pull(s, keys[i], outs[i], lens[i], location))) return rc;
+    return BYTEPS_REDUCE_OK;
+  }
+  std::vector<KeyState*> ks_of(n, nullptr);
+  std::vector<std::vector<int>> ready(s->lanes.size());  // rounds finished, copies not issued
+  std::vector<char> touched(s->lanes.size(), 0);
+  size_t ready_bytes = 0;
+  // Issue the copies of the keys found ready: per lane ONE wait for the lane's
+  // folds so far (they include every ready key's round: a round is published
+  // after its fold was issued and the mark raised), one batched copy (device
+  // destinations) or a hipMemcpyAsync per key (host), then the d2h mark.
+  auto flush = [&]() -> int {
+    for (size_t l = 0; l < ready.size(); ++l) {
+      if (ready[l].empty()) continue;
+      Lane& L = *s->lanes[l];
+      std::lock_guard<std::mutex> bg(L.batch_mu);
+      hipError_t e = hipStreamWaitEvent(L.d2h, L.fold_mark, 0);
+      if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+      if (location == BYTEPS_SERVER_HOST) {
+        for (int i : ready[l]) {
+          e = hipMemcpyAsync(outs[i], ks_of[i]->store, lens[i], hipMemcpyDeviceToHost, L.d2h);
+          if (e != hipSuccess) return hip_fail(e, "pull copy");
+        }
+      } else {
+        std::vector<byteps_bucket_desc> d(ready[l].size());
+        for (size_t k = 0; k < ready[l].size(); ++k) {
+          const int i = ready[l][k];
+          std::memset(&d[k], 0, sizeof(d[k]));
+          d[k].dst = outs[i];
+          d[k].srcs[0] = ks_of[i]->store;
+          d[k].len = lens[i];
+          d[k].n = 1;
+        }
+        int r = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
+                                  BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring);
+        if (r) return r;
+      }
+      if ((e = hipEventRecord(L.d2h_mark, L.d2h)) != hipSuccess)
+        return hip_fail(e, "hipEventRecord");
+      touched[l] = 1;
+      ready[l].clear();
+    }
+    return 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    KeyState* ks = key_for_pull(s, keys[i]);
+    if (!ks) {
+      (void)flush();
+      return BYTEPS_REDUCE_EARGS;
+    }
+    ks_of[i] = ks;
+    std::unique_lock<std::mutex> lk(ks->mu);
+    if (lens[i] > ks->len || !outs[i]) {
+      lk.unlock();
+      (void)flush();
+      return fail(BYTEPS_REDUCE_EARGS, "pull %d: bad buffer or %zu bytes > key len %zu", i,
+                  lens[i], ks->len);
+    }
+    if (!(ks->push_finished || ks->error)) {
+      lk.unlock();
+      // let enough ready bytes go while this round finishes; fewer, larger
+      // batched copies otherwise (rounds often complete together)
+      if (ready_bytes >= kPullFlushBytes) {
+        if ((rc = flush())) return rc;
+        ready_bytes = 0;
+      }
+      lk.lock();
+      ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+    }
+    if (ks->error) {
+      lk.unlock();
+      (void)flush();
+      return key_error(ks);
+    }
+    ready[ks->lane].push_back(i);
+    ready_bytes += lens[i];
+  }
+  if ((rc = flush())) return rc;
+  for (size_t l = 0; l < touched.size(); ++l) {  // a later record covers this call's copies too
+    if (!touched[l]) continue;
+    hipError_t e = hipEventSynchronize(s->lanes[l]->d2h_mark);
+    if (e != hipSuccess) return hip_fail(e, "pull copy");
+  }
+  for (int i = 0; i < n; ++i) {
+    std::lock_guard<std::mutex> g(ks_of[i]->mu);
+    count_pull(s, ks_of[i]);  // server.cc:105-113
+  }
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* log_keys,

@@ -22,7 +22,8 @@ SERVER_EXPORTS = (
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
-    "byteps_server_debug_lane",
+    "byteps_server_debug_lane", "byteps_server_push_ready_many", "byteps_server_push_many",
+    "byteps_server_pull_many",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -57,6 +58,11 @@ def _lib():
                                              ctypes.POINTER(_int), ctypes.POINTER(_int), _int]
         L.byteps_server_debug_lane.argtypes = [_vp, _int, _int, ctypes.POINTER(_u64), _int,
                                                ctypes.POINTER(_int)]
+        L.byteps_server_push_ready_many.argtypes = [_vp, ctypes.POINTER(_u64), _int, _int]
+        L.byteps_server_push_many.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_vp),
+                                              ctypes.POINTER(_sz), _int, _int, _int, _int]
+        L.byteps_server_pull_many.argtypes = [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_vp),
+                                              ctypes.POINTER(_sz), _int, _int]
         L._server_bound = True
     return L
 
@@ -173,6 +179,31 @@ class PSServer:
         _check(self.lib.byteps_server_key_info(self.handle, key, ctypes.byref(rounds),
                                                ctypes.byref(lane), order, self.cfg.num_workers))
         return int(rounds.value), int(lane.value), list(order)
+
+    # batched calls (server.h): one lane-wide launch for many keys
+    def push_ready_many(self, keys, worker: int) -> None:
+        arr = (_u64 * len(keys))(*keys)
+        _check(self.lib.byteps_server_push_ready_many(self.handle, arr, len(keys), worker))
+
+    def push_many(self, keys, worker: int, datas, dtype: int) -> None:
+        bufs = [_buf(d) for d in datas]
+        locs = {loc for _, _, loc in bufs}
+        if len(locs) > 1:
+            raise ValueError("push_many: all sources host, or all device")
+        n = len(keys)
+        _check(self.lib.byteps_server_push_many(
+            self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
+            (_sz * n)(*[b for _, b, _ in bufs]), n, worker, int(dtype), locs.pop() if n else 0))
+
+    def pull_many(self, keys, outs) -> None:
+        bufs = [_buf(o) for o in outs]
+        locs = {loc for _, _, loc in bufs}
+        if len(locs) > 1:
+            raise ValueError("pull_many: all destinations host, or all device")
+        n = len(keys)
+        _check(self.lib.byteps_server_pull_many(
+            self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
+            (_sz * n)(*[b for _, b, _ in bufs]), n, locs.pop() if n else 0))
 
     def debug_lane(self, lane: int, pause: int = -1, max_log: int = 4096) -> list[int]:
         """Scheduling test hook (byteps_server_debug_lane): pause (1) / release

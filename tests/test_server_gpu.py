@@ -681,3 +681,99 @@ def test_cfg1_two_workers_64mib(port, policy, layout):
         for w in range(N):
             assert np.array_equal(outs[(w, r)], want), (r, w)
     srv.close()
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+@pytest.mark.parametrize("dt", [DType.FLOAT16, DType.FLOAT32], ids=lambda d: DType(d).name)
+def test_batched_calls_many_keys(port, policy, dt):
+    """push_many / push_ready_many / pull_many (server.h batched calls): 6
+    worker threads x 40 keys of mixed sizes on 3 lanes, device-resident, three
+    rounds (the first from host buffers through push_many's per-key path);
+    every pulled byte equals the oracle's fold in the recorded arrival order,
+    and the rounds complete in any interleaving of the workers' batches."""
+    from prophet_amd.server import PSServer
+    N, R = 6, 3
+    sizes = [1 + (j * 7919) % 70_000 for j in range(40)]
+    es = elem_size(dt)
+    keys = list(range(100, 100 + len(sizes)))
+    srv = PSServer(N, engine_lanes=3, policy=policy)
+    dev = torch.device("cuda:0")
+    host = {(w, r, j): data(dt, n, w, r, j) for w in range(N) for r in range(R + 1)
+            for j, n in enumerate(sizes)}
+    outs = {(w, r): [torch.empty(n * es, dtype=torch.uint8, device=dev) for n in sizes]
+            for w in range(N) for r in range(1, R + 1)}
+    bar = threading.Barrier(N + 1)
+    errors, orders = [], {}
+
+    def worker(w):
+        try:
+            srv.push_many(keys, w, [host[(w, 0, j)] for j in range(len(sizes))], dt)   # init
+            for r in range(1, R + 1):
+                if r == 1:      # host sources, per-key copies
+                    srv.push_many(keys, w, [host[(w, r, j)] for j in range(len(sizes))], dt)
+                else:           # device slots written directly, then one ready call
+                    for j, k in enumerate(keys):
+                        slot = srv.recv_slot(k, w)
+                        _copy_to_ptr(slot, torch.from_numpy(host[(w, r, j)]).to(dev))
+                    srv.push_ready_many(keys, w)
+                srv.pull_many(keys, outs[(w, r)])
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for r in range(1, R + 1):
+        bar.wait(timeout=240)
+        for j, k in enumerate(keys):
+            rounds, _, order = srv.key_info(k)
+            assert rounds == r
+            orders[(r, j)] = order
+        bar.wait(timeout=120)
+    for t in ts:
+        t.join(timeout=60)
+    assert not errors, errors
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [host[(w, r, j)] for w in orders[(r, j)]], n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, outs[(w, r)][j].cpu().numpy(), want,
+                                   nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
+    srv.close()
+
+
+def _copy_to_ptr(ptr, src):
+    """Device copy of tensor `src` to raw device pointer `ptr` (the transport
+    writing into a receive slot)."""
+    from prophet_amd.reducer import GpuReducer
+    GpuReducer().copy(ptr, src, src.numel() * src.element_size())
+    torch.cuda.synchronize()
+
+
+def test_batched_calls_async_mode(port):
+    """Async mode through the batched calls: every push_many sums into the
+    store; pull_many answers at once with the store as it stands."""
+    from prophet_amd.server import PSServer
+    dt, N = DType.INT32, 3
+    sizes = [5, 40_000, 1_000_003]
+    keys = [7, 8, 9]
+    srv = PSServer(N, async_mode=True, engine_lanes=2)
+    dev = torch.device("cuda:0")
+    init = [torch.zeros(n, dtype=torch.int32, device=dev) for n in sizes]
+    ts = [threading.Thread(target=srv.push_many, args=(keys, w, init, dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    for w in range(N):
+        srv.push_many(keys, w, [torch.full((n,), w + 1, dtype=torch.int32, device=dev)
+                                for n in sizes], dt)
+    outs = [torch.empty(n, dtype=torch.int32, device=dev) for n in sizes]
+    srv.pull_many(keys, outs)
+    for o in outs:
+        assert (o == 6).all()
+    srv.close()

@@ -1,0 +1,221 @@
+// Config 3's key set through the GPU-resident PS server from native threads
+// (not product code): ResNet-50 fp16, 8 workers, the 165 BytePS partitions as
+// keys (tools/cfg3_resnet50_table.txt, Prophet block order), every push
+// device-resident.  Measures what a round of many small keys costs in the
+// server's state machine and launches, next to the block queue's one launch
+// per iteration (tools/cfg3_native.cpp).  One JSON line per variant:
+//   push_ready   the pushes already sit in the receive slots (an RDMA transport
+//                writing into HBM, byteps_server_recv_slot): each worker thread
+//                only signals arrival for its 165 keys;
+//   push_d2d     each worker thread pushes from its own device buffer
+//                (byteps_server_push_async, D2D copy into the slot);
+//   ..._many     the same through the batched calls (byteps_server_push_ready_many
+//                / push_many, then pull_many): one launch per lane per call.
+// Every round ends when every worker has pulled every key (device pulls).
+// Worker threads persist across rounds (a transport's receive threads).
+//   hipcc -O2 -std=c++17 -Iinclude -o tools/server_cfg3_native tools/server_cfg3_native.cpp \
+//         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd' -lpthread
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "bpsr/server.h"
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(2);                                                                  \
+    }                                                                           \
+  } while (0)
+#define CKR(x)                                                                           \
+  do {                                                                                   \
+    int r_ = (x);                                                                        \
+    if (r_ != 0) {                                                                       \
+      fprintf(stderr, "%s:%d rc=%d %s\n", __FILE__, __LINE__, r_, byteps_reduce_last_error()); \
+      exit(3);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+namespace {
+constexpr int N = 8;
+std::atomic<long> acks{0};
+void on_push(void*, uint64_t, int, int status) {
+  if (status) {
+    fprintf(stderr, "push ack status %d\n", status);
+    exit(4);
+  }
+  acks.fetch_add(1, std::memory_order_relaxed);
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  const char* path = argc > 1 ? argv[1] : "tools/cfg3_resnet50_table.txt";
+  const int rounds = argc > 2 ? atoi(argv[2]) : 20;
+  const int lanes = argc > 3 ? atoi(argv[3]) : 4;
+  const int only = argc > 4 ? atoi(argv[4]) : -1;  // run one variant (0..3), -1 all
+  FILE* f = fopen(path, "r");
+  if (!f) return 2;
+  size_t total = 0;
+  int np = 0, nb = 0;
+  if (fscanf(f, "%zu %d %d", &total, &np, &nb) != 3) return 2;
+  std::vector<std::pair<size_t, size_t>> parts(np);
+  for (auto& p : parts)
+    if (fscanf(f, "%zu %zu", &p.first, &p.second) != 2) return 2;
+  fclose(f);
+  // per worker: its gradient vector (device) and its pull destination (device)
+  std::vector<char*> grad(N), out(N);
+  std::vector<uint16_t> host(total / 2);
+  uint32_t x = 777u;
+  for (int k = 0; k < N; ++k) {
+    for (auto& h : host) {
+      x = x * 1664525u + 1013904223u;
+      h = (uint16_t)(((x >> 16) & 0x83ffu) | (((x >> 8) & 1u) ? 0x3800u : 0x3c00u));
+    }
+    CK(hipMalloc(&grad[k], total));
+    CK(hipMalloc(&out[k], total));
+    CK(hipMemcpy(grad[k], host.data(), total, hipMemcpyHostToDevice));
+  }
+  const double alg = (double)(N + 1) * (double)total;
+  const char* names[] = {"push_ready", "push_d2d", "push_ready_many+pull_many",
+                         "push_many_d2d+pull_many"};
+  std::vector<uint64_t> keys(np);
+  std::vector<size_t> lens(np);
+  for (int i = 0; i < np; ++i) {
+    keys[i] = (uint64_t)i;
+    lens[i] = parts[i].second;
+  }
+  for (int variant = 0; variant < 4; ++variant) {
+    if (only >= 0 && variant != only) continue;
+    const bool many = variant >= 2;
+    const bool ready = variant == 0 || variant == 2;
+    byteps_server_config cfg;
+    std::memset(&cfg, 0, sizeof(cfg));
+    cfg.num_workers = N;
+    cfg.engine_lanes = lanes;
+    cfg.policy = BYTEPS_SERVER_FUSED;
+    byteps_server* srv = nullptr;
+    CKR(byteps_server_create(&cfg, &srv));
+    // init round: blocking pushes from every worker thread, keys in order
+    {
+      std::vector<std::thread> th;
+      for (int k = 0; k < N; ++k)
+        th.emplace_back([&, k] {
+          for (int i = 0; i < np; ++i)
+            CKR(byteps_server_push(srv, (uint64_t)i, k, grad[k] + parts[i].first,
+                                   parts[i].second, BYTEPS_REDUCE_FLOAT16, BYTEPS_SERVER_DEVICE));
+        });
+      for (auto& t : th) t.join();
+    }
+    if (ready) {  // slots hold the pushes already (written once, as by DMA)
+      for (int k = 0; k < N; ++k)
+        for (int i = 0; i < np; ++i) {
+          void* slot = nullptr;
+          CKR(byteps_server_recv_slot(srv, (uint64_t)i, k, &slot));
+          CK(hipMemcpy(slot, grad[k] + parts[i].first, parts[i].second,
+                       hipMemcpyDeviceToDevice));
+        }
+    }
+    // persistent worker threads (a transport's receive threads), released per
+    // round by the driver and joined by a countdown
+    std::vector<double> ts;
+    std::mutex m;
+    std::condition_variable cv;
+    int go = -1, left = 0;
+    auto one_round = [&](int k) {
+      if (many) {
+            std::vector<const void*> srcs(np);
+            std::vector<void*> dsts(np);
+            for (int i = 0; i < np; ++i) {
+              srcs[i] = grad[k] + parts[i].first;
+              dsts[i] = out[k] + parts[i].first;
+            }
+            if (ready)
+              CKR(byteps_server_push_ready_many(srv, keys.data(), np, k));
+            else
+              CKR(byteps_server_push_many(srv, keys.data(), srcs.data(), lens.data(), np, k,
+                                          BYTEPS_REDUCE_FLOAT16, BYTEPS_SERVER_DEVICE));
+            CKR(byteps_server_pull_many(srv, keys.data(), dsts.data(), lens.data(), np,
+                                        BYTEPS_SERVER_DEVICE));
+            return;
+          }
+          for (int i = 0; i < np; ++i) {
+            if (ready)
+              CKR(byteps_server_push_ready(srv, (uint64_t)i, k));
+            else
+              CKR(byteps_server_push_async(srv, (uint64_t)i, k, grad[k] + parts[i].first,
+                                           parts[i].second, BYTEPS_REDUCE_FLOAT16,
+                                           BYTEPS_SERVER_DEVICE, on_push, nullptr));
+          }
+          for (int i = 0; i < np; ++i)
+            CKR(byteps_server_pull(srv, (uint64_t)i, out[k] + parts[i].first, parts[i].second,
+                                   BYTEPS_SERVER_DEVICE));
+    };
+    std::vector<std::thread> th;
+    for (int k = 0; k < N; ++k)
+      th.emplace_back([&, k] {
+        for (int r = 0; r < rounds + 2; ++r) {
+          {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return go >= r; });
+          }
+          one_round(k);
+          std::lock_guard<std::mutex> lk(m);
+          if (--left == 0) cv.notify_all();
+        }
+      });
+    for (int r = 0; r < rounds + 2; ++r) {
+      acks = 0;
+      auto t0 = std::chrono::steady_clock::now();
+      {
+        std::lock_guard<std::mutex> lk(m);
+        left = N;
+        go = r;
+      }
+      cv.notify_all();
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return left == 0; });
+      }
+      if (variant == 1)
+        while (acks.load() < (long)N * np) std::this_thread::yield();
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (r >= 2) ts.push_back(s);
+    }
+    for (auto& t : th) t.join();
+    // exactness: every worker's pull equals worker 0's (one store per key)
+    bool same = true;
+    std::vector<char> a(total), b(total);
+    CK(hipMemcpy(a.data(), out[0], total, hipMemcpyDeviceToHost));
+    for (int k = 1; k < N; ++k) {
+      CK(hipMemcpy(b.data(), out[k], total, hipMemcpyDeviceToHost));
+      same = same && std::memcmp(a.data(), b.data(), total) == 0;
+    }
+    std::sort(ts.begin(), ts.end());
+    const double med = ts[ts.size() / 2];
+    printf("{\"config\": \"cfg3_via_server\", \"driver\": \"native C++ threads "
+           "(tools/server_cfg3_native.cpp)\", \"variant\": \"%s\", \"n_workers\": %d, "
+           "\"keys\": %d, \"lanes\": %d, \"bytes_per_worker\": %zu, \"round_ms\": %.4f, "
+           "\"min_ms\": %.4f, \"us_per_key\": %.2f, \"hbm_frac_of_round\": %.4f, "
+           "\"pulls_agree\": %s}\n",
+           names[variant], N, np, lanes, total, med * 1e3,
+           ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, same ? "true" : "false");
+    fflush(stdout);
+    CKR(byteps_server_destroy(srv));
+  }
+  for (int k = 0; k < N; ++k) {
+    CK(hipFree(grad[k]));
+    CK(hipFree(out[k]));
+  }
+  return 0;
+}
