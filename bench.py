@@ -54,13 +54,15 @@ METRIC = "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 G
 DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
           "u8": (3, "uint8"), "i32": (4, "int32"), "i8": (5, "int8"), "i64": (6, "int64"),
           "bf16": (11, "bfloat16")}
-# Sources that define the headline kernel and its launch: a committed PMC
-# traffic record is quoted only while their hash matches (bench line
-# roofline.traffic_source).
+# What decides the headline kernel's code and launch: the ISA signature of
+# fold_kernel<OpF32,2,true,8> written by the build (prophet_amd/csrc/Makefile)
+# plus the launch-geometry rules of the C ABI (tuning defaults, residency by
+# source count: this span of bpsr_api.cpp).  A committed PMC traffic record is
+# quoted only while this id matches (roofline.traffic_source).  Without a
+# build signature, the kernel sources are hashed instead.
+KERNEL_SIG = "prophet_amd/libbpsr.fold_f32_8.sig"
 KERNEL_SOURCES = ("prophet_amd/csrc/bpsr_kernels_impl.h", "prophet_amd/csrc/bpsr_ops.h",
                   "prophet_amd/csrc/bpsr_internal.h", "prophet_amd/csrc/bpsr_k_f32.hip")
-# ... plus the launch-geometry rules of the C ABI (tuning defaults, residency by
-# source count): this span of bpsr_api.cpp, not the whole file
 KERNEL_SOURCE_SPANS = (("prophet_amd/csrc/bpsr_api.cpp", "static Tuning& tuning_storage()",
                         "static inline hipStream_t to_stream"),)
 
@@ -472,11 +474,16 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
 
 
 def kernel_build_id(root: str = ROOT) -> str:
-    """Hash of what decides the headline kernel's code and launch geometry."""
+    """Id of what decides the headline kernel's code and launch geometry."""
     h = hashlib.sha256()
-    for rel in KERNEL_SOURCES:
-        with open(os.path.join(root, rel), "rb") as f:
-            h.update(rel.encode() + b"\0" + f.read())
+    sig = os.path.join(root, KERNEL_SIG)
+    if os.path.exists(sig):
+        with open(sig, "rb") as f:
+            h.update(b"isa\0" + f.read().strip())
+    else:
+        for rel in KERNEL_SOURCES:
+            with open(os.path.join(root, rel), "rb") as f:
+                h.update(rel.encode() + b"\0" + f.read())
     for rel, a, b in KERNEL_SOURCE_SPANS:
         with open(os.path.join(root, rel)) as f:
             text = f.read()
