@@ -513,9 +513,9 @@ def pmc_traffic(workload: str):
     except OSError:
         now = None
     if d.get("kernel_build") != now:
-        src["status"] = f"kernel sources changed since the PMC pass (now {now}): not quoted"
+        src["status"] = f"kernel build changed since the PMC pass (now {now}): not quoted"
         return None, src
-    src["status"] = "same workload, same kernel sources"
+    src["status"] = "same workload, same kernel build (ISA signature + launch rules)"
     return d.get("hbm_bytes_per_launch"), src
 
 
