@@ -244,6 +244,11 @@ def test_graph_replay_matches_plans(red, dev, port, shape):
             assert torch.equal(a, v[0])
         for p in plans:
             p.close()
+        if it == 1:     # and the oracle, on every bucket of the replayed iteration
+            for i, (a, (dst, srcs, L, *_)) in enumerate(zip(got, tab.views)):
+                want = np.zeros(L, np.uint8)
+                port.sum_n(want, [s.cpu().numpy() for s in srcs], L, dt)
+                assert np.array_equal(a.cpu().numpy(), want), f"bucket {i}"
     q.close()
 
 

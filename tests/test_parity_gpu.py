@@ -126,13 +126,15 @@ def test_not_coaligned_and_unaligned(red, dev, port, dt):
 
 
 @pytest.mark.parametrize("dt", list(ALL_DTYPES), ids=lambda d: DType(d).name)
-def test_engine_pattern_equals_fused(red, dev, dt):
-    """N-1 in-place sum() calls (server.cc:127-130 engine loop) == one sum_n()."""
+def test_engine_pattern_equals_fused(red, dev, port, dt):
+    """N-1 in-place sum() calls (server.cc:127-130 engine loop) == one sum_n()
+    == the oracle's fold of the same inputs."""
     es = elem_size(dt)
     n = 65536 + 5
     L = n * es
-    ins = [torch.from_numpy(np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 9))
-                            .view(np.uint8)).to(dev) for k in range(8)]
+    host = [np.ascontiguousarray(synth.bucket(dt, n, k, "normal", 9)).view(np.uint8)
+            for k in range(8)]
+    ins = [torch.from_numpy(h).to(dev) for h in host]
     acc = ins[0].clone()
     for s in ins[1:]:
         red.sum(acc, s, L, dt)
@@ -143,6 +145,9 @@ def test_engine_pattern_equals_fused(red, dev, dt):
     torch.cuda.synchronize()
     assert torch.equal(acc, fused)
     assert torch.equal(acc, inplace)
+    want = np.zeros(L, np.uint8)
+    port.sum_n(want, host, L, dt)
+    assert_bytes_match(dt, acc.cpu().numpy(), want, nan_class_f32_f64=False)
 
 
 def test_more_than_32_sources_chains_left_fold(red, dev, port):

@@ -64,6 +64,7 @@ for s in $STEPS; do
            run server_cfg3_l8 300 ./tools/server_cfg3_native tools/cfg3_resnet50_table.txt 20 8 ;;
     srv3trace) run srv3_trace 300 rocprofv3 --hip-runtime-trace --kernel-trace --stats --output-format csv \
              -d "$OUT/srv3trace" -o srv3 -- ./tools/server_cfg3_native tools/cfg3_resnet50_table.txt 10 4 2 ;;
+    policy) run hbm_policy 300 env PROBE_POLICY=1 ./tools/hbm_probe2 256 ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
     cfg1memcpy) run cfg1_native_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy ./tools/cfg1_native 4 20 ;;
     cfg1prio) run cfg1_native_d2h_normal 300 env BPSR_SERVER_D2H_PRIORITY=normal ./tools/cfg1_native 4 20 ;;

@@ -170,6 +170,17 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  std::vector<V> vs_policy = {  // cache policy at the product's shape (aux 2 = nt, 16 = sc1)
+      {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
+      {"n8_product", PROD<8>},
+      {"n8_v2_wg1cu_l2s18", L<2, 18, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l2s16", L<2, 16, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l18s18", L<18, 18, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l18s2", L<18, 2, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l3s2", L<3, 2, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l2s3", L<2, 3, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l2s0", L<2, 0, 2, false, 8, false, 160>},
+  };
   std::vector<V> vs = {
       {"n8", L<2, 2, 4, false, 8>},
       {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
@@ -184,6 +195,7 @@ int main(int argc, char** argv) {
       {"n1_copy", L<2, 2, 4, false, 1>},
       {"n16_v2_wg1cu", L<2, 2, 2, false, 16, false, 160>},
   };
+  if (getenv("PROBE_POLICY")) vs = vs_policy;
   const size_t skews[] = {16384};
   for (int rep = 0; rep < 2; ++rep) {
     for (size_t skew : skews) {
