@@ -65,6 +65,13 @@ for s in $STEPS; do
     srv3trace) run srv3_trace 300 rocprofv3 --hip-runtime-trace --kernel-trace --stats --output-format csv \
              -d "$OUT/srv3trace" -o srv3 -- ./tools/server_cfg3_native tools/cfg3_resnet50_table.txt 10 4 2 ;;
     policy) run hbm_policy 300 env PROBE_POLICY=1 ./tools/hbm_probe2 256 ;;
+    bqsweep) for v in 1 2 4; do for o in 1 2 3; do
+               run bq_v${v}_o${o} 200 env BPSR_BQ_VPT=$v BPSR_BQ_GATE_OCC=$o ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 || exit 1
+             done; done ;;
+    bqwrite) run bq_kernel 200 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
+             run bq_write 200 env BPSR_BQ_RELEASE=write ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
+             run bq_kernel2 200 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
+             run bq_write2 200 env BPSR_BQ_RELEASE=write ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
     cfg1memcpy) run cfg1_native_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy ./tools/cfg1_native 4 20 ;;
     cfg1prio) run cfg1_native_d2h_normal 300 env BPSR_SERVER_D2H_PRIORITY=normal ./tools/cfg1_native 4 20 ;;
