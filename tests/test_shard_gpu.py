@@ -133,3 +133,41 @@ def test_sharded_nccl_multi_gpu():
     if n < 2:
         pytest.skip("needs >= 2 GPUs (RCCL ranks one per GPU)")
     _run(min(n, 4), "nccl")
+
+
+def test_cfg4_vgg16_full_size_owner_slices_one_gpu():
+    """BASELINE config 4 at its own size on one GPU: the 8-way fp32 VGG-16 set
+    (138,357,544 elements per worker) cut by the reference's reduce-scatter
+    ownership for G = 8 (core_loops.cc:208-211), each owner's slice folded by
+    the HIP fold as its GPU would; the slices put together equal torch's left
+    fold of the whole set bit for bit, and sampled windows equal the oracle."""
+    from oracle.oracle import PortReducer
+    from prophet_amd.buckets import vgg16_param_sizes
+    from prophet_amd.dtypes import DType
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.shard import owner_ranges
+    dev = torch.device("cuda:0")
+    E, N, G = sum(vgg16_param_sizes()), 8, 8
+    assert E == 138_357_544
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(44)
+    pushes = [torch.randn(E, device=dev, generator=gen) for _ in range(N)]
+    out = torch.empty(E, device=dev)
+    red = GpuReducer(device=0)
+    ranges = owner_ranges(E, G)
+    assert all(hi - lo == 17_294_693 for lo, hi in ranges)
+    for lo, hi in ranges:
+        red.sum_n(out[lo:hi], [p[lo:hi] for p in pushes], (hi - lo) * 4, DType.FLOAT32)
+    ref = pushes[0].clone()
+    for p in pushes[1:]:
+        ref.add_(p)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    port = PortReducer(nthreads=4)
+    W = 50_000
+    for lo, hi in ranges:                 # each shard's first and last window
+        for a in (lo, hi - W):
+            ins = [p[a:a + W].cpu().numpy().view(np.uint8) for p in pushes]
+            want = np.zeros(W * 4, np.uint8)
+            port.sum_n(want, ins, W * 4, DType.FLOAT32)
+            assert np.array_equal(out[a:a + W].cpu().numpy().view(np.uint8), want), a
