@@ -1,0 +1,134 @@
+/*
+ * bpsr/prophet.h — Prophet's PUSH-stage scheduler (C ABI of libbpsr.so), the
+ * native counterpart of BytePSScheduledQueue for the PUSH queue
+ * (byteps/common/scheduled_queue.cc:94-108 addTask, :199-215 findTask,
+ * :217-296 getTask, :362-371 reportFinish; constants scheduled_queue.h:77-95).
+ *
+ * It decides WHICH partitions reach the server together — the release groups
+ * a batched fold launch or a block-queue release (bpsr/reduce.h) receives:
+ *   - tasks whose tensor name matches Z_keyword ("scheduled") are collected
+ *     in backward order from the last checkpoint down; when the expected
+ *     gradient has a queued partition, all of its partition slots are stacked;
+ *     reaching the previous checkpoint opens a byte budget
+ *     backward_exec[k] * (int)(batch/64) * Z_NET_B * 125 (constructor, :26-33);
+ *   - release pops the stack top (lowest gradient index first) while the budget
+ *     strictly exceeds the task's length (:262); a task that does not fit ends
+ *     the block and collection resumes; an empty stack ends it too;
+ *   - once gradient 0 is stacked, the rest is released under the byte credit
+ *     Z_CREDIT, refilled by report_finish (:362-371); the empty stack resets
+ *     the iteration (:276-290);
+ *   - other tasks ("unscheduled") form the FIFO (_sq), served only while no
+ *     scheduled task is queued (:292-318).
+ * Equal gradient indices keep insertion order (the multiset compares priority
+ * only, scheduled_queue.h:58-62; findTask takes lower_bound).
+ *
+ * Deviations from the reference: an empty stack at release
+ * simply ends the block (the reference reads _mystack.top() of an empty stack,
+ * :250); a credit exactly equal to the task's length releases it once and
+ * charges it (the reference returns it without erasing it, :281-285, so it
+ * would be sent again); checkpoints, exec times and the gradient count are
+ * parameters (the reference hard-codes a 157-gradient model and 160-entry
+ * arrays); exec times are doubles (the pre-run profiler's measured values,
+ * global.h's _backward_exec).  The FIFO ignores ready events and ready tables
+ * (they belong to the stages around PUSH).
+ *
+ * Host-only: no call touches a GPU.  Every call on one queue is serialised by
+ * the queue's mutex (the reference's _mutex), so transport and engine threads
+ * may share it.  Errors: 0 / positive on success, a negative BYTEPS_REDUCE_E*
+ * code otherwise, message in byteps_reduce_last_error().
+ */
+#ifndef BPSR_PROPHET_H
+#define BPSR_PROPHET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "bpsr/reduce.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct byteps_prophet_config {
+  int64_t batch_size;           /* Z_BATCH_SIZE                                     */
+  int64_t net_b;                /* Z_NET_B (multiplied by 125, :27)                 */
+  int64_t credit;               /* Z_CREDIT, bytes                                  */
+  const int32_t* checkpoints;   /* ascending, checkpoints[0] == -1; NULL = the
+                                   reference's 13 (scheduled_queue.h:81-82)         */
+  int32_t ncheckpoints;         /* >= 2 when checkpoints is given                   */
+  const double* backward_exec;  /* ncheckpoints entries; NULL = the reference's
+                                   (scheduled_queue.h:84-85)                        */
+} byteps_prophet_config;
+
+typedef struct byteps_prophet_task {
+  int32_t grad;           /* declared gradient index (= -priority), 0..last checkpoint */
+  int32_t part;           /* partition index inside the gradient                 */
+  int64_t len;            /* bytes                                               */
+  int32_t total_partnum;  /* partitions of the gradient (_tensor_part)           */
+  int32_t scheduled;      /* 1: name matches Z_keyword (Prophet order); 0: FIFO  */
+  uint64_t key;           /* (declared_key << 16) + part                         */
+  uint64_t handle;        /* caller's cookie, returned unchanged                 */
+} byteps_prophet_task;
+
+/* Phase of a released task: the budget block it was released under (>= 0),
+ * BYTEPS_PROPHET_CREDIT after gradient 0, BYTEPS_PROPHET_FIFO for the FIFO. */
+enum { BYTEPS_PROPHET_CREDIT = -1, BYTEPS_PROPHET_FIFO = -2 };
+
+typedef struct byteps_prophet_queue byteps_prophet_queue;
+
+int byteps_prophet_create(const byteps_prophet_config* cfg, byteps_prophet_queue** out);
+int byteps_prophet_destroy(byteps_prophet_queue* q);
+
+/* addTask (scheduled_queue.cc:94-108).  EARGS for a scheduled task whose
+ * gradient lies outside [0, last checkpoint] or with total_partnum < 1. */
+int byteps_prophet_add_task(byteps_prophet_queue* q, const byteps_prophet_task* t);
+
+/* One getTask() call (scheduled_queue.cc:217-296): returns 1 and fills *out
+ * (and *phase if non-NULL) when a task is released, 0 when none is. */
+int byteps_prophet_get_task(byteps_prophet_queue* q, byteps_prophet_task* out, int32_t* phase);
+
+/* reportFinish(size) (scheduled_queue.cc:362-371). */
+int byteps_prophet_report_finish(byteps_prophet_queue* q, int64_t size);
+
+/* Queued tasks (scheduled + FIFO). */
+int byteps_prophet_pending(byteps_prophet_queue* q, uint64_t* n);
+
+/* The iteration state, for tests and tracing. */
+typedef struct byteps_prophet_state {
+  int32_t pointer;      /* _pointer: checkpoint index of the block being collected */
+  int32_t expected;     /* expected_priority * -1: next gradient to collect      */
+  int32_t sizepointer;  /* _sizepointer: budgets opened so far                   */
+  int32_t dequeue;      /* _dequeue: releasing (1) or collecting (0)             */
+  int32_t meetzero;     /* _meetzero: gradient 0 stacked                         */
+  int32_t stack_depth;  /* _mystack.size()                                       */
+  int64_t credit;       /* _bps_credit                                           */
+  double budget_left;   /* dynamic_size                                          */
+} byteps_prophet_state;
+int byteps_prophet_get_state(byteps_prophet_queue* q, byteps_prophet_state* out);
+
+/* Back to the start of an iteration (collection from the last checkpoint,
+ * full credit); queued tasks stay. */
+int byteps_prophet_reset(byteps_prophet_queue* q);
+
+/* Drive the queue through one iteration (the queue must hold no task when
+ * called; byteps_prophet_reset first for a fresh iteration): arrivals[i] is
+ * added before the i-th getTask poll (one arrival per poll, as gradients come
+ * off backward); polls continue until every arrival was added and nothing is
+ * queued.
+ * Releases are written to released[0..n) in order; group g is
+ * released[group_start[g] .. group_start[g+1]) — a run of consecutive
+ * successful polls, also split where the phase changes if split_on_phase —
+ * with group_phase[g] its phase.  finish_immediately reports each released
+ * task finished at once (credit refilled).  group_start needs n+1 entries,
+ * group_phase n.  Returns the number of groups; EARGS if max_idle consecutive
+ * empty polls pass (no progress possible, e.g. credit smaller than a task). */
+int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_task* arrivals,
+                                  size_t n, int finish_immediately, int split_on_phase,
+                                  uint64_t max_idle, byteps_prophet_task* released,
+                                  int32_t* group_start, int32_t* group_phase);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BPSR_PROPHET_H */

@@ -1,0 +1,195 @@
+"""TEST INFRASTRUCTURE — the CPU restatement (oracle) of Prophet's PUSH-queue
+release logic.  Only tests/ may import it; the product scheduler is the native
+one in libbpsr.so (include/bpsr/prophet.h, prophet_amd/prophet.py), checked
+against this module task for task (tests/test_prophet.py).
+
+Prophet's only change to BytePS is the PUSH-stage scheduler
+(byteps/common/scheduled_queue.cc:217-296, constants in scheduled_queue.h:77-95,
+credit replenishment in :362-371).  It decides WHICH partitions reach the
+server together, i.e. the buckets one batched reduce launch gets:
+
+* collection: gradients are expected in backward order, from the last
+  checkpoint down; when some partition of the expected gradient is queued, all
+  of that gradient's partition slots are pushed on a stack; when the expected
+  index reaches the previous checkpoint, the block is complete and a byte
+  budget ``dynamic_size = backward_exec[k] * (batch/64) * Z_NET_B * 125`` opens
+  (constructor, scheduled_queue.cc:26-33);
+* release: the stack is popped from the top (the lowest gradient index first)
+  while the budget exceeds the task's length; a task that does not fit ends the
+  release and collection resumes for the next block (the leftover stays on the
+  stack, under the next block's gradients);
+* once gradient 0 has been collected (``_meetzero``), every remaining stack
+  entry is released under a byte credit (``Z_CREDIT``) that ``report_finish``
+  refills; when the stack is empty the iteration state resets;
+* tasks whose name does not match Z_keyword (``scheduled=False``) go to the
+  FIFO ``_sq``, served only while no scheduled task is queued (:292-318;
+  ready events / tables are not modelled).
+
+Deviations (reference bugs, documented in DESIGN.md):
+* popping from an empty stack (``_mystack.top()`` on an empty stack,
+  scheduled_queue.cc:250) is undefined behaviour there; here the block simply
+  ends;
+* with credit exactly equal to the task length the reference returns the task
+  without erasing or popping it (so it would be sent twice, :281-285); here the
+  task is released once and the credit is charged (>=).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+from prophet_amd.buckets import PROPHET_CHECKPOINTS
+from prophet_amd.prophet import BACKWARD_EXEC, PushTask
+
+@dataclass
+class OracleProphetQueue:
+    """One PUSH queue (the root device's, scheduled_queue.cc:69-72)."""
+    batch_size: int                       # Z_BATCH_SIZE
+    net_b: int                            # Z_NET_B (the constructor multiplies by 125)
+    credit: int                           # Z_CREDIT
+    checkpoints: tuple = PROPHET_CHECKPOINTS
+    backward_exec: tuple = BACKWARD_EXEC
+
+    def __post_init__(self):
+        b = self.net_b * 125
+        scale = int(float(self.batch_size) / 64)
+        self._budget = [e * scale * b for e in self.backward_exec]
+        self._tasks: dict[int, list[PushTask]] = {}      # grad -> queued partitions
+        self._tensor_part: dict[int, int] = {}
+        self._fifo: list[PushTask] = []
+        self._credit0 = self.credit
+        self.reset()
+
+    def reset(self) -> None:
+        self._pointer = len(self.checkpoints) - 1
+        self._expected = self.checkpoints[self._pointer]
+        self._stack: list[int] = []                      # gradient indices
+        self._visited: set[int] = set()
+        self._dequeue = False
+        self._meetzero = False
+        self._sizepointer = 0
+        self._dynamic = 0
+        self._bps_credit = self._credit0
+        self.phase = None          # block index of the last release, or "credit"
+
+    # scheduled_queue.cc:94-108 (tasks whose name matches Z_keyword).  The
+    # multiset orders by priority only (scheduled_queue.h:58-62), so equal
+    # priorities keep insertion order and findTask (:199-215) returns the
+    # earliest-queued partition of a gradient.
+    def add_task(self, t: PushTask) -> None:
+        if not t.scheduled:
+            self._fifo.append(t)
+            return
+        self._tasks.setdefault(t.grad, []).append(t)
+        self._tensor_part[t.grad] = t.total_partnum
+
+    def pending(self) -> int:
+        return self._scheduled_pending() + len(self._fifo)
+
+    def _scheduled_pending(self) -> int:
+        return sum(len(v) for v in self._tasks.values())
+
+    def _find(self, grad: int):
+        lst = self._tasks.get(grad)
+        return lst[0] if lst else None
+
+    def _take(self, t: PushTask) -> None:
+        self._tasks[t.grad].pop(0)
+
+    def get_task(self) -> PushTask | None:
+        """One call of getTask() (scheduled_queue.cc:217-296)."""
+        if not self._scheduled_pending():
+            if not self._fifo:
+                return None
+            self.phase = "fifo"
+            return self._fifo.pop(0)
+        if not self._dequeue:
+            if self._find(self._expected) is None:
+                return None
+            if self._expected not in self._visited:
+                for _ in range(self._tensor_part.get(self._expected, 0)):
+                    self._stack.append(self._expected)
+                    if self._expected == 0:
+                        self._meetzero = True
+                self._visited.add(self._expected)
+            if self._expected >= 0:
+                self._expected -= 1
+            if self._pointer > 0 and self._expected == self.checkpoints[self._pointer - 1]:
+                self._dequeue = True
+                self._dynamic = self._budget[self._sizepointer]
+                self._sizepointer += 1
+            return None
+        if not self._stack:
+            self._end_block()
+            return None
+        task = self._find(self._stack[-1])
+        if task is None:
+            return None
+        if not self._meetzero:
+            if self._dynamic > task.len:
+                self._dynamic -= task.len
+                self.phase = self._sizepointer - 1
+            else:
+                self._end_block()
+                return None
+        elif self._bps_credit < task.len:
+            return None
+        else:
+            self._bps_credit -= task.len
+            self.phase = "credit"
+        self._take(task)
+        self._stack.pop()
+        if not self._stack and self._meetzero:
+            phase = self.phase
+            self.reset()
+            self.phase = phase
+        return task
+
+    def _end_block(self) -> None:
+        self._dequeue = False
+        if self._pointer > 0:
+            self._pointer -= 1
+
+    # scheduled_queue.cc:362-371
+    def report_finish(self, size: int) -> None:
+        if size > 0 and self._meetzero:
+            self._bps_credit += size
+
+
+def oracle_release_groups(queue: OracleProphetQueue, arrivals, finish_immediately: bool = True,
+                   max_idle: int = 1_000_000, with_phase: bool = False):
+    """Drive ``queue`` with ``arrivals`` (an iterable of PushTask in backward
+    order, one arrival per scheduler poll) and return the release groups: runs
+    of tasks released by consecutive successful get_task calls.  Each group is
+    what one batched reduce launch receives.  ``with_phase`` returns
+    ``(phase, group)`` pairs, phase being the budget block index or "credit"."""
+    groups, cur = [], []
+    it = iter(arrivals)
+    exhausted = False
+    idle = 0
+    cur_phase = None
+    while True:
+        if not exhausted:
+            try:
+                queue.add_task(next(it))
+            except StopIteration:
+                exhausted = True
+        t = queue.get_task()
+        if t is not None:
+            if cur and with_phase and queue.phase != cur_phase:
+                groups.append((cur_phase, cur))
+                cur = []
+            cur_phase = queue.phase
+            cur.append(t)
+            idle = 0
+            if finish_immediately:
+                queue.report_finish(t.len)
+            continue
+        if cur:
+            groups.append((cur_phase, cur) if with_phase else cur)
+            cur = []
+        if exhausted and queue.pending() == 0:
+            break
+        idle += 1
+        if idle > max_idle:
+            raise RuntimeError("scheduler made no progress")
+    return groups

@@ -1,42 +1,32 @@
-"""Prophet's PUSH-queue release logic, restated as a deterministic simulator.
+"""Prophet's PUSH-stage scheduler — the native one in libbpsr.so
+(include/bpsr/prophet.h, prophet_amd/csrc/bpsr_prophet.cpp), behind the
+interface of BytePSScheduledQueue's PUSH queue
+(byteps/common/scheduled_queue.cc:94-108 addTask, :217-296 getTask,
+:362-371 reportFinish).
 
-Prophet's only change to BytePS is the PUSH-stage scheduler
-(byteps/common/scheduled_queue.cc:217-296, constants in scheduled_queue.h:77-95,
-credit replenishment in :362-371).  It decides WHICH partitions reach the
-server together, i.e. the buckets one batched reduce launch gets.  This module
-reproduces its state machine so the reduce path can be fed realistic release
-groups (one ``byteps_reduce_plan`` per group):
-
-* collection: gradients are expected in backward order, from the last
-  checkpoint down; when some partition of the expected gradient is queued, all
-  of that gradient's partition slots are pushed on a stack; when the expected
-  index reaches the previous checkpoint, the block is complete and a byte
-  budget ``dynamic_size = backward_exec[k] * (batch/64) * Z_NET_B * 125`` opens
-  (constructor, scheduled_queue.cc:26-33);
-* release: the stack is popped from the top (the lowest gradient index first)
-  while the budget exceeds the task's length; a task that does not fit ends the
-  release and collection resumes for the next block (the leftover stays on the
-  stack, under the next block's gradients);
-* once gradient 0 has been collected (``_meetzero``), every remaining stack
-  entry is released under a byte credit (``Z_CREDIT``) that ``report_finish``
-  refills; when the stack is empty the iteration state resets.
-
-Deviations (reference bugs, documented in DESIGN.md):
-* popping from an empty stack (``_mystack.top()`` on an empty stack,
-  scheduled_queue.cc:250) is undefined behaviour there; here the block simply
-  ends;
-* with credit exactly equal to the task length the reference returns the task
-  without erasing or popping it (so it would be sent twice, :281-285); here the
-  task is released once and the credit is charged (>=).
+It decides which partitions reach the server together: the release groups a
+batched fold launch (``byteps_reduce_plan``) or a block-queue release
+(``byteps_reduce_blockq_release_range``) receives.  The algorithm, its
+deviations from the reference and its thread-safety are documented in the
+header; ``oracle/prophet_oracle.py`` restates it in Python and the tests
+compare the two task for task.  There is no Python fallback: a missing
+``libbpsr.so`` raises.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+import ctypes
+import threading
+from dataclasses import dataclass
 
 from .buckets import DEFAULT_PARTITION_BYTES, PROPHET_CHECKPOINTS, partition_all
+from .reducer import _check, load_library
 
 # scheduled_queue.h:84-85
 BACKWARD_EXEC = (16, 15, 9, 10, 12, 18, 15, 21, 30, 25, 20, 5, 0)
+
+PHASE_CREDIT = -1      # BYTEPS_PROPHET_CREDIT
+PHASE_FIFO = -2        # BYTEPS_PROPHET_FIFO
+_PHASE_NAMES = {PHASE_CREDIT: "credit", PHASE_FIFO: "fifo"}
 
 
 @dataclass(frozen=True, order=True)
@@ -46,111 +36,135 @@ class PushTask:
     len: int           # bytes
     total_partnum: int = 1
     key: int = 0
+    scheduled: bool = True   # the tensor name matches Z_keyword (else: FIFO)
 
 
-@dataclass
+class _Config(ctypes.Structure):
+    _fields_ = [("batch_size", ctypes.c_int64), ("net_b", ctypes.c_int64),
+                ("credit", ctypes.c_int64), ("checkpoints", ctypes.POINTER(ctypes.c_int32)),
+                ("ncheckpoints", ctypes.c_int32), ("backward_exec", ctypes.POINTER(ctypes.c_double))]
+
+
+class _Task(ctypes.Structure):
+    _fields_ = [("grad", ctypes.c_int32), ("part", ctypes.c_int32), ("len", ctypes.c_int64),
+                ("total_partnum", ctypes.c_int32), ("scheduled", ctypes.c_int32),
+                ("key", ctypes.c_uint64), ("handle", ctypes.c_uint64)]
+
+
+class _State(ctypes.Structure):
+    _fields_ = [("pointer", ctypes.c_int32), ("expected", ctypes.c_int32),
+                ("sizepointer", ctypes.c_int32), ("dequeue", ctypes.c_int32),
+                ("meetzero", ctypes.c_int32), ("stack_depth", ctypes.c_int32),
+                ("credit", ctypes.c_int64), ("budget_left", ctypes.c_double)]
+
+
+PROPHET_EXPORTS = (
+    "byteps_prophet_create", "byteps_prophet_destroy", "byteps_prophet_add_task",
+    "byteps_prophet_get_task", "byteps_prophet_report_finish", "byteps_prophet_pending",
+    "byteps_prophet_get_state", "byteps_prophet_reset", "byteps_prophet_release_groups",
+)
+
+_BOUND = None
+
+
+def _ck(rc: int) -> None:
+    if rc < 0:
+        _check(rc)
+
+
+def _lib():
+    global _BOUND
+    if _BOUND is None:
+        L = load_library()
+        vp, P = ctypes.c_void_p, ctypes.POINTER
+        L.byteps_prophet_create.argtypes = [P(_Config), P(vp)]
+        L.byteps_prophet_destroy.argtypes = [vp]
+        L.byteps_prophet_add_task.argtypes = [vp, P(_Task)]
+        L.byteps_prophet_get_task.argtypes = [vp, P(_Task), P(ctypes.c_int32)]
+        L.byteps_prophet_report_finish.argtypes = [vp, ctypes.c_int64]
+        L.byteps_prophet_pending.argtypes = [vp, P(ctypes.c_uint64)]
+        L.byteps_prophet_get_state.argtypes = [vp, P(_State)]
+        L.byteps_prophet_reset.argtypes = [vp]
+        L.byteps_prophet_release_groups.argtypes = [
+            vp, P(_Task), ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+            P(_Task), P(ctypes.c_int32), P(ctypes.c_int32)]
+        for name in PROPHET_EXPORTS:
+            getattr(L, name).restype = ctypes.c_int
+        _BOUND = L
+    return _BOUND
+
+
 class ProphetPushQueue:
-    """One PUSH queue (the root device's, scheduled_queue.cc:69-72)."""
-    batch_size: int                       # Z_BATCH_SIZE
-    net_b: int                            # Z_NET_B (the constructor multiplies by 125)
-    credit: int                           # Z_CREDIT
-    checkpoints: tuple = PROPHET_CHECKPOINTS
-    backward_exec: tuple = BACKWARD_EXEC
+    """One PUSH queue (the root device's, scheduled_queue.cc:69-72), native.
 
-    def __post_init__(self):
-        b = self.net_b * 125
-        scale = int(float(self.batch_size) / 64)
-        self._budget = [e * scale * b for e in self.backward_exec]
-        self._tasks: dict[int, list[PushTask]] = {}      # grad -> queued partitions
-        self._tensor_part: dict[int, int] = {}
-        self._credit0 = self.credit
-        self.reset()
+    ``batch_size`` = Z_BATCH_SIZE, ``net_b`` = Z_NET_B (the constructor
+    multiplies it by 125), ``credit`` = Z_CREDIT bytes.  ``phase`` is the phase
+    of the last released task: its budget block index, "credit" or "fifo"."""
 
-    def reset(self) -> None:
-        self._pointer = len(self.checkpoints) - 1
-        self._expected = self.checkpoints[self._pointer]
-        self._stack: list[int] = []                      # gradient indices
-        self._visited: set[int] = set()
-        self._dequeue = False
-        self._meetzero = False
-        self._sizepointer = 0
-        self._dynamic = 0
-        self._bps_credit = self._credit0
-        self.phase = None          # block index of the last release, or "credit"
+    def __init__(self, batch_size: int, net_b: int, credit: int,
+                 checkpoints=PROPHET_CHECKPOINTS, backward_exec=BACKWARD_EXEC):
+        if len(backward_exec) != len(checkpoints):
+            raise ValueError("backward_exec needs one entry per checkpoint")
+        self._L = _lib()
+        cps = (ctypes.c_int32 * len(checkpoints))(*checkpoints)
+        ex = (ctypes.c_double * len(backward_exec))(*backward_exec)
+        cfg = _Config(int(batch_size), int(net_b), int(credit), cps, len(checkpoints), ex)
+        h = ctypes.c_void_p()
+        _ck(self._L.byteps_prophet_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.checkpoints = tuple(checkpoints)
+        self.phase = None
+        self._lock = threading.Lock()          # guards the handle -> task map
+        self._live: dict[int, PushTask] = {}
+        self._next = 0
 
-    # scheduled_queue.cc:94-108 (tasks whose name matches Z_keyword).  The
-    # multiset orders by priority only (scheduled_queue.h:58-62), so equal
-    # priorities keep insertion order and findTask (:199-215) returns the
-    # earliest-queued partition of a gradient.
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._L.byteps_prophet_destroy(h)
+            self._h = None
+
+    def _to_c(self, t: PushTask) -> _Task:
+        with self._lock:
+            hid = self._next
+            self._next += 1
+            self._live[hid] = t
+        return _Task(t.grad, t.part, t.len, t.total_partnum, int(t.scheduled), t.key, hid)
+
     def add_task(self, t: PushTask) -> None:
-        self._tasks.setdefault(t.grad, []).append(t)
-        self._tensor_part[t.grad] = t.total_partnum
-
-    def pending(self) -> int:
-        return sum(len(v) for v in self._tasks.values())
-
-    def _find(self, grad: int):
-        lst = self._tasks.get(grad)
-        return lst[0] if lst else None
-
-    def _take(self, t: PushTask) -> None:
-        self._tasks[t.grad].pop(0)
+        c = self._to_c(t)
+        rc = self._L.byteps_prophet_add_task(self._h, ctypes.byref(c))
+        if rc:
+            with self._lock:
+                del self._live[c.handle]
+            _ck(rc)
 
     def get_task(self) -> PushTask | None:
-        """One call of getTask() (scheduled_queue.cc:217-296)."""
-        if not self.pending():
+        """One getTask() poll: the released task, or None."""
+        out, ph = _Task(), ctypes.c_int32()
+        rc = self._L.byteps_prophet_get_task(self._h, ctypes.byref(out), ctypes.byref(ph))
+        _ck(rc if rc < 0 else 0)
+        if rc == 0:
             return None
-        if not self._dequeue:
-            if self._find(self._expected) is None:
-                return None
-            if self._expected not in self._visited:
-                for _ in range(self._tensor_part.get(self._expected, 0)):
-                    self._stack.append(self._expected)
-                    if self._expected == 0:
-                        self._meetzero = True
-                self._visited.add(self._expected)
-            if self._expected >= 0:
-                self._expected -= 1
-            if self._pointer > 0 and self._expected == self.checkpoints[self._pointer - 1]:
-                self._dequeue = True
-                self._dynamic = self._budget[self._sizepointer]
-                self._sizepointer += 1
-            return None
-        if not self._stack:
-            self._end_block()
-            return None
-        task = self._find(self._stack[-1])
-        if task is None:
-            return None
-        if not self._meetzero:
-            if self._dynamic > task.len:
-                self._dynamic -= task.len
-                self.phase = self._sizepointer - 1
-            else:
-                self._end_block()
-                return None
-        elif self._bps_credit < task.len:
-            return None
-        else:
-            self._bps_credit -= task.len
-            self.phase = "credit"
-        self._take(task)
-        self._stack.pop()
-        if not self._stack and self._meetzero:
-            phase = self.phase
-            self.reset()
-            self.phase = phase
-        return task
+        self.phase = _PHASE_NAMES.get(ph.value, ph.value)
+        with self._lock:
+            return self._live.pop(out.handle)
 
-    def _end_block(self) -> None:
-        self._dequeue = False
-        if self._pointer > 0:
-            self._pointer -= 1
-
-    # scheduled_queue.cc:362-371
     def report_finish(self, size: int) -> None:
-        if size > 0 and self._meetzero:
-            self._bps_credit += size
+        _ck(self._L.byteps_prophet_report_finish(self._h, int(size)))
+
+    def pending(self) -> int:
+        n = ctypes.c_uint64()
+        _ck(self._L.byteps_prophet_pending(self._h, ctypes.byref(n)))
+        return n.value
+
+    def reset(self) -> None:
+        _ck(self._L.byteps_prophet_reset(self._h))
+
+    def state(self) -> dict:
+        s = _State()
+        _ck(self._L.byteps_prophet_get_state(self._h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in _State._fields_}
 
 
 def model_checkpoints(n_tensors: int, checkpoints=PROPHET_CHECKPOINTS) -> tuple:
@@ -177,39 +191,37 @@ def backward_arrivals(sizes_bytes, bound: int = DEFAULT_PARTITION_BYTES) -> list
 
 def release_groups(queue: ProphetPushQueue, arrivals, finish_immediately: bool = True,
                    max_idle: int = 1_000_000, with_phase: bool = False):
-    """Drive ``queue`` with ``arrivals`` (an iterable of PushTask in backward
-    order, one arrival per scheduler poll) and return the release groups: runs
-    of tasks released by consecutive successful get_task calls.  Each group is
-    what one batched reduce launch receives.  ``with_phase`` returns
-    ``(phase, group)`` pairs, phase being the budget block index or "credit"."""
-    groups, cur = [], []
-    it = iter(arrivals)
-    exhausted = False
-    idle = 0
-    cur_phase = None
-    while True:
-        if not exhausted:
-            try:
-                queue.add_task(next(it))
-            except StopIteration:
-                exhausted = True
-        t = queue.get_task()
-        if t is not None:
-            if cur and with_phase and queue.phase != cur_phase:
-                groups.append((cur_phase, cur))
-                cur = []
-            cur_phase = queue.phase
-            cur.append(t)
-            idle = 0
-            if finish_immediately:
-                queue.report_finish(t.len)
-            continue
-        if cur:
-            groups.append((cur_phase, cur) if with_phase else cur)
-            cur = []
-        if exhausted and queue.pending() == 0:
-            break
-        idle += 1
-        if idle > max_idle:
-            raise RuntimeError("scheduler made no progress")
+    """Drive ``queue`` through one iteration in native code
+    (``byteps_prophet_release_groups``): one arrival per scheduler poll, in
+    the given (backward) order; a release group is a run of consecutive
+    successful polls — what one batched reduce launch receives.  ``with_phase``
+    returns ``(phase, group)`` pairs (groups also split at phase changes),
+    phase being the budget block index, "credit" or "fifo".  The queue must be
+    empty; it is not reset first."""
+    arrivals = list(arrivals)
+    n = len(arrivals)
+    arr = (_Task * max(n, 1))(*[queue._to_c(t) for t in arrivals])
+    rel = (_Task * max(n, 1))()
+    starts = (ctypes.c_int32 * (n + 1))()
+    phases = (ctypes.c_int32 * max(n, 1))()
+    ng = queue._L.byteps_prophet_release_groups(
+        queue._h, arr, n, int(finish_immediately), int(with_phase), int(max_idle),
+        rel, starts, phases)
+    if ng < 0:
+        with queue._lock:
+            for c in arr[:n]:
+                queue._live.pop(c.handle, None)
+        _ck(ng)
+    groups = []
+    with queue._lock:
+        for g in range(ng):
+            tasks = [queue._live.pop(rel[i].handle) for i in range(starts[g], starts[g + 1])]
+            ph = _PHASE_NAMES.get(phases[g], phases[g])
+            groups.append((ph, tasks) if with_phase else tasks)
+        if ng:
+            queue.phase = _PHASE_NAMES.get(phases[ng - 1], phases[ng - 1])
     return groups
+
+
+__all__ = ["PushTask", "ProphetPushQueue", "BACKWARD_EXEC", "PHASE_CREDIT", "PHASE_FIFO",
+           "model_checkpoints", "backward_arrivals", "release_groups", "PROPHET_EXPORTS"]

@@ -1,5 +1,5 @@
 """The C-ABI library loads here (no GPU) and exports exactly what
-include/bpsr/reduce.h declares; host-only argument checks run without a GPU."""
+include/bpsr/{reduce,server,prophet}.h declare; host-only argument checks run without a GPU."""
 import ctypes
 import os
 import re
@@ -11,7 +11,7 @@ from prophet_amd import reducer
 from prophet_amd.dtypes import ALL_DTYPES, elem_size
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "bpsr", h) for h in ("reduce.h", "server.h")]
+HEADERS = [os.path.join(ROOT, "include", "bpsr", h) for h in ("reduce.h", "server.h", "prophet.h")]
 
 
 def header_functions(headers=HEADERS):
@@ -25,7 +25,9 @@ def header_functions(headers=HEADERS):
 def test_header_declares_expected_api():
     from prophet_amd.server import SERVER_EXPORTS
     assert header_functions(HEADERS[:1]) == sorted(reducer.EXPORTS)
-    assert header_functions(HEADERS[1:]) == sorted(SERVER_EXPORTS)
+    assert header_functions(HEADERS[1:2]) == sorted(SERVER_EXPORTS)
+    from prophet_amd.prophet import PROPHET_EXPORTS
+    assert header_functions(HEADERS[2:]) == sorted(PROPHET_EXPORTS)
 
 
 def test_library_exports_every_header_symbol():
@@ -150,3 +152,18 @@ def test_block_queue_argument_errors_without_gpu():
     assert lib.byteps_reduce_blockq_status(None, None) == reducer.EARGS
     assert lib.byteps_reduce_blockq_config(None, 0, 1.0) == reducer.EARGS
     assert lib.byteps_reduce_blockq_destroy(None) == reducer.OK
+
+
+def test_prophet_scheduler_from_c(tmp_path):
+    """include/bpsr/prophet.h from plain C99 (gcc -Wall -Werror), linked to
+    libbpsr.so: polls and the whole-iteration driver give the hand trace of
+    tests/test_prophet.py::test_budget_releases_lowest_index_first, handles
+    come back unchanged.  Host-only calls: no GPU."""
+    exe = tmp_path / "prophet_drive"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "prophet_drive.c"), "-o", str(exe),
+                    "-L", os.path.dirname(reducer.LIB_PATH), "-lbpsr",
+                    "-Wl,-rpath," + os.path.dirname(reducer.LIB_PATH)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert out[0].split() == ["2:0", "3:0", "0:-1", "1:-1"]
+    assert out[1].split() == ["2:0:101", "3:0:100", "|", "0:-1:103", "1:-1:102", "|"]

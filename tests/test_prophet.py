@@ -1,17 +1,47 @@
 """Prophet PUSH-queue release logic (scheduled_queue.cc:217-296, :362-371):
-hand-worked small traces, budget carry-over, credit gating, and whole-iteration
-properties on the ResNet-50 fp16 partition set (config 3)."""
+hand-worked small traces, budget carry-over, credit gating, the FIFO, and
+whole-iteration properties on the ResNet-50 fp16 partition set (config 3).
+
+Every test runs twice: on the native scheduler in libbpsr.so (the product,
+host-only calls — no GPU needed) and on its restatement
+(oracle/prophet_oracle.py), so the hand-worked traces pin the oracle and the
+native code alike; test_native_equals_oracle_fuzz then compares the two task
+for task on random configurations.  The reference scheduler cannot be built
+on its own (it reads BytePSGlobal), so these traces are derived from its
+source by hand: parity pinned by hand-worked traces."""
+import random
+
 import pytest
 
-from prophet_amd.buckets import resnet50_param_sizes
+from oracle.prophet_oracle import OracleProphetQueue, oracle_release_groups
+from prophet_amd.buckets import resnet50_param_sizes, vgg16_param_sizes
 from prophet_amd.prophet import (BACKWARD_EXEC, ProphetPushQueue, PushTask, backward_arrivals,
                                  model_checkpoints, release_groups)
 
+IMPLS = {"native": (ProphetPushQueue, release_groups),
+         "oracle": (OracleProphetQueue, oracle_release_groups)}
 
-def _q(exec_, credit=150, cps=(-1, 1, 3)):
+
+@pytest.fixture(params=["native", "oracle"])
+def impl(request):
+    return IMPLS[request.param]
+
+
+def _mk(impl, **kw):
+    return impl[0](**kw)
+
+
+def _state(q):
+    if isinstance(q, ProphetPushQueue):
+        s = q.state()
+        return s["pointer"], s["expected"], bool(s["meetzero"]), s["credit"]
+    return q._pointer, q._expected, q._meetzero, q._bps_credit
+
+
+def _q(impl, exec_, credit=150, cps=(-1, 1, 3)):
     # batch 64 -> scale 1; Z_NET_B 1 -> B = 125 bytes per exec unit
-    return ProphetPushQueue(batch_size=64, net_b=1, credit=credit, checkpoints=cps,
-                            backward_exec=exec_)
+    return _mk(impl, batch_size=64, net_b=1, credit=credit, checkpoints=cps,
+               backward_exec=exec_)
 
 
 def _arrivals(n=4, ln=100):
@@ -22,28 +52,28 @@ def _grads(groups):
     return [[t.grad for t in g] for g in groups]
 
 
-def test_budget_releases_lowest_index_first():
+def test_budget_releases_lowest_index_first(impl):
     # block {3,2}: budget 250 -> 2 then 3; block {1,0} released under credit
-    q = _q((2, 5, 0))
-    assert _grads(release_groups(q, _arrivals())) == [[2, 3], [0, 1]]
+    q = _q(impl, (2, 5, 0))
+    assert _grads(impl[1](q, _arrivals())) == [[2, 3], [0, 1]]
 
 
-def test_budget_leftover_stays_under_next_block():
+def test_budget_leftover_stays_under_next_block(impl):
     # budget 150 releases only gradient 2 (150 > 100, then 50 > 100 fails);
     # gradient 3 stays on the stack under 1 and 0 and goes last
-    q = _q((1.2, 5, 0))
-    assert _grads(release_groups(q, _arrivals())) == [[2], [0, 1, 3]]
+    q = _q(impl, (1.2, 5, 0))
+    assert _grads(impl[1](q, _arrivals())) == [[2], [0, 1, 3]]
 
 
-def test_strict_budget_comparison():
+def test_strict_budget_comparison(impl):
     # dynamic_size > len is strict (scheduled_queue.cc:262): budget exactly
     # one task long releases nothing in that block
-    q = _q((0.8, 5, 0))
-    assert _grads(release_groups(q, _arrivals())) == [[0, 1, 2, 3]]
+    q = _q(impl, (0.8, 5, 0))
+    assert _grads(impl[1](q, _arrivals())) == [[0, 1, 2, 3]]
 
 
-def test_credit_gates_after_gradient_zero():
-    q = _q((2, 5, 0), credit=150)
+def test_credit_gates_after_gradient_zero(impl):
+    q = _q(impl, (2, 5, 0), credit=150)
     for t in _arrivals():
         q.add_task(t)
     got = []
@@ -60,37 +90,37 @@ def test_credit_gates_after_gradient_zero():
     assert q.pending() == 0
 
 
-def test_report_finish_only_counts_after_meetzero():
-    q = _q((2, 5, 0), credit=150)
+def test_report_finish_only_counts_after_meetzero(impl):
+    q = _q(impl, (2, 5, 0), credit=150)
     q.report_finish(1000)                     # before _meetzero: ignored
-    assert q._bps_credit == 150
+    assert _state(q)[3] == 150
 
 
-def test_partitions_stack_per_gradient():
+def test_partitions_stack_per_gradient(impl):
     # a 3-partition gradient pushes three stack slots; partitions leave in
     # arrival order (multiset keeps insertion order for equal priority)
-    q = _q((100, 100, 0))
+    q = _q(impl, (100, 100, 0))
     arr = [PushTask(3, 0, 10, 1), PushTask(2, 0, 10, 3), PushTask(2, 1, 10, 3),
            PushTask(2, 2, 10, 3), PushTask(1, 0, 10, 1), PushTask(0, 0, 10, 1)]
-    out = [(t.grad, t.part) for g in release_groups(q, arr) for t in g]
+    out = [(t.grad, t.part) for g in impl[1](q, arr) for t in g]
     assert out == [(2, 0), (2, 1), (2, 2), (3, 0), (0, 0), (1, 0)]
 
 
-def test_state_resets_between_iterations():
-    q = _q((2, 5, 0))
-    a = _grads(release_groups(q, _arrivals()))
-    b = _grads(release_groups(q, _arrivals()))
+def test_state_resets_between_iterations(impl):
+    q = _q(impl, (2, 5, 0))
+    a = _grads(impl[1](q, _arrivals()))
+    b = _grads(impl[1](q, _arrivals()))
     assert a == b
-    assert q._pointer == 2 and q._expected == 3 and not q._meetzero
+    assert _state(q)[:3] == (2, 3, False)
 
 
 @pytest.mark.parametrize("batch,net_b", [(64, 1), (256, 10), (64, 100)])
-def test_resnet50_iteration_releases_every_partition_once(batch, net_b):
+def test_resnet50_iteration_releases_every_partition_once(impl, batch, net_b):
     sizes = [n * 2 for n in resnet50_param_sizes()]
     arr = backward_arrivals(sizes)
-    q = ProphetPushQueue(batch_size=batch, net_b=net_b, credit=8 << 20,
+    q = _mk(impl, batch_size=batch, net_b=net_b, credit=8 << 20,
                          checkpoints=model_checkpoints(len(sizes)))
-    phased = release_groups(q, arr, with_phase=True)
+    phased = impl[1](q, arr, with_phase=True)
     groups = [g for _, g in phased]
     flat = [t for g in groups for t in g]
     assert sorted(flat) == sorted(arr)
@@ -103,17 +133,186 @@ def test_resnet50_iteration_releases_every_partition_once(batch, net_b):
     # the credit phase is last and starts at gradient 0
     assert phased[-1][0] == "credit" and groups[-1][0].grad == 0
     # a second iteration on the same queue reproduces the grouping
-    assert [[(t.grad, t.part) for t in g] for g in release_groups(q, arr)] == \
+    assert [[(t.grad, t.part) for t in g] for g in impl[1](q, arr)] == \
         [[(t.grad, t.part) for t in g] for g in groups]
 
 
-def test_huge_budget_releases_whole_blocks():
+def test_huge_budget_releases_whole_blocks(impl):
     sizes = [n * 2 for n in resnet50_param_sizes()]
-    q = ProphetPushQueue(batch_size=64, net_b=10**9, credit=1 << 40,
+    q = _mk(impl, batch_size=64, net_b=10**9, credit=1 << 40,
                          checkpoints=model_checkpoints(len(sizes)))
-    groups = release_groups(q, backward_arrivals(sizes))
+    groups = impl[1](q, backward_arrivals(sizes))
     cps = model_checkpoints(len(sizes))
     want = [sorted(range(cps[i] + 1, cps[i + 1] + 1)) for i in range(len(cps) - 2, -1, -1)]
     assert [sorted({t.grad for t in g}) for g in groups] == want
     # inside a block the lowest index leaves first
     assert groups[0][0].grad == cps[-2] + 1
+
+
+def test_fifo_served_only_without_scheduled_tasks(impl):
+    # unscheduled tasks (names not matching Z_keyword) wait in _sq while any
+    # scheduled task is queued, then leave in arrival order (:292-318)
+    q = _q(impl, (2, 5, 0), credit=1 << 20)
+    q.add_task(PushTask(7, 0, 64, scheduled=False))
+    q.add_task(PushTask(3, 0, 100))
+    q.add_task(PushTask(8, 0, 64, scheduled=False))
+    assert q.pending() == 3
+    got = []
+    for t in _arrivals()[1:]:
+        q.add_task(t)
+    for _ in range(30):
+        t = q.get_task()
+        if t is not None:
+            got.append((t.grad, q.phase))
+    assert got[:4] == [(2, 0), (3, 0), (0, "credit"), (1, "credit")]
+    assert got[4:] == [(7, "fifo"), (8, "fifo")]
+    assert q.pending() == 0
+
+
+def _fuzz_case(rng):
+    ngrad = rng.randint(3, 40)
+    ncp = rng.randint(2, min(ngrad, 8))
+    inner = sorted(rng.sample(range(0, ngrad - 1), ncp - 2)) if ncp > 2 else []
+    cps = tuple([-1] + inner + [ngrad - 1])
+    exec_ = tuple(round(rng.uniform(0, 6), rng.choice([0, 1, 2])) for _ in cps)
+    kw = dict(batch_size=rng.choice([32, 64, 100, 256]), net_b=rng.choice([1, 2, 7]),
+              credit=rng.randint(0, 3000), checkpoints=cps, backward_exec=exec_)
+    arr = []
+    for g in range(ngrad - 1, -1, -1):
+        nparts = rng.choice([1, 1, 1, 2, 3])
+        for p in range(nparts):
+            arr.append(PushTask(g, p, rng.choice([50, 100, 125, 250, 400, 1000]), nparts,
+                                (g << 16) + p))
+    for i in range(rng.randint(0, 3)):
+        arr.insert(rng.randrange(len(arr) + 1), PushTask(1000 + i, 0, 77, scheduled=False))
+    for _ in range(rng.randint(0, 3)):        # a little arrival jitter
+        i = rng.randrange(len(arr) - 1)
+        arr[i], arr[i + 1] = arr[i + 1], arr[i]
+    return kw, arr
+
+
+@pytest.mark.parametrize("seed", range(int(__import__("os").environ.get("PROPHET_FUZZ", "60"))))
+def test_native_equals_oracle_fuzz(seed):
+    """Random models, budgets, credits, arrival jitter, FIFO tasks and
+    report_finish timing: the native scheduler releases the same tasks in the
+    same order with the same phases and state as the restatement."""
+    rng = random.Random(seed)
+    kw, arr = _fuzz_case(rng)
+    nat, ora = ProphetPushQueue(**kw), OracleProphetQueue(**kw)
+    seq_n, seq_o = [], []
+    inflight = []
+    it = iter(arr)
+    for _ in range(20 * len(arr) + 200):
+        if rng.random() < 0.6:
+            t = next(it, None)
+            if t is not None:
+                nat.add_task(t)
+                ora.add_task(t)
+        a, b = nat.get_task(), ora.get_task()
+        assert a == b
+        if a is not None:
+            assert nat.phase == ora.phase
+            seq_n.append((a, nat.phase))
+            seq_o.append((b, ora.phase))
+            inflight.append(a.len)
+        if inflight and rng.random() < 0.5:
+            sz = inflight.pop(0)
+            nat.report_finish(sz)
+            ora.report_finish(sz)
+        assert _state(nat) == _state(ora)
+        assert nat.pending() == ora.pending()
+    assert seq_n == seq_o
+    # the whole-iteration driver agrees too (fresh queues, immediate finish)
+    nat, ora = ProphetPushQueue(**kw), OracleProphetQueue(**kw)
+    try:
+        want = oracle_release_groups(ora, arr, with_phase=True, max_idle=5000)
+    except RuntimeError:
+        with pytest.raises(Exception, match="no progress"):
+            release_groups(nat, arr, with_phase=True, max_idle=5000)
+        return
+    assert release_groups(nat, arr, with_phase=True, max_idle=5000) == want
+
+
+@pytest.mark.parametrize("model", ["resnet50_fp16", "vgg16_fp32"])
+def test_native_equals_oracle_configs(model):
+    """BASELINE configs 3 and 4's partition sets through one iteration."""
+    sizes = ([n * 2 for n in resnet50_param_sizes()] if model == "resnet50_fp16"
+             else [n * 4 for n in vgg16_param_sizes()])
+    if model == "resnet50_fp16":
+        extra = dict(checkpoints=model_checkpoints(len(sizes)))
+    else:   # 32 gradients: checkpoints as the pre-run profiler would cut them
+        extra = dict(checkpoints=(-1, 7, 15, 23, 31), backward_exec=(9, 14, 30, 25, 0))
+    for batch, net_b, credit in [(64, 1, 8 << 20), (128, 10000, 16 << 20), (256, 3, 1 << 24)]:
+        kw = dict(batch_size=batch, net_b=net_b, credit=credit, **extra)
+        arr = backward_arrivals(sizes)
+        a = release_groups(ProphetPushQueue(**kw), arr, with_phase=True)
+        b = oracle_release_groups(OracleProphetQueue(**kw), arr, with_phase=True)
+        assert a == b
+        assert sorted(t for _, g in a for t in g) == sorted(arr)
+
+
+def test_native_errors():
+    from prophet_amd.reducer import ReduceError
+    with pytest.raises(ReduceError, match="checkpoints"):
+        ProphetPushQueue(64, 1, 100, checkpoints=(0, 3), backward_exec=(1, 0))
+    with pytest.raises(ReduceError, match="ascend"):
+        ProphetPushQueue(64, 1, 100, checkpoints=(-1, 3, 3), backward_exec=(1, 1, 0))
+    q = ProphetPushQueue(64, 1, 100, checkpoints=(-1, 1, 3), backward_exec=(2, 5, 0))
+    with pytest.raises(ReduceError, match="outside"):
+        q.add_task(PushTask(4, 0, 10))
+    with pytest.raises(ReduceError, match="total_partnum"):
+        q.add_task(PushTask(1, 0, 10, 0))
+    q.add_task(PushTask(3, 0, 10))
+    with pytest.raises(ReduceError, match="pending"):
+        release_groups(q, _arrivals())
+    # credit smaller than a task and nothing reported: no progress
+    q2 = ProphetPushQueue(64, 1, 50, checkpoints=(-1, 1, 3), backward_exec=(0, 0, 0))
+    with pytest.raises(ReduceError, match="no progress"):
+        release_groups(q2, _arrivals(), finish_immediately=False, max_idle=1000)
+
+
+def test_native_defaults_are_the_reference_model():
+    """No checkpoints given: the reference's 157-gradient model (scheduled_queue.h:81-85)."""
+    from prophet_amd.buckets import PROPHET_CHECKPOINTS
+    q = ProphetPushQueue(64, 1, 1 << 30)
+    s = q.state()
+    assert s["pointer"] == 12 and s["expected"] == PROPHET_CHECKPOINTS[-1] == 156
+
+
+def test_native_queue_is_thread_safe():
+    """Transport threads add while an engine thread polls (the queue's mutex,
+    scheduled_queue.cc:95,218): every task leaves exactly once."""
+    import threading
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    arr = backward_arrivals(sizes)
+    q = ProphetPushQueue(64, 10**6, 1 << 40, checkpoints=model_checkpoints(len(sizes)))
+    got = []
+    done = threading.Event()
+
+    def feeder(chunk):
+        for t in chunk:
+            q.add_task(t)
+
+    def poller():
+        while not (done.is_set() and q.pending() == 0):
+            t = q.get_task()
+            if t is not None:
+                got.append(t)
+                q.report_finish(t.len)
+
+    # one feeder keeps backward order (the scheduler collects in that order);
+    # extra FIFO feeders race it
+    fifo = [[PushTask(10_000 + 100 * k + i, 0, 8, scheduled=False) for i in range(50)]
+            for k in range(3)]
+    th = [threading.Thread(target=feeder, args=(arr,))]
+    th += [threading.Thread(target=feeder, args=(c,)) for c in fifo]
+    pt = threading.Thread(target=poller)
+    pt.start()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    done.set()
+    pt.join(timeout=60)
+    assert not pt.is_alive()
+    assert sorted(got) == sorted(arr + [t for c in fifo for t in c])

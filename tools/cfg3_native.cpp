@@ -7,6 +7,12 @@
 // `reps` timed runs of `iters` iterations), fraction of the 8 TB/s roofline at
 // (N+1) x bytes per iteration, run-to-run spread, and exactness against one
 // plan over all partitions.
+// With the task file (tools/cfg3_resnet50_tasks.txt, argv[4]) one more variant
+// runs the native Prophet scheduler (include/bpsr/prophet.h) in the loop: per
+// iteration the 165 partitions arrive in backward order, one per getTask poll,
+// and every release group completes blocks that are released then (one
+// release_range per run of consecutive blocks) — Z_BATCH_SIZE 64, Z_NET_B
+// 10000, Z_CREDIT 16 MiB (tools/bench_configs.py's setting).
 //   hipcc -O2 -std=c++17 -Iinclude -o tools/cfg3_native tools/cfg3_native.cpp \
 //         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd'
 #include <hip/hip_runtime.h>
@@ -19,6 +25,9 @@
 #include <string>
 #include <vector>
 
+#include <chrono>
+
+#include "bpsr/prophet.h"
 #include "bpsr/reduce.h"
 
 #define CK(x)                                                                   \
@@ -71,6 +80,45 @@ Table read_table(const char* path) {
   return t;
 }
 
+struct Tasks {
+  std::vector<int32_t> cps;
+  std::vector<byteps_prophet_task> arrivals;  // backward order; handle = table index
+};
+
+Tasks read_tasks(const char* path) {
+  Tasks t;
+  FILE* f = fopen(path, "r");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path);
+    exit(2);
+  }
+  int nc = 0;
+  if (fscanf(f, "%d", &nc) != 1) exit(2);
+  t.cps.resize(nc);
+  for (auto& c : t.cps)
+    if (fscanf(f, "%d", &c) != 1) exit(2);
+  int g, p, np;
+  long long len;
+  for (uint64_t i = 0; fscanf(f, "%d %d %d %lld", &g, &p, &np, &len) == 4; ++i) {
+    byteps_prophet_task k;
+    std::memset(&k, 0, sizeof(k));
+    k.grad = g;
+    k.part = p;
+    k.total_partnum = np;
+    k.len = len;
+    k.scheduled = 1;
+    k.key = ((uint64_t)g << 16) + (uint64_t)p;
+    k.handle = i;
+    t.arrivals.push_back(k);
+  }
+  fclose(f);
+  std::sort(t.arrivals.begin(), t.arrivals.end(),
+            [](const byteps_prophet_task& a, const byteps_prophet_task& b) {
+              return a.grad != b.grad ? a.grad > b.grad : a.part < b.part;
+            });
+  return t;
+}
+
 struct Set {
   std::vector<char*> in;
   char* out = nullptr;
@@ -97,8 +145,39 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tools/cfg3_resnet50_table.txt";
   const int iters = argc > 2 ? atoi(argv[2]) : 200;
   const int reps = argc > 3 ? atoi(argv[3]) : 7;
+  const char* task_path = argc > 4 ? argv[4] : nullptr;
   const Table t = read_table(path);
   const int nb = (int)t.block_end.size();
+  Tasks tasks;
+  byteps_prophet_queue* sched = nullptr;
+  std::vector<int> block_of(t.parts.size()), block_size(nb);
+  for (int b = 0, i = 0; b < nb; ++b)
+    for (; i < t.block_end[b]; ++i) {
+      block_of[i] = b;
+      ++block_size[b];
+    }
+  if (task_path) {
+    tasks = read_tasks(task_path);
+    if (tasks.arrivals.size() != t.parts.size()) {
+      fprintf(stderr, "task file has %zu partitions, table %zu\n", tasks.arrivals.size(),
+              t.parts.size());
+      return 2;
+    }
+    byteps_prophet_config pc;
+    std::memset(&pc, 0, sizeof(pc));
+    pc.batch_size = 64;
+    pc.net_b = 10000;
+    pc.credit = 16 << 20;
+    pc.checkpoints = tasks.cps.data();
+    pc.ncheckpoints = (int32_t)tasks.cps.size();
+    std::vector<double> ex = {16, 15, 9, 10, 12, 18, 15, 21, 30, 25, 20, 5, 0};
+    if (ex.size() != tasks.cps.size()) return 2;
+    pc.backward_exec = ex.data();  // copied by create
+    CKR(byteps_prophet_create(&pc, &sched));
+  }
+  std::vector<int> left(nb);
+  double sched_us = 0;
+  long sched_iters = 0, groups_seen = 0, release_calls = 0;
   CKR(byteps_reduce_init(0));
   // fp16 inputs: random signs and mantissas, exponents around 1 (finite)
   std::vector<uint16_t> host(t.total / 2);
@@ -163,6 +242,56 @@ int main(int argc, char** argv) {
     for (int b = 0; b < nb; ++b) CKR(byteps_reduce_blockq_release(s.q, b, rel[0]));
     CKR(byteps_reduce_blockq_launch(s.q, cons));
   };
+  // the scheduler in the loop: arrivals one per poll, releases per group
+  const Fn prophet_live = [&](int i) {
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_launch(s.q, cons));
+    const auto t0 = std::chrono::steady_clock::now();
+    CKR(byteps_prophet_reset(sched));
+    for (int b = 0; b < nb; ++b) left[b] = block_size[b];
+    std::vector<char> done(nb, 0);
+    int first_open = 0;  // lowest block not yet released
+    size_t next = 0;
+    bool in_group = false;
+    for (;;) {
+      if (next < tasks.arrivals.size()) CKR(byteps_prophet_add_task(sched, &tasks.arrivals[next++]));
+      byteps_prophet_task got;
+      const int rc = byteps_prophet_get_task(sched, &got, nullptr);
+      if (rc < 0) CKR(rc);
+      if (rc == 1) {
+        in_group = true;
+        const int b = block_of[got.handle];
+        if (--left[b] == 0) done[b] = 1;
+        CKR(byteps_prophet_report_finish(sched, got.len));
+        continue;
+      }
+      if (in_group) {  // end of a release group: release the completed blocks, by runs
+        ++groups_seen;
+        for (int b = 0; b < nb;) {
+          if (done[b] != 1) {
+            ++b;
+            continue;
+          }
+          int e = b;
+          while (e < nb && done[e] == 1) done[e++] = 2;
+          CKR(byteps_reduce_blockq_release_range(s.q, b, e - b, rel[0]));
+          ++release_calls;
+          b = e;
+        }
+        while (first_open < nb && done[first_open] == 2) ++first_open;
+        in_group = false;
+      }
+      uint64_t pend = 0;
+      CKR(byteps_prophet_pending(sched, &pend));
+      if (next >= tasks.arrivals.size() && pend == 0) break;
+    }
+    if (first_open != nb) {
+      fprintf(stderr, "scheduler left blocks unreleased\n");
+      exit(5);
+    }
+    sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ++sched_iters;
+  };
   const Fn plan_no_blocks = [&](int i) {
     CKR(byteps_reduce_plan_launch(sets[i % kSets].plan_blocks, cons));
   };
@@ -170,17 +299,20 @@ int main(int argc, char** argv) {
     const char* name;
     const Fn* fn;
   };
-  const V variants[] = {{"plan_all_partitions_no_blocks", &plan_no_blocks},
-                        {"blockq_pre_released", &pre_released},
-                        {"blockq_live_release", &live},
-                        {"blockq_live_release_2streams", &live_2streams},
-                        {"blockq_live_release_ranges4", &live_ranges},
-                        {"blockq_releases_first_other_stream", &release_first}};
+  std::vector<V> variants = {{"plan_all_partitions_no_blocks", &plan_no_blocks},
+                             {"blockq_pre_released", &pre_released},
+                             {"blockq_live_release", &live},
+                             {"blockq_live_release_2streams", &live_2streams},
+                             {"blockq_live_release_ranges4", &live_ranges},
+                             {"blockq_releases_first_other_stream", &release_first}};
+  if (sched) variants.push_back({"blockq_live_prophet_scheduler", &prophet_live});
   const double alg = (double)(N + 1) * (double)t.total;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (const V& v : variants) {
+    sched_us = 0;
+    sched_iters = groups_seen = release_calls = 0;
     for (int i = 0; i < 30; ++i) (*v.fn)(i);
     CK(hipDeviceSynchronize());
     std::vector<double> ms;
@@ -209,12 +341,16 @@ int main(int argc, char** argv) {
            "\"variant\": \"%s\", \"n_workers\": %d, \"partitions\": %zu, \"blocks\": %d, "
            "\"bytes_per_worker\": %zu, \"iters\": %d, \"reps\": %d, \"ms\": %.5f, "
            "\"min_ms\": %.5f, \"max_ms\": %.5f, \"spread\": %.4f, \"hbm_frac\": %.4f, "
-           "\"status\": %d, \"exact_vs_plan\": %s}\n",
+           "\"status\": %d, \"exact_vs_plan\": %s, \"scheduler_host_us_per_iter\": %.2f, "
+           "\"release_groups_per_iter\": %.2f, \"release_calls_per_iter\": %.2f}\n",
            v.name, N, t.parts.size(), nb, t.total, iters, reps, med, ms.front(), ms.back(),
            (ms.back() - ms.front()) / med, alg / (med * 1e-3) / 8e12, status,
-           exact ? "true" : "false");
+           exact ? "true" : "false", sched_iters ? sched_us / sched_iters : 0.0,
+           sched_iters ? (double)groups_seen / sched_iters : 0.0,
+           sched_iters ? (double)release_calls / sched_iters : 0.0);
     fflush(stdout);
   }
+  if (sched) byteps_prophet_destroy(sched);
   for (auto& s : sets) {
     byteps_reduce_blockq_destroy(s.q);
     byteps_reduce_plan_destroy(s.plan_blocks);
