@@ -95,6 +95,10 @@ def parse(argv=None):
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: launcher/plumbing self-test over gloo with torch's CPU add "
                         "(no HIP; the line is marked and is not a measurement)")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 rehearsal on a 1-GPU box: every rank on cuda:0 with the HIP "
+                        "fold, gloo for the barrier / max-over-ranks (RCCL refuses two ranks "
+                        "on one GPU); no scatter leg; the line is marked, not a measurement")
     return p.parse_args(argv)
 
 
@@ -539,15 +543,19 @@ def main(argv=None):
         print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE",
               file=sys.stderr)
     cuda = args.device == "cuda"
+    rehearse = cuda and args.rehearse_one_gpu and world > 1
+    if rehearse:
+        args.no_scatter = True
+    gpu = 0 if rehearse else local_rank
     if cuda:
         # Bind this rank's GPU before the process group exists, so RCCL's
         # communicator (barrier, the max-over-ranks all_reduce) uses it.
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
     else:
         dev = torch.device("cpu")
     if world > 1:
-        if cuda:
+        if cuda and not rehearse:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
@@ -565,7 +573,7 @@ def main(argv=None):
     n_elems = B // es
     if cuda:
         from prophet_amd.reducer import GpuReducer
-        red = GpuReducer(device=local_rank)
+        red = GpuReducer(device=gpu)
         stream = torch.cuda.current_stream(dev)
 
         def fold_bytes(dst, srcs):
@@ -634,7 +642,7 @@ def main(argv=None):
 
     devices = [f"{local_rank}"]
     if cuda:
-        devices = [f"{local_rank}:{torch.cuda.get_device_name(dev)}"]
+        devices = [f"{gpu}:{torch.cuda.get_device_name(dev)}"]
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, devices[0])
@@ -676,6 +684,9 @@ def main(argv=None):
     }
     if not cuda:
         line["device"] = "cpu plumbing self-test (torch CPU add, gloo): NOT a measurement"
+    if rehearse:
+        line["device"] = (f"rehearsal: {world} ranks sharing cuda:0 over gloo (HIP fold, "
+                          "no RCCL, no scatter leg): NOT a measurement")
 
     def extra_legs():
         if not args.no_scaling:

@@ -1,0 +1,36 @@
+"""bench.py on the GPU at N > 1, rehearsed on one GPU: ``--gpus 2`` starts two
+rank processes (the launcher the driver's scaling run uses), both fold with
+the HIP kernel on cuda:0, gloo carries the barrier and max-over-ranks (RCCL
+refuses two ranks on one GPU), and the config-4 sharded fold runs at world
+size 2 with its G=1 reference measured on rank 0.  One JSON line comes back."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_rehearsed_on_one_gpu():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
+           "--steps", "5", "--warmup", "2", "--bucket-mib", "16", "--no-cpu-baseline",
+           "--scaling-elems", "4000037"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["config"]["devices"]) == 2
+    assert "rehearsal" in line["device"]
+    assert line["check_vs_torch_fold"] is True
+    assert line["roofline"]["kernel_ms"] > 0
+    sc = line["scaling_cfg4"]
+    assert sc["exact_vs_torch_fold"] is True, sc
+    assert sum(sc["shard_elems"]) == 4000037 and len(sc["shard_elems"]) == 2
+    assert sc["g1_fold_ms"] > 0 and sc["per_gpu_fold_ms"] > 0
+    assert "scatter" not in sc
