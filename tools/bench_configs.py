@@ -235,27 +235,59 @@ def cfg3(red, dev, N=8, sets=3):
     # (include/bpsr/reduce.h; under rocprofv3 with both at normal priority the
     # first live launch of each queue waited out its 5-s timeout).
     live_stream = torch.cuda.Stream(priority=-100)
+    nblk = len(by_block)
 
     def blockq_live(i, occ=0):
-        """Consumer launched first on s; the 12 releases follow on another
-        stream (as the push path issues them behind each block's H2D).  The
-        releases are ordered after the previous launch (which re-arms the
-        queue) by an event recorded before this one."""
+        """Consumer launched on live_stream; the 12 releases follow on another
+        stream (as the push path issues them behind each block's H2D).  No
+        cross-stream events: launch k consumes the k-th release of each block
+        (epochs), so iteration k+1 may be issued at once, as from native code
+        (tools/cfg3_native.cpp)."""
         bq = bqs[occ][i % sets]
-        ev = torch.cuda.Event()
-        ev.record(s)
-        rel_stream.wait_event(ev)
-        live_stream.wait_event(ev)
         bq.launch(live_stream)
-        for b in range(len(by_block)):
+        for b in range(nblk):
             bq.release(b, rel_stream)
-        done = torch.cuda.Event()
-        done.record(live_stream)
-        s.wait_event(done)
 
-    bq_variants.append(("prophet_blockq_dispatch_live_release", blockq_live))
-    bq_variants.append(("prophet_blockq_persistent_live_release",
-                        lambda i: blockq_live(i, occ=1)))
+    def blockq_live_ranges(i):
+        """Release groups of 4 blocks, one call and one kernel each."""
+        bq = bqs[0][i % sets]
+        bq.launch(live_stream)
+        for b in range(0, nblk, 4):
+            bq.release_range(b, min(4, nblk - b), rel_stream)
+
+    live_variants = [("prophet_blockq_dispatch_live_release", blockq_live),
+                     ("prophet_blockq_persistent_live_release", lambda i: blockq_live(i, occ=1)),
+                     ("prophet_blockq_dispatch_live_release_ranges4", blockq_live_ranges)]
+    for name, fn in live_variants:
+        ts = []
+        for _ in range(30):
+            fn(_)
+        torch.cuda.synchronize()
+        for r in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(live_stream)
+            t0 = time.perf_counter()
+            for i in range(200):
+                fn(i)
+            host_us = (time.perf_counter() - t0) / 200 * 1e6
+            e1.record(live_stream)
+            torch.cuda.synchronize()
+            ts.append((e0.elapsed_time(e1) / 200, host_us))
+        w, out, _ = data[0]
+        out.zero_()
+        fn(0)
+        fn(1)
+        fn(2)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(out, torch_fold(w, torch.float16)))
+        ms = sorted(t for t, _ in ts)
+        med = ms[len(ms) // 2]
+        emit(config="cfg3", variant=name, driver="python (ctypes), 200 iterations x 5, timed on "
+             "the consumer stream", n_workers=N, tensors=len(sizes), partitions=len(parts),
+             blocks=len(blocks), bytes_per_worker=total, ms=round(med, 4), min_ms=round(ms[0], 4),
+             max_ms=round(ms[-1], 4), host_us_per_iter=round(statistics.median(h for _, h in ts), 1),
+             gibps=round(N * total / (med * 1e-3) / GIB, 1),
+             hbm_frac=round((N + 1) * total / (med * 1e-3) / 8e12, 4), exact=ok)
 
     for name, fn in bq_variants + ([] if VARIANTS == "blockq" else [("per_partition_launch", per_partition),
                      ("prophet_block_batched", per_block),

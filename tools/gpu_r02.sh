@@ -41,19 +41,6 @@ for s in $STEPS; do
             run cfg1py_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy python tools/bench_configs.py --only cfg1 &&
             run cfg1py_both 300 env BPSR_SERVER_PULL_COPY=memcpy BPSR_SERVER_D2H_PRIORITY=normal python tools/bench_configs.py --only cfg1 &&
             run cfg1py_default2 300 python tools/bench_configs.py --only cfg1 ;;
-    cfg1r01) run cfg1py_now_a 300 python tools/bench_configs.py --only cfg1 &&
-             run cfg1py_r01_a 300 bash -c "cd r01ab && python tools/bench_configs.py --only cfg1" &&
-             run cfg1py_now_b 300 python tools/bench_configs.py --only cfg1 &&
-             run cfg1py_r01_b 300 bash -c "cd r01ab && python tools/bench_configs.py --only cfg1" ;;
-    cfg1hyb) run cfg1py_now_a 300 python tools/bench_configs.py --only cfg1 &&
-             run cfg1py_r01_a 300 bash -c "cd r01ab && python tools/bench_configs.py --only cfg1" &&
-             run cfg1py_hyb_a 300 bash -c "cd r01ab_h && python tools/bench_configs.py --only cfg1" &&
-             run cfg1py_hyb_b 300 bash -c "cd r01ab_h && python tools/bench_configs.py --only cfg1" ;;
-    cfg1d2h) run cfg1py_plain_a 300 python tools/bench_configs.py --only cfg1 &&
-             run cfg1py_high_a 300 env BPSR_SERVER_D2H_PRIORITY=high python tools/bench_configs.py --only cfg1 &&
-             run cfg1py_r01_a 300 bash -c "cd r01ab && python tools/bench_configs.py --only cfg1" &&
-             run cfg1py_plain_b 300 python tools/bench_configs.py --only cfg1 &&
-             run cfg1n_plain 300 ./tools/cfg1_native 4 20 ;;
     cfg1pull) run cfg1py_kernel_a 300 python tools/bench_configs.py --only cfg1 &&
              run cfg1py_memcpy_a 300 env BPSR_SERVER_PULL_COPY=memcpy python tools/bench_configs.py --only cfg1 &&
              run cfg1py_kernel_b 300 python tools/bench_configs.py --only cfg1 &&
