@@ -275,6 +275,7 @@ def cfg3(red, dev, N=8, sets=3):
             ts.append((e0.elapsed_time(e1) / 200, host_us))
         w, out, _ = data[0]
         out.zero_()
+        torch.cuda.synchronize()          # the consumer runs on live_stream
         fn(0)
         fn(1)
         fn(2)
