@@ -120,8 +120,10 @@ int byteps_prophet_reset(byteps_prophet_queue* q);
  * successful polls, also split where the phase changes if split_on_phase —
  * with group_phase[g] its phase.  finish_immediately reports each released
  * task finished at once (credit refilled).  group_start needs n+1 entries,
- * group_phase n.  Returns the number of groups; EARGS if max_idle consecutive
- * empty polls pass (no progress possible, e.g. credit smaller than a task). */
+ * group_phase n.  Returns the number of groups; EARGS (nothing added) if an
+ * arrival is invalid, or if max_idle consecutive empty polls pass (no progress
+ * possible, e.g. credit smaller than a task; the queue then keeps what it
+ * holds — reset and drain it, or destroy it). */
 int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_task* arrivals,
                                   size_t n, int finish_immediately, int split_on_phase,
                                   uint64_t max_idle, byteps_prophet_task* released,

@@ -118,17 +118,23 @@ struct byteps_prophet_queue {
     return true;
   }
 
-  int add(const byteps_prophet_task& t) {
+  int validate(const byteps_prophet_task& t) const {
     if (t.len < 0) return bpsr::fail(BYTEPS_REDUCE_EARGS, "task length %lld < 0", (long long)t.len);
-    if (!t.scheduled) {
-      fifo.push_back(t);
-      return 0;
-    }
+    if (!t.scheduled) return 0;
     if (t.grad < 0 || t.grad >= (int32_t)tasks.size())
       return bpsr::fail(BYTEPS_REDUCE_EARGS, "gradient %d outside [0, %d] (the last checkpoint)",
                         t.grad, (int)tasks.size() - 1);
     if (t.total_partnum < 1)
       return bpsr::fail(BYTEPS_REDUCE_EARGS, "total_partnum %d < 1", t.total_partnum);
+    return 0;
+  }
+
+  int add(const byteps_prophet_task& t) {
+    if (const int rc = validate(t)) return rc;
+    if (!t.scheduled) {
+      fifo.push_back(t);
+      return 0;
+    }
     tasks[t.grad].push_back(t);
     tensor_part[t.grad] = t.total_partnum;
     ++nsched;
@@ -243,6 +249,8 @@ int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_
   if (q->nsched + q->fifo.size() > 0)
     return bpsr::fail(BYTEPS_REDUCE_EARGS, "queue must be empty (%llu tasks pending)",
                       (unsigned long long)(q->nsched + q->fifo.size()));
+  for (size_t i = 0; i < n; ++i)  // all or nothing: a bad arrival adds none
+    if (const int rc = q->validate(arrivals[i])) return rc;
   size_t next = 0, nrel = 0;
   int32_t ngroups = 0, cur_phase = 0;
   bool open = false;  // a group is being filled

@@ -262,6 +262,9 @@ def test_native_errors():
         q.add_task(PushTask(4, 0, 10))
     with pytest.raises(ReduceError, match="total_partnum"):
         q.add_task(PushTask(1, 0, 10, 0))
+    with pytest.raises(ReduceError, match="outside"):       # all or nothing
+        release_groups(q, _arrivals() + [PushTask(9, 0, 10)])
+    assert q.pending() == 0
     q.add_task(PushTask(3, 0, 10))
     with pytest.raises(ReduceError, match="pending"):
         release_groups(q, _arrivals())
