@@ -189,23 +189,30 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
     except Exception:
         pass
 
-    def leg(red, threads, budget):
-        def round_once():
-            merged[:] = ins[0]           # stands in for the ps-lite receive buffer
-            t0 = time.perf_counter()
-            for s in ins[1:]:
-                assert red.sum(merged, s, L, dtype_id) == 0
-            red.copy(store, merged, L)
-            return time.perf_counter() - t0
-        for _ in range(2):
-            round_once()
-        ts = []
-        t_begin = time.perf_counter()
-        while len(ts) < 10 or (time.perf_counter() - t_begin < budget and len(ts) < 2000):
-            ts.append(round_once())
-        med = statistics.median(ts)
-        return dict(threads=threads, gibps=n_workers * L / med / GIB, median_s=med,
-                    min_s=min(ts), reps=len(ts))
+    def round_once(red):
+        merged[:] = ins[0]           # stands in for the ps-lite receive buffer
+        t0 = time.perf_counter()
+        for s in ins[1:]:
+            assert red.sum(merged, s, L, dtype_id) == 0
+        red.copy(store, merged, L)
+        return time.perf_counter() - t0
+
+    def legs(impls, slices):
+        """Interleaved timing: each slice runs every implementation for its
+        share of seconds in turn, so a noisy host (other jobs on the box's
+        shared cores) weighs on all of them alike.  Median per implementation."""
+        ts = {k: [] for k in impls}
+        for red, _ in impls.values():
+            for _ in range(2):
+                round_once(red)
+        for _ in range(slices):
+            for k, (red, share) in impls.items():
+                t_s = time.perf_counter()
+                while time.perf_counter() - t_s < share or not ts[k]:
+                    ts[k].append(round_once(red))
+        return {k: dict(gibps=n_workers * L / statistics.median(v) / GIB,
+                        median_s=statistics.median(v), min_s=min(v), reps=len(v))
+                for k, v in ts.items()}
 
     class _Baseline:
         """The restatement in the reference's loop shape (bpsr_oracle_sum_simd:
@@ -220,7 +227,6 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
         def copy(self, d, s, n):
             return self.p.copy(d, s, n)
 
-    default = leg(_Baseline(4), 4, 10.0)
     # the host share this process may use: OMP_NUM_THREADS when the box sets it
     # (16 per GPU on the GPU pool, whose affinity mask shows every host CPU)
     try:
@@ -228,13 +234,18 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
     except ValueError:
         share = 0
     all_threads = max(1, min(share or ncpu, 64))
-    allc = leg(_Baseline(all_threads), all_threads, 4.0)
+    impls = {"port": (_Baseline(4), 1.0), "all": (_Baseline(all_threads), 0.4)}
+    with_ref = dtype_id != 11 and RefReducer.available()
+    if with_ref:
+        impls["ref"] = (RefReducer(nthreads=4), 0.4)
+    res = legs(impls, 10)
+    default, allc = res["port"], res["all"]
     ref = None
-    if dtype_id != 11 and RefReducer.available():
-        r = leg(RefReducer(nthreads=4), 4, 3.0)
+    if with_ref:
+        r = res["ref"]
         ref = {"value": round(r["gibps"], 3), "cores": 4, "reps": r["reps"],
                "what": "the reference's own cpu_reducer.cc built from /root/reference "
-                       "(oracle/_ref), secondary only"}
+                       "(oracle/_ref), secondary only; timed interleaved with the port"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -245,15 +256,16 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
     except OSError:
         pass
     return {
-        "value": round(default["gibps"], 3), "unit": "GiB/s", "cores": default["threads"],
+        "value": round(default["gibps"], 3), "unit": "GiB/s", "cores": 4,
         "kind": "port",
         "sample": (f"{n_workers}-way server round (zero-copy first arrival, {n_workers - 1} "
-                   f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket (the "
-                   f"headline bucket), clean-room restatement oracle/bpsr_oracle.c in the "
+                   f"CpuReducer::sum + 1 copy) of one {L / (1 << 20):.0f} MiB bucket"
+                   f"{' (the headline bucket)' if L == 256 << 20 else ''}, clean-room restatement oracle/bpsr_oracle.c in the "
                    f"reference's omp-simd loop shape (bpsr_oracle_sum_simd), median of "
-                   f"{default['reps']} reps (~10 s of CPU work); 4 OpenMP threads = "
+                   f"{default['reps']} reps (~10 s of CPU work, in 10 slices interleaved "
+                   f"with the other legs); 4 OpenMP threads = "
                    f"BYTEPS_OMP_THREAD_PER_GPU default (cpu_reducer.cc:40-44)"),
-        "all_cores": {"value": round(allc["gibps"], 3), "cores": allc["threads"],
+        "all_cores": {"value": round(allc["gibps"], 3), "cores": all_threads,
                       "reps": allc["reps"]},
         "reference_build": ref,
         "cpu_model": cpu_model, "host_cpus": ncpu,
