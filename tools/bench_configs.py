@@ -153,7 +153,7 @@ def cfg3(red, dev, N=8, sets=3):
     def per_block_graph4(i):
         graphs4[i % sets].replay()
 
-    # Release groups from the Prophet PUSH-queue simulator (scheduled_queue.cc:
+    # Release groups from the native Prophet PUSH scheduler (scheduled_queue.cc:
     # 217-296) at batch 64 and Z_NET_B = 10000 (10 Gb/s in Mb/s), credit 16 MiB:
     # one plan per group, the whole iteration captured in one graph.
     from prophet_amd.prophet import ProphetPushQueue, backward_arrivals, model_checkpoints, \
