@@ -13,6 +13,7 @@
 // and every release group completes blocks that are released then (one
 // release_range per run of consecutive blocks) — Z_BATCH_SIZE 64, Z_NET_B
 // 10000, Z_CREDIT 16 MiB (tools/bench_configs.py's setting).
+//   usage: cfg3_native [table] [iters] [reps] [tasks|""] [variant substring]
 //   hipcc -O2 -std=c++17 -Iinclude -o tools/cfg3_native tools/cfg3_native.cpp \
 //         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd'
 #include <hip/hip_runtime.h>
@@ -145,7 +146,11 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tools/cfg3_resnet50_table.txt";
   const int iters = argc > 2 ? atoi(argv[2]) : 200;
   const int reps = argc > 3 ? atoi(argv[3]) : 7;
-  const char* task_path = argc > 4 ? argv[4] : nullptr;
+  const char* task_path = argc > 4 && argv[4][0] ? argv[4] : nullptr;
+  // optional: run only the variants whose name contains one of argv[5]'s comma-separated substrings (a PMC pass
+  // serialises dispatches, so a live variant's consumer could never see its
+  // releases: profile "pre_released" / "plan" there)
+  const char* only = argc > 5 ? argv[5] : nullptr;
   const Table t = read_table(path);
   const int nb = (int)t.block_end.size();
   Tasks tasks;
@@ -311,6 +316,17 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (const V& v : variants) {
+    if (only) {  // comma-separated substrings
+      bool hit = false;
+      std::string list(only);
+      for (size_t a = 0; a <= list.size();) {
+        size_t b = list.find(',', a);
+        if (b == std::string::npos) b = list.size();
+        if (b > a && std::strstr(v.name, list.substr(a, b - a).c_str())) hit = true;
+        a = b + 1;
+      }
+      if (!hit) continue;
+    }
     sched_us = 0;
     sched_iters = groups_seen = release_calls = 0;
     for (int i = 0; i < 30; ++i) (*v.fn)(i);

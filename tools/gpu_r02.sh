@@ -33,6 +33,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     cfg3n) run cfg3_native 300 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 7 tools/cfg3_resnet50_tasks.txt ;;
+    pmc3)  run pmc_cfg3 400 python tools/pmc_cfg3.py "$OUT/pmc_cfg3" ;;
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
     cfg3py) run cfg3_python 600 python tools/bench_configs.py --only cfg3 ;;
