@@ -36,7 +36,7 @@ def run_pass(counter: str, outdir: str) -> dict:
            os.path.join(ROOT, "tools", "cfg3_native"),
            os.path.join(ROOT, "tools", "cfg3_resnet50_table.txt"), "20", "1", "",
            "plan_all,pre_released"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)  # SIGKILL on expiry
     if r.returncode != 0:
         raise SystemExit(f"pass {counter} rc={r.returncode}\n{r.stderr[-3000:]}")
     vals: dict = {k: {} for k in KERNELS}
