@@ -86,6 +86,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-scaling", action="store_true",
                    help="skip the config-4 (VGG-16 sharded) scaling object")
+    p.add_argument("--no-cfg3", action="store_true",
+                   help="N = 1: skip the config-3 (ResNet-50 fp16 Prophet blocks) object")
     p.add_argument("--no-scatter", action="store_true",
                    help="N > 1: skip the RCCL scatter + all-gather leg of `scaling`")
     p.add_argument("--scaling-elems", type=int, default=0,
@@ -486,6 +488,116 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
 
 
 # --------------------------------------------------------------------------
+# config 3: ResNet-50 fp16 Prophet blocks through the block queue
+
+
+def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 8) -> dict:
+    """BASELINE config 3 on this GPU: 8 workers' ResNet-50 fp16 gradients
+    (161 tensors, 51,114,064 B) cut into the 165 BytePS partitions
+    (operations.cc:99-136) and grouped into the 12 Prophet blocks
+    (scheduled_queue.h:78-79, last checkpoint extended to 160), folded by the
+    block queue: ONE consumer launch per iteration that starts each block once
+    it is released (byteps_reduce_blockq_*).  ``live``: the
+    launch, then the 12 per-block releases from a second stream (as the push
+    path issues them behind each block's pushes); ``pre_released``: every block
+    released before the launch.  Device time per iteration from HIP events on
+    the consumer's stream (median of ``reps`` runs of ``iters`` back-to-back
+    iterations over ``sets`` rotated input sets), host time of the issuing
+    loop, exactness against torch's own left fold."""
+    import torch
+    from prophet_amd.buckets import partition_all, prophet_blocks, resnet50_param_sizes
+    from prophet_amd.dtypes import DType
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    parts = partition_all(sizes)
+    toff = [0]
+    for n in sizes:
+        toff.append(toff[-1] + n)
+    total = toff[-1]
+    by_block = []
+    for blk in prophet_blocks(len(sizes)):
+        tset = set(blk)
+        by_block.append([p for p in parts if p.tensor in tset])
+    gen = torch.Generator(device=dev)
+    data, queues = [], []
+    for i in range(sets):
+        w = []
+        for k in range(N):
+            gen.manual_seed(3000 + 10 * i + k)
+            w.append(torch.randn(total // 2, device=dev, generator=gen).half().view(torch.uint8))
+        out = torch.empty(total, dtype=torch.uint8, device=dev)
+        data.append((w, out))
+        q = red.make_blockq([[(out[toff[p.tensor] + p.offset:][:p.len],
+                               [x[toff[p.tensor] + p.offset:][:p.len] for x in w], p.len)
+                              for p in bp] for bp in by_block], DType.FLOAT16)
+        q.config(wg_per_cu=0, timeout_s=1.0)
+        queues.append(q)
+    # the consumer outranks the release stream: its own hardware queue
+    live_s = torch.cuda.Stream(device=dev, priority=-100)
+    rel_s = torch.cuda.Stream(device=dev)
+    nb = len(by_block)
+
+    def live(i):
+        q = queues[i % sets]
+        q.launch(live_s)
+        for b in range(nb):
+            q.release(b, rel_s)
+
+    def pre_released(i):
+        q = queues[i % sets]
+        q.release(-1, live_s)
+        q.launch(live_s)
+
+    # probe: one live iteration must complete before anything is timed (a
+    # profiler that serialises dispatches would strand the consumer; it then
+    # gives up after its 1-s timeout and status() raises, ending this leg)
+    live(0)
+    torch.cuda.synchronize()
+    queues[0].status(live_s)
+    alg = (N + 1) * total
+    res = {"workload": (f"config 3: {N}-way fp16 ResNet-50 ({total} B per worker), "
+                        f"{len(parts)} partitions in {nb} Prophet blocks, block queue "
+                        "(one consumer launch per iteration)"),
+           "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
+    for name, fn in (("live", live), ("pre_released", pre_released)):
+        for i in range(30):
+            fn(i)
+        torch.cuda.synchronize()
+        ts, hs = [], []
+        for _ in range(reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(live_s)
+            t0 = time.perf_counter()
+            for i in range(iters):
+                fn(i)
+            hs.append((time.perf_counter() - t0) / iters * 1e6)
+            e1.record(live_s)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / iters)
+        ms = statistics.median(ts)
+        res[name] = {"ms_per_iter": round(ms, 5), "min_ms": round(min(ts), 5),
+                     "spread": round((max(ts) - min(ts)) / ms, 4),
+                     "frac_of_roofline": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "host_us_per_iter": round(statistics.median(hs), 1)}
+    for q in queues:
+        q.status(live_s)
+    ok = True
+    for i, (w, out) in enumerate(data):
+        out.zero_()
+        torch.cuda.synchronize()
+        live(i)
+        torch.cuda.synchronize()
+        ref = w[0].view(torch.float16).clone()
+        for x in w[1:]:
+            ref.add_(x.view(torch.float16))
+        ok = ok and bool(torch.equal(ref.view(torch.uint8), out))
+    res["exact_vs_torch_fold"] = ok
+    for q in queues:
+        q.close()
+    return res
+
+
+# --------------------------------------------------------------------------
 # provenance of roofline.traffic
 
 
@@ -717,6 +829,11 @@ def main(argv=None):
 
     if world == 1:
         extra_legs()
+        if cuda and not args.no_cfg3:
+            try:
+                line["cfg3_blockq"] = cfg3_leg(dev, red)
+            except Exception as e:  # report, never hide
+                line["cfg3_blockq"] = {"error": repr(e)}
         if rank == 0 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)
