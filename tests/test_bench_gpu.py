@@ -34,3 +34,26 @@ def test_bench_two_ranks_rehearsed_on_one_gpu():
     assert sum(sc["shard_elems"]) == 4000037 and len(sc["shard_elems"]) == 2
     assert sc["g1_fold_ms"] > 0 and sc["per_gpu_fold_ms"] > 0
     assert "scatter" not in sc
+
+
+def test_bench_one_gpu_line_has_every_object():
+    """The N = 1 line the driver records: headline fold checked, the config-4
+    scaling object and the config-3 block-queue object present and exact (a
+    leg that raised would carry an "error" field instead)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
+           "--bucket-mib", "16", "--no-cpu-baseline", "--scaling-elems", "4000037"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["check_vs_torch_fold"] is True
+    assert "device" not in line                      # a measurement, not a self-test
+    assert line["scaling_cfg4"]["exact_vs_torch_fold"] is True
+    c3 = line["cfg3_blockq"]
+    assert "error" not in c3, c3
+    assert c3["exact_vs_torch_fold"] is True
+    for k in ("live", "pre_released"):
+        assert 0 < c3[k]["frac_of_roofline"] < 1
