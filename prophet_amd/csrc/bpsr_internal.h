@@ -7,6 +7,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "bpsr_error.h"
+
 namespace bpsr {
 
 // dtype ids: byteps/common/common.h:52-65 + bf16 extension (include/bpsr/reduce.h)
@@ -164,9 +166,8 @@ void stage_ring_destroy(StageRing* r);
 int batched_with_ring(const struct byteps_bucket_desc* buckets, int nbuckets, int dtype,
                       int mode, hipStream_t s, StageRing* ring);
 
-// Thread-local error reporting shared by every C-ABI entry point
-// (byteps_reduce_last_error): returns `code`.
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+// Thread-local error reporting (byteps_reduce_last_error): fail() is in
+// bpsr_error.h; hip_fail formats a HIP error the same way.
 int hip_fail(hipError_t e, const char* what);
 
 // Host-side geometry: vector range, head/tail split (fp16 body/tail rule of

@@ -14,7 +14,7 @@
 #include <vector>
 
 #include "bpsr/prophet.h"
-#include "bpsr_internal.h"
+#include "bpsr_error.h"
 
 namespace {
 
