@@ -20,15 +20,18 @@ from prophet_amd import reducer
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_engine_queue_schedule_order(tmp_path):
+@pytest.mark.parametrize("san", [None, "thread", "address,undefined"])
+def test_engine_queue_schedule_order(tmp_path, san):
     exe = tmp_path / "engine_queue_check"
-    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-pthread",
+    flags = [f"-fsanitize={san}", "-g"] if san else []
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-pthread", *flags,
                     "-I", os.path.join(ROOT, "prophet_amd", "csrc"),
                     os.path.join(ROOT, "tests", "cpp", "engine_queue_check.cpp"), "-o", str(exe)],
                    check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "fails=0" in r.stdout
+    assert "Sanitizer" not in r.stderr, r.stderr[-4000:]
 
 
 def test_set_tuning_from_threads_never_tears():
