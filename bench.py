@@ -86,6 +86,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-scaling", action="store_true",
                    help="skip the config-4 (VGG-16 sharded) scaling object")
+    p.add_argument("--no-fp16", action="store_true",
+                   help="N = 1: skip the fp16 run of the headline workload")
     p.add_argument("--no-cfg3", action="store_true",
                    help="N = 1: skip the config-3 (ResNet-50 fp16 Prophet blocks) object")
     p.add_argument("--no-scatter", action="store_true",
@@ -488,6 +490,52 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
 
 
 # --------------------------------------------------------------------------
+# the metric's other dtype: the same bucket in fp16
+
+
+def fp16_leg(dev, red, N: int, B: int, steps: int, sets: int = 3) -> dict:
+    """The headline workload in fp16 (the metric names fp32/fp16): N workers'
+    B-byte fp16 buckets in the same skewed arena, folded with the reference's
+    fp16 rule (fp32 add, RNE to fp16 after every add — cpu_reducer.cc:94-128).
+    HIP-event time per launch on the launch stream; bit-exact check against
+    torch's own half-precision left fold (it rounds after every add too)."""
+    import torch
+    from prophet_amd.arena import BucketArena
+    from prophet_amd.dtypes import DType
+    stream = torch.cuda.current_stream(dev)
+    gen = torch.Generator(device=dev)
+    data = []
+    for s in range(sets):
+        slots = BucketArena(N + 1, B, dev).slots()
+        for k in range(N):
+            gen.manual_seed(5000 + 31 * s + k)
+            slots[k].view(torch.float16).copy_(
+                torch.randn(B // 2, device=dev, generator=gen).half())
+        data.append((slots[N], slots[:N]))
+    clock = _Clock(dev)
+
+    def step(i):
+        dst, srcs = data[i % sets]
+        red.sum_n(dst, srcs, B, DType.FLOAT16, stream=stream)
+    for i in range(3):
+        step(i)
+    clock.sync()
+    ms = clock.time(step, steps)
+    dst, srcs = data[(steps - 1) % sets]
+    step(steps - 1)
+    clock.sync()
+    ref = srcs[0].view(torch.float16).clone()
+    for x in srcs[1:]:
+        ref.add_(x.view(torch.float16))
+    ok = bool(torch.equal(ref.view(torch.uint8), dst))
+    alg = (N + 1) * B
+    return {"workload": f"{N}-way f16 left-fold sum of one {B / (1 << 20):.0f} MiB bucket",
+            "kernel_ms": round(ms, 5), "value_GiBps": round(N * B / (ms * 1e-3) / GIB, 1),
+            "frac_of_roofline": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "exact_vs_torch_fold": ok, "steps": steps}
+
+
+# --------------------------------------------------------------------------
 # config 3: ResNet-50 fp16 Prophet blocks through the block queue
 
 
@@ -829,6 +877,11 @@ def main(argv=None):
 
     if world == 1:
         extra_legs()
+        if cuda and args.dtype == "f32" and mode == 0 and not args.no_fp16:
+            try:
+                line["fp16"] = fp16_leg(dev, red, N, B, args.steps)
+            except Exception as e:  # report, never hide
+                line["fp16"] = {"error": repr(e)}
         if cuda and not args.no_cfg3:
             try:
                 line["cfg3_blockq"] = cfg3_leg(dev, red)

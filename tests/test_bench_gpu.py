@@ -52,6 +52,9 @@ def test_bench_one_gpu_line_has_every_object():
     assert line["n_gpus"] == 1 and line["check_vs_torch_fold"] is True
     assert "device" not in line                      # a measurement, not a self-test
     assert line["scaling_cfg4"]["exact_vs_torch_fold"] is True
+    f16 = line["fp16"]
+    assert "error" not in f16, f16
+    assert f16["exact_vs_torch_fold"] is True and 0 < f16["frac_of_roofline"] < 1
     c3 = line["cfg3_blockq"]
     assert "error" not in c3, c3
     assert c3["exact_vs_torch_fold"] is True

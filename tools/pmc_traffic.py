@@ -64,7 +64,7 @@ def main():
                    help="session tag recorded with the numbers (bench line traffic_source)")
     p.add_argument("bench_args", nargs="*",
                    default=["--steps", "12", "--warmup", "2", "--no-cpu-baseline",
-                            "--no-scaling", "--no-cfg3"])
+                            "--no-scaling", "--no-cfg3", "--no-fp16"])
     a = p.parse_args()
     os.makedirs(a.out, exist_ok=True)
     fetch, bl = run_pass("FETCH_SIZE", a.out, a.bench_args)
