@@ -33,6 +33,14 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     cfg3n) run cfg3_native 300 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 7 tools/cfg3_resnet50_tasks.txt ;;
+    dtypes) for spec in "f32 reference 8" "f64 reference 8" "f16 reference 8" "bf16 reference 8" \
+                        "i32 reference 8" "i64 reference 8" "u8 reference 8" "i8 reference 8" \
+                        "f16 accum 8" "bf16 accum 8" "f32 reference 16" "bf16 reference 16" \
+                        "f32 reference 2"; do
+              set -- $spec
+              run dt_$1_$2_$3 200 python bench.py --dtype $1 --mode $2 --workers $3 --steps 50 \
+                  --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 || exit 1
+            done ;;
     pmc3)  run pmc_cfg3 400 python tools/pmc_cfg3.py "$OUT/pmc_cfg3" ;;
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
