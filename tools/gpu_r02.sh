@@ -41,6 +41,7 @@ for s in $STEPS; do
               run dt_$1_$2_$3 200 python bench.py --dtype $1 --mode $2 --workers $3 --steps 50 \
                   --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 || exit 1
             done ;;
+    configs) run configs 900 python tools/bench_configs.py --only cfg1,sweep,cfg4,cfg5,cfg2e2e ;;
     pmc3)  run pmc_cfg3 400 python tools/pmc_cfg3.py "$OUT/pmc_cfg3" ;;
     cfg3prof) run cfg3_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$OUT/cfg3prof" -o cfg3 -- ./tools/cfg3_native tools/cfg3_resnet50_table.txt 100 3 ;;
