@@ -35,7 +35,7 @@ def main():
     did = {"f32": DType.FLOAT32, "f16": DType.FLOAT16}[a.dtype]
     N = a.workers
     for mib in [float(x) for x in a.mib.split(",")]:
-        B = int(mib * (1 << 20))
+        B = int(mib * (1 << 20)) // 16 * 16
         sets = 3
         data = []
         for _ in range(sets):
