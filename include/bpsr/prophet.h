@@ -129,6 +129,26 @@ int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_
                                   uint64_t max_idle, byteps_prophet_task* released,
                                   int32_t* group_start, int32_t* group_phase);
 
+/* Prophet's pre-run profile (scheduled_queue.cc:110-167, the Global::pre_run
+ * branch of addTask_helper): from the first time each gradient reached the
+ * PUSH queue in one profiled iteration (tic_us[i] for gradient i, µs, any
+ * epoch), derive the block boundaries and the per-block budgets that the
+ * constructor then scales (:26-33):
+ *   gaps x_i = |tic[i] - tic[i-1]|, i = 1..ngrad-1; avg = 2 x their mean;
+ *   checkpoints = -1, then i-1 for every i whose gap exceeds avg (ascending),
+ *   then ngrad-1;
+ *   backward_exec (ms) = the qualifying gaps / 1000, LAST i first, then
+ *   |tic[i0-1] - tic[0]| / 1000 for the first qualifying i0 — one entry per
+ *   block in the order getTask opens them — padded with a final 0 so it has
+ *   one entry per checkpoint, as byteps_prophet_config wants.
+ * Deviation: with no qualifying gap the reference leaves backward_exec empty
+ * and getTask reads past it (:240); here the one block gets the whole span
+ * |tic[ngrad-1] - tic[0]| / 1000.  Writes at most `cap` entries to each
+ * array; returns the number of checkpoints (EARGS if ngrad < 1, a tic is
+ * negative, or cap is too small). */
+int byteps_prophet_profile(const int64_t* tic_us, int32_t ngrad, int32_t* checkpoints,
+                           double* backward_exec, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -193,3 +193,32 @@ def oracle_release_groups(queue: OracleProphetQueue, arrivals, finish_immediatel
         if idle > max_idle:
             raise RuntimeError("scheduler made no progress")
     return groups
+
+
+def oracle_profile(tic_us):
+    """Pre-run profile (scheduled_queue.cc:110-167): first-arrival time of each
+    gradient (µs) -> (checkpoints, backward_exec in ms, padded with a final 0).
+    With no gap above twice the mean gap the reference leaves backward_exec
+    empty (and getTask reads past it); here the one block gets the whole span."""
+    n = len(tic_us)
+    if n < 1 or any(t < 0 for t in tic_us):
+        raise ValueError("need >= 1 non-negative tics")
+    avg = 0.0
+    for i in range(1, n):
+        x = abs(float(tic_us[i] - tic_us[i - 1]))
+        avg = ((i - 1) / i) * avg + (1.0 / i) * x
+    avg *= 2
+    cps, ex = [-1], []
+    for i in range(1, n):
+        diff = abs(float(tic_us[i] - tic_us[i - 1]))
+        if diff > avg:
+            diff /= 1000
+            if not ex:
+                ex.append(abs(float(tic_us[i - 1] - tic_us[0])) / 1000)
+            cps.append(i - 1)
+            ex.insert(0, diff)
+    cps.append(n - 1)
+    if not ex:
+        ex.append(abs(float(tic_us[n - 1] - tic_us[0])) / 1000)
+    ex.append(0.0)
+    return tuple(cps), tuple(ex)

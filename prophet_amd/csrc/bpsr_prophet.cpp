@@ -7,6 +7,7 @@
 // lookup, and equal priorities keep insertion order), the 160-entry arrays are
 // sized by the model's last checkpoint, the stack holds gradient indices.
 #include <climits>
+#include <cmath>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -289,6 +290,46 @@ int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_
   }
   if (ngroups == 0) group_start[0] = 0;
   return ngroups;
+}
+
+int byteps_prophet_profile(const int64_t* tic_us, int32_t ngrad, int32_t* checkpoints,
+                           double* backward_exec, int32_t cap) {
+  if (!tic_us || !checkpoints || !backward_exec || ngrad < 1)
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "null array or ngrad < 1");
+  for (int32_t i = 0; i < ngrad; ++i)
+    if (tic_us[i] < 0) return bpsr::fail(BYTEPS_REDUCE_EARGS, "tic of gradient %d < 0", i);
+  // :129-135 running mean of the gaps, doubled
+  double avg = 0;
+  for (int32_t i = 1; i < ngrad; ++i) {
+    const double x = std::fabs((double)(tic_us[i] - tic_us[i - 1]));
+    avg = ((double)(i - 1) / i) * avg + (1.0 / i) * x;
+  }
+  avg *= 2;
+  // :136-152
+  std::vector<int32_t> cps{-1};
+  std::deque<double> ex;
+  for (int32_t i = 1; i < ngrad; ++i) {
+    double diff = std::fabs((double)(tic_us[i] - tic_us[i - 1]));
+    if (diff > avg) {
+      diff /= 1000;
+      if (ex.empty()) ex.push_back(std::fabs((double)(tic_us[i - 1] - tic_us[0])) / 1000);
+      cps.push_back(i - 1);
+      ex.push_front(diff);
+    }
+  }
+  cps.push_back(ngrad - 1);
+  if (ex.empty()) ex.push_back(std::fabs((double)(tic_us[ngrad - 1] - tic_us[0])) / 1000);
+  ex.push_back(0);  // one entry per checkpoint (the last is never opened)
+  if (cps.size() > (size_t)cap || ex.size() > (size_t)cap)
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "cap %d < %zu checkpoints", cap, cps.size());
+  if (cps.size() != ex.size())
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "internal: %zu checkpoints, %zu exec entries",
+                      cps.size(), ex.size());
+  for (size_t i = 0; i < cps.size(); ++i) {
+    checkpoints[i] = cps[i];
+    backward_exec[i] = ex[i];
+  }
+  return (int)cps.size();
 }
 
 }  // extern "C"

@@ -62,6 +62,7 @@ PROPHET_EXPORTS = (
     "byteps_prophet_create", "byteps_prophet_destroy", "byteps_prophet_add_task",
     "byteps_prophet_get_task", "byteps_prophet_report_finish", "byteps_prophet_pending",
     "byteps_prophet_get_state", "byteps_prophet_reset", "byteps_prophet_release_groups",
+    "byteps_prophet_profile",
 )
 
 _BOUND = None
@@ -85,6 +86,8 @@ def _lib():
         L.byteps_prophet_pending.argtypes = [vp, P(ctypes.c_uint64)]
         L.byteps_prophet_get_state.argtypes = [vp, P(_State)]
         L.byteps_prophet_reset.argtypes = [vp]
+        L.byteps_prophet_profile.argtypes = [P(ctypes.c_int64), ctypes.c_int32,
+                                             P(ctypes.c_int32), P(ctypes.c_double), ctypes.c_int32]
         L.byteps_prophet_release_groups.argtypes = [
             vp, P(_Task), ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
             P(_Task), P(ctypes.c_int32), P(ctypes.c_int32)]
@@ -167,6 +170,25 @@ class ProphetPushQueue:
         return {f: getattr(s, f) for f, _ in _State._fields_}
 
 
+def profile_checkpoints(tic_us) -> tuple[tuple, tuple]:
+    """Prophet's pre-run profile (scheduled_queue.cc:110-167), native
+    (``byteps_prophet_profile``): the first time each gradient i reached the
+    PUSH queue in one profiled iteration (``tic_us[i]``, microseconds) ->
+    ``(checkpoints, backward_exec)`` for ``ProphetPushQueue``: a block boundary
+    wherever the gap before a gradient exceeds twice the mean gap, each block's
+    budget the compute gap that follows it (ms; the constructor scales it by
+    batch/64 and Z_NET_B * 125)."""
+    L = _lib()
+    n = len(tic_us)
+    tics = (ctypes.c_int64 * max(n, 1))(*[int(t) for t in tic_us])
+    cap = n + 2
+    cps = (ctypes.c_int32 * cap)()
+    ex = (ctypes.c_double * cap)()
+    k = L.byteps_prophet_profile(tics, n, cps, ex, cap)
+    _ck(k)
+    return tuple(cps[:k]), tuple(ex[:k])
+
+
 def model_checkpoints(n_tensors: int, checkpoints=PROPHET_CHECKPOINTS) -> tuple:
     """The reference hard-codes a 157-gradient model; a model with more
     gradients gets its last checkpoint extended to ``n_tensors - 1`` (same rule
@@ -224,4 +246,5 @@ def release_groups(queue: ProphetPushQueue, arrivals, finish_immediately: bool =
 
 
 __all__ = ["PushTask", "ProphetPushQueue", "BACKWARD_EXEC", "PHASE_CREDIT", "PHASE_FIFO",
-           "model_checkpoints", "backward_arrivals", "release_groups", "PROPHET_EXPORTS"]
+           "model_checkpoints", "backward_arrivals", "release_groups", "profile_checkpoints",
+           "PROPHET_EXPORTS"]

@@ -319,3 +319,77 @@ def test_native_queue_is_thread_safe():
     pt.join(timeout=60)
     assert not pt.is_alive()
     assert sorted(got) == sorted(arr + [t for c in fifo for t in c])
+
+
+# ------------------------------------------------------------ pre-run profile
+from oracle.prophet_oracle import oracle_profile  # noqa: E402
+from prophet_amd.prophet import profile_checkpoints  # noqa: E402
+
+
+def test_profile_hand_trace():
+    """10 gradients, gaps of 100 us except 2,000 before gradient 3 and 5,000
+    before gradient 7 (tic = first arrival, gradient 9 first in backward).
+    mean gap = (7*100 + 2000 + 5000)/9 = 855.6, doubled 1711.1: both big gaps
+    qualify -> checkpoints -1, 2, 6, 9; exec (ms) = gap before 7, gap before
+    3, then tic[2]-tic[0] for the bottom block, then the 0 pad."""
+    gaps = {i: 100 for i in range(1, 10)}
+    gaps[3], gaps[7] = 2000, 5000
+    tic = [0] * 10
+    t = 1_000_000
+    for i in range(9, -1, -1):          # backward: gradient 9 ready first
+        tic[i] = t
+        if i:
+            t += gaps[i]
+    want = ((-1, 2, 6, 9), (5.0, 2.0, 0.2, 0.0))
+    assert oracle_profile(tic) == want
+    assert profile_checkpoints(tic) == want
+
+
+def test_profile_no_gap_one_block():
+    tic = [1000 + 10 * (4 - i) for i in range(5)]      # uniform gaps
+    assert oracle_profile(tic) == ((-1, 4), (0.04, 0.0))
+    assert profile_checkpoints(tic) == oracle_profile(tic)
+    assert profile_checkpoints([7]) == ((-1, 0), (0.0, 0.0))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_profile_native_equals_oracle(seed):
+    rng = random.Random(seed)
+    n = rng.randint(1, 200)
+    t, tic = rng.randint(0, 10**9), [0] * n
+    for i in range(n - 1, -1, -1):
+        tic[i] = t
+        t += rng.choice([rng.randint(0, 300), rng.randint(0, 300), rng.randint(500, 20000)])
+    if rng.random() < 0.2:
+        rng.shuffle(tic)                                   # arbitrary arrival order
+    assert profile_checkpoints(tic) == oracle_profile(tic)
+
+
+def test_profiled_schedule_runs_an_iteration(impl):
+    """The profile's output drives the queue: a ResNet-50-sized model whose
+    profiled backward has four long compute gaps gets five blocks, and every
+    partition is released exactly once with the per-block budgets honoured."""
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    n = len(sizes)
+    tic, t = [0] * n, 0
+    for i in range(n - 1, -1, -1):
+        tic[i] = t
+        t += 4000 if i in (30, 70, 110, 140) else 150
+    cps, ex = profile_checkpoints(tic)
+    assert cps == (-1, 29, 69, 109, 139, 160) and len(ex) == len(cps)
+    q = _mk(impl, batch_size=64, net_b=100, credit=8 << 20, checkpoints=cps, backward_exec=ex)
+    arr = backward_arrivals(sizes)
+    phased = impl[1](q, arr, with_phase=True)
+    flat = [t for _, g in phased for t in g]
+    assert sorted(flat) == sorted(arr)
+    for ph, g in phased:
+        if ph != "credit":
+            assert sum(t.len for t in g) < ex[ph] * 100 * 125
+
+
+def test_profile_errors():
+    from prophet_amd.reducer import ReduceError
+    with pytest.raises(ReduceError):
+        profile_checkpoints([])
+    with pytest.raises(ReduceError, match="< 0"):
+        profile_checkpoints([5, -1])
