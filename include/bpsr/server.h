@@ -116,6 +116,18 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
  * The caller must not write through the view. */
 int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** data, size_t* len);
 
+/* Zero-copy pull for a transport that sends straight from HBM (GPUDirect RDMA
+ * into the NIC, or a device-side consumer): blocks like byteps_server_pull
+ * until the key's round is finished and its fold has completed, then sets
+ * *data to the key's store in DEVICE memory (*len = key length) and counts
+ * the pull.  No copy at all — the device counterpart of SendPullResponse
+ * answering with an SArray over the store (server.cc:42-70).  Sync mode only
+ * (EARGS in async mode: every push rewrites the store).  The view stays valid
+ * until this worker's next push of the key (the next round cannot finish
+ * without it); the caller must not write through it. */
+int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** data,
+                                   size_t* len);
+
 /* Non-blocking pull for a transport's receive thread: the reference's default
  * non-blocking engine queues a pull that arrives before the round has finished
  * (q_pull_reqmeta_, server.cc:286-305) and the engine thread answers it once

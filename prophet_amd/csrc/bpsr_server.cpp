@@ -983,6 +983,37 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   return BYTEPS_REDUCE_OK;
 }
 
+int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** data,
+                                   size_t* len) {
+  if (!s || !data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  *data = nullptr;
+  if (len) *len = 0;
+  if (s->cfg.async_mode)
+    return fail(BYTEPS_REDUCE_EARGS, "device views need sync mode (async pushes rewrite the store)");
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = key_for_pull(s, key);
+  if (!ks) return BYTEPS_REDUCE_EARGS;
+  std::unique_lock<std::mutex> lk(ks->mu);
+  ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  if (ks->error) return key_error(ks);
+  // The round is published only after its fold (or the lane's batch mark
+  // behind it) was recorded, so this event covers the store's last write.
+  const bool has = ks->has_done;
+  hipEvent_t ev = ks->fold_ev;
+  const void* view = ks->store;
+  lk.unlock();
+  if (has) {
+    hipError_t e = hipEventSynchronize(ev);
+    if (e != hipSuccess) return hip_fail(e, "store fold sync");
+  }
+  lk.lock();
+  count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
+  *data = view;
+  if (len) *len = ks->len;
+  return BYTEPS_REDUCE_OK;
+}
+
 int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_cb cb,
                              void* ctx) {
   if (!s || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");

@@ -23,7 +23,7 @@ SERVER_EXPORTS = (
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
     "byteps_server_debug_lane", "byteps_server_push_ready_many", "byteps_server_push_many",
-    "byteps_server_pull_many",
+    "byteps_server_pull_many", "byteps_server_pull_device_view",
 )
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
@@ -51,6 +51,8 @@ def _lib():
         L.byteps_server_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
         L.byteps_server_pull_host_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
                                                    ctypes.POINTER(_sz)]
+        L.byteps_server_pull_device_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
+                                                     ctypes.POINTER(_sz)]
         L.byteps_server_pull_async.argtypes = [_vp, _u64, PULL_CB, _vp]
         L.byteps_server_push_async.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int, PUSH_CB,
                                                _vp]
@@ -149,6 +151,17 @@ class PSServer:
                                                      ctypes.byref(n)))
         buf = (ctypes.c_char * n.value).from_address(p.value)
         return memoryview(buf).cast("B").toreadonly()
+
+    def pull_device_view(self, key: int) -> tuple[int, int]:
+        """Zero-copy pull from HBM (byteps_server_pull_device_view): blocks until
+        the round is finished and folded, counts the pull, and returns
+        ``(device_pointer, nbytes)`` of the key's store — what a GPUDirect
+        transport would send from.  Sync mode only; valid until this worker's
+        next push of the key; read-only."""
+        p, n = _vp(), _sz()
+        _check(self.lib.byteps_server_pull_device_view(self.handle, key, ctypes.byref(p),
+                                                       ctypes.byref(n)))
+        return int(p.value), int(n.value)
 
     def pull_async(self, key: int, callback) -> None:
         """Non-blocking pull (byteps_server_pull_async; server.cc:286-305 queues

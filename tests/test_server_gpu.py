@@ -777,3 +777,90 @@ def test_batched_calls_async_mode(port):
     for o in outs:
         assert (o == 6).all()
     srv.close()
+
+
+def _read_device(red, ptr, nbytes):
+    out = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    red.copy(out, ptr, nbytes)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("batched", [False, True], ids=["single", "push_many"])
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+def test_pull_device_view_rounds(port, policy, batched):
+    """byteps_server_pull_device_view: the store's own HBM, no copy (what a
+    GPUDirect transport sends from).  Every round's view is bit-exact with the
+    oracle's fold in arrival order — pushes one by one or through push_many
+    (one batched fold per lane, the round published behind the lane's mark);
+    views and copying pulls count toward the same re-arm (server.cc:105-113)."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    red = GpuReducer(device=0)
+    dt, N = DType.FLOAT32, 3
+    sizes = [3, 1_000_003, 4_096_000 // 4]
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2, policy=policy)
+    _init_round(srv, dt, N, sizes)
+    for rnd in range(1, 5):
+        order = random.Random(rnd).sample(range(N), N)
+        for w in order:
+            if batched:
+                srcs = [torch.from_numpy(data(dt, n, w, rnd, j)).cuda()
+                        for j, n in enumerate(sizes)]
+                torch.cuda.synchronize()               # the server's copies use its own streams
+                srv.push_many(list(range(len(sizes))), w, srcs, dt)
+                torch.cuda.synchronize()
+                del srcs
+            else:
+                for j, n in enumerate(sizes):
+                    srv.push(j, w, data(dt, n, w, rnd, j), dt)
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, rnd, j) for w in order], n * es, dt)
+            for w in range(N):
+                if w == 0 and rnd % 2:                 # a copying pull counts too
+                    out = np.zeros(n * es, np.uint8)
+                    srv.pull(j, out)
+                    got = out
+                else:
+                    ptr, nb = srv.pull_device_view(j)
+                    assert nb == n * es and ptr
+                    got = _read_device(red, ptr, nb)
+                assert np.array_equal(got, want), f"round {rnd} key {j} worker {w}"
+    srv.close()
+
+
+def test_pull_device_view_held_until_own_push(port):
+    """A worker's device view still holds round r while the other workers push
+    round r + 1 — the store is rewritten only by the fold its own push
+    completes — and async mode refuses device views."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    red = GpuReducer(device=0)
+    dt, N, n = DType.FLOAT32, 3, 500_001
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=1)
+    _init_round(srv, dt, N, [n])
+    for w in range(N):
+        srv.push(0, w, data(dt, n, w, 1, 0), dt)
+    want1 = np.zeros(n * es, np.uint8)
+    port.sum_n(want1, [data(dt, n, w, 1, 0) for w in range(N)], n * es, dt)
+    views = [srv.pull_device_view(0) for _ in range(N)]      # every worker pulls round 1
+    assert len({p for p, _ in views}) == 1
+    ptr, nb = views[-1]
+    for w in range(N - 1):                                    # round 2 without worker N-1
+        srv.push(0, w, data(dt, n, w, 2, 0), dt)
+    torch.cuda.synchronize()
+    assert np.array_equal(_read_device(red, ptr, nb), want1)   # still round 1
+    srv.push(0, N - 1, data(dt, n, N - 1, 2, 0), dt)            # completes round 2
+    want2 = np.zeros(n * es, np.uint8)
+    port.sum_n(want2, [data(dt, n, w, 2, 0) for w in range(N)], n * es, dt)
+    p2, _ = srv.pull_device_view(0)
+    assert np.array_equal(_read_device(red, p2, nb), want2)
+    srv.close()
+    from prophet_amd.reducer import ReduceError
+    with PSServer(2, async_mode=True) as a:
+        _init_round(a, dt, 2, [16])
+        with pytest.raises(ReduceError, match="sync mode"):
+            a.pull_device_view(0)
