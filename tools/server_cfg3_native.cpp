@@ -10,7 +10,10 @@
 //   push_d2d     each worker thread pushes from its own device buffer
 //                (byteps_server_push_async, D2D copy into the slot);
 //   ..._many     the same through the batched calls (byteps_server_push_ready_many
-//                / push_many, then pull_many): one launch per lane per call.
+//                / push_many, then pull_many): one launch per lane per call;
+//   ...+device_view  pulls as zero-copy device views of the store
+//                (byteps_server_pull_device_view: what a GPUDirect transport
+//                sends from); one extra round with copying pulls checks the bits.
 // Every round ends when every worker has pulled every key (device pulls).
 // Worker threads persist across rounds (a transport's receive threads).
 //   hipcc -O2 -std=c++17 -Iinclude -o tools/server_cfg3_native tools/server_cfg3_native.cpp \
@@ -88,17 +91,20 @@ int main(int argc, char** argv) {
   }
   const double alg = (double)(N + 1) * (double)total;
   const char* names[] = {"push_ready", "push_d2d", "push_ready_many+pull_many",
-                         "push_many_d2d+pull_many"};
+                         "push_many_d2d+pull_many", "push_ready+device_view",
+                         "push_ready_many+device_view"};
+  constexpr int kVariants = 6;
   std::vector<uint64_t> keys(np);
   std::vector<size_t> lens(np);
   for (int i = 0; i < np; ++i) {
     keys[i] = (uint64_t)i;
     lens[i] = parts[i].second;
   }
-  for (int variant = 0; variant < 4; ++variant) {
+  for (int variant = 0; variant < kVariants; ++variant) {
     if (only >= 0 && variant != only) continue;
-    const bool many = variant >= 2;
-    const bool ready = variant == 0 || variant == 2;
+    const bool view = variant >= 4;
+    const bool many = variant == 2 || variant == 3 || variant == 5;
+    const bool ready = variant != 1 && variant != 3;
     byteps_server_config cfg;
     std::memset(&cfg, 0, sizeof(cfg));
     cfg.num_workers = N;
@@ -132,7 +138,21 @@ int main(int argc, char** argv) {
     std::mutex m;
     std::condition_variable cv;
     int go = -1, left = 0;
-    auto one_round = [&](int k) {
+    const int total_rounds = rounds + 2 + (view ? 1 : 0);  // + a checking round
+    auto one_round = [&](int k, int r) {
+      if (view && r < rounds + 2) {  // zero-copy: every pull is a view of the store
+        if (many)
+          CKR(byteps_server_push_ready_many(srv, keys.data(), np, k));
+        else
+          for (int i = 0; i < np; ++i) CKR(byteps_server_push_ready(srv, (uint64_t)i, k));
+        for (int i = 0; i < np; ++i) {
+          const void* v = nullptr;
+          size_t vl = 0;
+          CKR(byteps_server_pull_device_view(srv, (uint64_t)i, &v, &vl));
+          if (!v || vl != parts[i].second) exit(6);
+        }
+        return;
+      }
       if (many) {
             std::vector<const void*> srcs(np);
             std::vector<void*> dsts(np);
@@ -164,17 +184,17 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     for (int k = 0; k < N; ++k)
       th.emplace_back([&, k] {
-        for (int r = 0; r < rounds + 2; ++r) {
+        for (int r = 0; r < total_rounds; ++r) {
           {
             std::unique_lock<std::mutex> lk(m);
             cv.wait(lk, [&] { return go >= r; });
           }
-          one_round(k);
+          one_round(k, r);
           std::lock_guard<std::mutex> lk(m);
           if (--left == 0) cv.notify_all();
         }
       });
-    for (int r = 0; r < rounds + 2; ++r) {
+    for (int r = 0; r < total_rounds; ++r) {
       acks = 0;
       auto t0 = std::chrono::steady_clock::now();
       {
@@ -190,7 +210,7 @@ int main(int argc, char** argv) {
       if (variant == 1)
         while (acks.load() < (long)N * np) std::this_thread::yield();
       const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (r >= 2) ts.push_back(s);
+      if (r >= 2 && r < rounds + 2) ts.push_back(s);
     }
     for (auto& t : th) t.join();
     // exactness: every worker's pull equals worker 0's (one store per key)
