@@ -3,6 +3,10 @@
 // it — per worker one push thread (non-blocking pushes) and one pull thread
 // (zero-copy views), 64 MiB fp32 per worker split into BytePS's 4,096,000-B
 // partitions (17 keys).  No Python in the loop.  Prints one JSON line per mode.
+// Modes 2 and 3 are the device-resident round (pushes written into the receive
+// slots by an RDMA transport — byteps_server_recv_slot, filled once here —
+// announced with byteps_server_push_ready; pulls as zero-copy device views,
+// byteps_server_pull_device_view): 17 keys and 1 key of 64 MiB.
 //   hipcc -O2 -std=c++17 -Iinclude -o tools/cfg1_native tools/cfg1_native.cpp \
 //         -Lprophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../prophet_amd' -lpthread
 #include <hip/hip_runtime.h>
@@ -62,11 +66,14 @@ int main(int argc, char** argv) {
       host[k][i] = (float)((int)(x >> 9) - (1 << 22)) / (float)(1 << 20);
     }
   }
-  std::vector<std::pair<size_t, size_t>> parts;  // (offset, len)
-  for (size_t o = 0; o < B; o += kPart) parts.push_back({o, std::min(kPart, B - o)});
-  const int P = (int)parts.size();
+  std::vector<std::pair<size_t, size_t>> parts17, parts1{{0, B}};  // (offset, len)
+  for (size_t o = 0; o < B; o += kPart) parts17.push_back({o, std::min(kPart, B - o)});
 
-  for (int view_pulls = 0; view_pulls < 2; ++view_pulls) {
+  for (int mode = 0; mode < 4; ++mode) {
+    const int view_pulls = mode == 1;
+    const bool device = mode >= 2;
+    const auto& parts = mode == 3 ? parts1 : parts17;
+    const int P = (int)parts.size();
     byteps_server_config cfg{N, lanes, BYTEPS_SERVER_FUSED, 0, 0};
     byteps_server* srv = nullptr;
     CKS(byteps_server_create(&cfg, &srv));
@@ -80,6 +87,14 @@ int main(int argc, char** argv) {
                                      parts[i].second, BYTEPS_REDUCE_FLOAT32, BYTEPS_SERVER_HOST,
                                      on_push, nullptr));
     while (acks.load() < N * P) std::this_thread::yield();
+    if (device)  // the transport's RDMA writes land in the slots (once here)
+      for (int i = 0; i < P; ++i)
+        for (int k = 0; k < N; ++k) {
+          void* slot = nullptr;
+          CKS(byteps_server_recv_slot(srv, (uint64_t)i, k, &slot));
+          CK(hipMemcpy(slot, (char*)host[k] + parts[i].first, parts[i].second,
+                       hipMemcpyHostToDevice));
+        }
 
     std::vector<double> ts;
     for (int r = 0; r < rounds + 2; ++r) {
@@ -91,6 +106,11 @@ int main(int argc, char** argv) {
       for (int k = 0; k < N; ++k) {
         th.emplace_back([&, k] {  // PushLoop (core_loops.cc:492-528)
           for (int i = 0; i < P; ++i) {
+            if (device) {
+              CKS(byteps_server_push_ready(srv, (uint64_t)i, k));
+              pushed[k * P + i].store(1, std::memory_order_release);
+              continue;
+            }
             CKS(byteps_server_push_async(srv, (uint64_t)i, k, (char*)host[k] + parts[i].first,
                                          parts[i].second, BYTEPS_REDUCE_FLOAT32,
                                          BYTEPS_SERVER_HOST, on_push, nullptr));
@@ -100,7 +120,12 @@ int main(int argc, char** argv) {
         th.emplace_back([&, k] {  // PullLoop (core_loops.cc:530-564)
           for (int i = 0; i < P; ++i) {
             while (!pushed[k * P + i].load(std::memory_order_acquire)) std::this_thread::yield();
-            if (view_pulls) {
+            if (device) {
+              const void* v = nullptr;
+              size_t n = 0;
+              CKS(byteps_server_pull_device_view(srv, (uint64_t)i, &v, &n));
+              if (check) CK(hipMemcpy(out[k] + parts[i].first, v, n, hipMemcpyDeviceToHost));
+            } else if (view_pulls) {
               const void* v = nullptr;
               size_t n = 0;
               CKS(byteps_server_pull_host_view(srv, (uint64_t)i, &v, &n));
@@ -128,10 +153,13 @@ int main(int argc, char** argv) {
     std::sort(ts.begin(), ts.end());
     const double med = ts[ts.size() / 2];
     printf("{\"config\": \"cfg1\", \"driver\": \"native C++ threads\", \"layout\": "
-           "\"17keys_push_pull_threads\", \"pushes\": \"byteps_server_push_async\", \"pulls\": "
+           "\"%dkeys_push_pull_threads\", \"pushes\": \"%s\", \"pulls\": "
            "\"%s\", \"lanes\": %d, \"n_workers\": %d, \"bucket_bytes\": %zu, \"round_ms\": %.3f, "
-           "\"min_ms\": %.3f, \"gibps\": %.2f, \"exact\": %s}\n",
-           view_pulls ? "byteps_server_pull_host_view" : "byteps_server_pull", lanes, N, B,
+           "\"min_ms\": %.3f, \"gibps\": %.2f, \"exact\": %s}\n", P,
+           device ? "byteps_server_push_ready (device-resident slots)" : "byteps_server_push_async",
+           device ? "byteps_server_pull_device_view"
+                  : view_pulls ? "byteps_server_pull_host_view" : "byteps_server_pull",
+           lanes, N, B,
            med * 1e3, ts.front() * 1e3, N * (double)B / med / (1 << 30), bad ? "false" : "true");
     fflush(stdout);
     CKS(byteps_server_destroy(srv));
