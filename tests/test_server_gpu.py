@@ -623,16 +623,23 @@ def _fast_bucket(n, seed):
     return np.random.default_rng(seed).standard_normal(n, dtype=np.float32).view(np.uint8)
 
 
+@pytest.mark.parametrize("transport", ["host", "device_zero_copy"])
 @pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
 @pytest.mark.parametrize("layout", ["1key", "17keys"])
-def test_cfg1_two_workers_64mib(port, policy, layout):
-    """BASELINE config 1 at its own workload: 2 workers push fp32 64 MiB each
-    (host buffers), as ONE key, or split into BytePS's 4,096,000-B partitions
-    (17 keys, global.cc:128-135) on 4 engine lanes; each worker pushes then
-    pulls every key from its own thread; 2 rounds after init.  Every pulled
-    byte equals the oracle's left fold in the recorded arrival order
+def test_cfg1_two_workers_64mib(port, policy, layout, transport):
+    """BASELINE config 1 at its own workload: 2 workers push fp32 64 MiB each,
+    as ONE key, or split into BytePS's 4,096,000-B partitions (17 keys,
+    global.cc:128-135) on 4 engine lanes; each worker pushes then pulls every
+    key from its own thread; 2 rounds after init.  ``host``: pushes from host
+    buffers, copying pulls.  ``device_zero_copy``: each round's bytes written
+    straight into the receive slots (recv_slot, as an RDMA transport would),
+    announced with push_ready, pulled as device views of the store.  Every
+    pulled byte equals the oracle's left fold in the recorded arrival order
     (server.cc:147-308)."""
+    from prophet_amd.reducer import GpuReducer
     from prophet_amd.server import PSServer
+    red = GpuReducer(device=0)
+    zc = transport == "device_zero_copy"
     dt, N, B, R = DType.FLOAT32, 2, 64 << 20, 2
     parts = [(0, B)] if layout == "1key" else \
         [(o, min(4_096_000, B - o)) for o in range(0, B, 4_096_000)]
@@ -647,14 +654,29 @@ def test_cfg1_two_workers_64mib(port, policy, layout):
     def worker(w):
         try:
             for r in range(R + 1):
-                for j, (o, ln) in enumerate(parts):
-                    srv.push(j, w, ins[(w, r)][o:o + ln], dt)
+                if zc and r > 0:
+                    src = torch.from_numpy(ins[(w, r)]).cuda()
+                    torch.cuda.synchronize()
+                    for j, (o, ln) in enumerate(parts):   # the transport's write
+                        red.copy(srv.recv_slot(j, w), src[o:o + ln], ln)
+                    torch.cuda.synchronize()
+                    for j in range(len(parts)):
+                        srv.push_ready(j, w)
+                    del src
+                else:
+                    for j, (o, ln) in enumerate(parts):
+                        srv.push(j, w, ins[(w, r)][o:o + ln], dt)
                 bar.wait()
                 bar.wait()
                 if r == 0:
                     continue
                 for j, (o, ln) in enumerate(parts):
-                    srv.pull(j, outs[(w, r)][o:o + ln])
+                    if zc:
+                        ptr, nb = srv.pull_device_view(j)
+                        assert nb == ln
+                        outs[(w, r)][o:o + ln] = _read_device(red, ptr, nb)
+                    else:
+                        srv.pull(j, outs[(w, r)][o:o + ln])
         except Exception as e:  # surfaced below
             errors.append(repr(e))
             bar.abort()
