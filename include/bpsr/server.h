@@ -94,7 +94,13 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
                              void* ctx);
 
 /* Zero-copy transport path: where worker `worker`'s push for `key` must land,
- * then the arrival notice once the bytes are there (visible to the device). */
+ * then the arrival notice once the bytes are there (visible to the device).
+ * recv_slot waits until the key's last issued fold (or init copy) is done, so
+ * the slot is free to be written once it returns — provided the worker's
+ * previous push of the key has been folded, i.e. the transport writes a
+ * worker's round r + 1 only after that worker pulled round r (BytePS's
+ * push-then-pull order per key; the init round is complete once the init
+ * pushes have been answered). */
 int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot);
 int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 
