@@ -149,6 +149,18 @@ int byteps_prophet_release_groups(byteps_prophet_queue* q, const byteps_prophet_
 int byteps_prophet_profile(const int64_t* tic_us, int32_t ngrad, int32_t* checkpoints,
                            double* backward_exec, int32_t cap);
 
+/* Prophet's bandwidth monitor (reportFinish(size, priority),
+ * scheduled_queue.cc:373-398, same pre-run pass): the highest rate any one
+ * gradient's push achieved, possible_B = size * 1000 / (finish - start) bytes
+ * per ms, maximised over the pushes — returned in Z_NET_B's unit (Mb/s, the
+ * constructor's x125 turns it back into bytes per ms): *net_b = max over i of
+ * size[i] * 8 / (finish_us[i] - start_us[i]).  Pushes with finish <= start are
+ * skipped (the reference would divide by zero); EARGS if none is left.  The
+ * reference never records the push start it reads (_push_start_tic is
+ * declared nowhere), so the caller supplies it. */
+int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
+                                  const int64_t* finish_us, int32_t n, double* net_b);
+
 #ifdef __cplusplus
 }
 #endif

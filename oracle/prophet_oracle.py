@@ -222,3 +222,14 @@ def oracle_profile(tic_us):
         ex.append(abs(float(tic_us[n - 1] - tic_us[0])) / 1000)
     ex.append(0.0)
     return tuple(cps), tuple(ex)
+
+
+def oracle_estimate_net_b(sizes, starts, finishes):
+    """reportFinish(size, priority) (scheduled_queue.cc:373-398): max over the
+    profiled pushes of size * 1000 / t bytes per ms, as Z_NET_B (Mb/s) =
+    that / 125 = size * 8 / t_us.  Pushes with t <= 0 are skipped."""
+    rates = [sz * 8.0 / (f - s) for sz, s, f in zip(sizes, starts, finishes)
+             if f - s > 0 and sz >= 0]
+    if not rates:
+        raise ValueError("no push with finish > start")
+    return max(rates)

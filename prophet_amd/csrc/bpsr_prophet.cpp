@@ -332,4 +332,20 @@ int byteps_prophet_profile(const int64_t* tic_us, int32_t ngrad, int32_t* checkp
   return (int)cps.size();
 }
 
+int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
+                                  const int64_t* finish_us, int32_t n, double* net_b) {
+  if (!size || !start_us || !finish_us || !net_b || n < 1)
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "null array or n < 1");
+  double best = -1;
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t t = finish_us[i] - start_us[i];
+    if (t <= 0 || size[i] < 0) continue;
+    const double mbps = (double)size[i] * 8.0 / (double)t;  // = possible_B / 125
+    if (mbps > best) best = mbps;
+  }
+  if (best < 0) return bpsr::fail(BYTEPS_REDUCE_EARGS, "no push with finish > start");
+  *net_b = best;
+  return 0;
+}
+
 }  // extern "C"

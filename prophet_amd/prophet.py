@@ -62,7 +62,7 @@ PROPHET_EXPORTS = (
     "byteps_prophet_create", "byteps_prophet_destroy", "byteps_prophet_add_task",
     "byteps_prophet_get_task", "byteps_prophet_report_finish", "byteps_prophet_pending",
     "byteps_prophet_get_state", "byteps_prophet_reset", "byteps_prophet_release_groups",
-    "byteps_prophet_profile",
+    "byteps_prophet_profile", "byteps_prophet_estimate_net_b",
 )
 
 _BOUND = None
@@ -86,6 +86,8 @@ def _lib():
         L.byteps_prophet_pending.argtypes = [vp, P(ctypes.c_uint64)]
         L.byteps_prophet_get_state.argtypes = [vp, P(_State)]
         L.byteps_prophet_reset.argtypes = [vp]
+        L.byteps_prophet_estimate_net_b.argtypes = [P(ctypes.c_int64)] * 3 + [
+            ctypes.c_int32, P(ctypes.c_double)]
         L.byteps_prophet_profile.argtypes = [P(ctypes.c_int64), ctypes.c_int32,
                                              P(ctypes.c_int32), P(ctypes.c_double), ctypes.c_int32]
         L.byteps_prophet_release_groups.argtypes = [
@@ -189,6 +191,32 @@ def profile_checkpoints(tic_us) -> tuple[tuple, tuple]:
     return tuple(cps[:k]), tuple(ex[:k])
 
 
+def estimate_net_b(sizes, start_us, finish_us) -> float:
+    """Prophet's bandwidth monitor (reportFinish(size, priority),
+    scheduled_queue.cc:373-398), native: the fastest profiled push as Z_NET_B
+    (Mb/s) = max of size * 8 / (finish - start) over the pushes."""
+    L = _lib()
+    n = len(sizes)
+    arr = lambda xs: (ctypes.c_int64 * max(n, 1))(*[int(x) for x in xs])  # noqa: E731
+    out = ctypes.c_double()
+    _ck(L.byteps_prophet_estimate_net_b(arr(sizes), arr(start_us), arr(finish_us), n,
+                                        ctypes.byref(out)))
+    return out.value
+
+
+def queue_from_profile(tic_us, batch_size: int, credit: int, net_b: float | None = None,
+                       push_sizes=None, push_start_us=None, push_finish_us=None):
+    """A PUSH queue configured the way Prophet's pre-run pass configures it:
+    checkpoints and block budgets from the gradients' first-arrival times
+    (``profile_checkpoints``) and Z_NET_B from the profiled pushes
+    (``estimate_net_b``) unless given."""
+    cps, ex = profile_checkpoints(tic_us)
+    if net_b is None:
+        net_b = estimate_net_b(push_sizes, push_start_us, push_finish_us)
+    return ProphetPushQueue(batch_size=batch_size, net_b=int(net_b), credit=credit,
+                            checkpoints=cps, backward_exec=ex)
+
+
 def model_checkpoints(n_tensors: int, checkpoints=PROPHET_CHECKPOINTS) -> tuple:
     """The reference hard-codes a 157-gradient model; a model with more
     gradients gets its last checkpoint extended to ``n_tensors - 1`` (same rule
@@ -247,4 +275,4 @@ def release_groups(queue: ProphetPushQueue, arrivals, finish_immediately: bool =
 
 __all__ = ["PushTask", "ProphetPushQueue", "BACKWARD_EXEC", "PHASE_CREDIT", "PHASE_FIFO",
            "model_checkpoints", "backward_arrivals", "release_groups", "profile_checkpoints",
-           "PROPHET_EXPORTS"]
+           "estimate_net_b", "queue_from_profile", "PROPHET_EXPORTS"]

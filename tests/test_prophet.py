@@ -393,3 +393,40 @@ def test_profile_errors():
         profile_checkpoints([])
     with pytest.raises(ReduceError, match="< 0"):
         profile_checkpoints([5, -1])
+
+
+def test_estimate_net_b_matches_oracle_and_hand_value():
+    from oracle.prophet_oracle import oracle_estimate_net_b
+    from prophet_amd.prophet import estimate_net_b
+    # 4,096,000 B in 3,276.8 us = 10,000 Mb/s; a slower push and a zero-length
+    # interval (skipped) around it
+    sizes, starts, fins = [4_096_000, 1_000_000, 77], [0, 100, 500], [3277, 2100, 500]
+    want = 4_096_000 * 8 / 3277
+    assert oracle_estimate_net_b(sizes, starts, fins) == pytest.approx(want, rel=0)
+    assert estimate_net_b(sizes, starts, fins) == oracle_estimate_net_b(sizes, starts, fins)
+    rng = random.Random(5)
+    for _ in range(30):
+        n = rng.randint(1, 50)
+        sz = [rng.randint(0, 10**8) for _ in range(n)]
+        st = [rng.randint(0, 10**6) for _ in range(n)]
+        fi = [s + rng.randint(1, 10**5) for s in st]
+        assert estimate_net_b(sz, st, fi) == oracle_estimate_net_b(sz, st, fi)
+    from prophet_amd.reducer import ReduceError
+    with pytest.raises(ReduceError, match="finish > start"):
+        estimate_net_b([10], [5], [5])
+
+
+def test_queue_from_profile_runs_an_iteration():
+    from prophet_amd.prophet import queue_from_profile
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    n = len(sizes)
+    tic, t = [0] * n, 0
+    for i in range(n - 1, -1, -1):
+        tic[i] = t
+        t += 3000 if i in (40, 100) else 120
+    q = queue_from_profile(tic, batch_size=64, credit=8 << 20, push_sizes=[4_096_000],
+                           push_start_us=[0], push_finish_us=[3277])
+    assert q.checkpoints == (-1, 39, 99, 160)
+    arr = backward_arrivals(sizes)
+    flat = [t for g in release_groups(q, arr) for t in g]
+    assert sorted(flat) == sorted(arr)
