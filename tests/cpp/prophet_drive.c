@@ -55,5 +55,22 @@ int main(void) {
   }
   printf("\n");
   byteps_prophet_destroy(q);
+  /* pre-run profile: gaps of 100 us, 2,000 before gradient 3, 5,000 before 7 */
+  int64_t tic[10];
+  int64_t t = 1000000;
+  for (int i = 9; i >= 0; --i) {
+    tic[i] = t;
+    if (i) t += i == 3 ? 2000 : i == 7 ? 5000 : 100;
+  }
+  int32_t pc[12];
+  double pe[12];
+  const int k = byteps_prophet_profile(tic, 10, pc, pe, 12);
+  if (k < 0) return 7;
+  for (int i = 0; i < k; ++i) printf("%d:%g ", pc[i], pe[i]);
+  printf("\n");
+  const int64_t sz[1] = {4096000}, st[1] = {0}, fi[1] = {3277};
+  double nb = 0;
+  if (byteps_prophet_estimate_net_b(sz, st, fi, 1, &nb)) return 8;
+  printf("%.3f\n", nb);
   return 0;
 }

@@ -167,3 +167,5 @@ def test_prophet_scheduler_from_c(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
     assert out[0].split() == ["2:0", "3:0", "0:-1", "1:-1"]
     assert out[1].split() == ["2:0:101", "3:0:100", "|", "0:-1:103", "1:-1:102", "|"]
+    assert out[2].split() == ["-1:5", "2:2", "6:0.2", "9:0"]       # profile
+    assert out[3] == f"{4_096_000 * 8 / 3277:.3f}"                 # Z_NET_B, Mb/s
