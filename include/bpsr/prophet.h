@@ -161,6 +161,34 @@ int byteps_prophet_profile(const int64_t* tic_us, int32_t ngrad, int32_t* checkp
 int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
                                   const int64_t* finish_us, int32_t n, double* net_b);
 
+/* The PUSH loop (core_loops.cc RunPushLoopOnce -> reportFinish, as a native
+ * thread): the scheduler feeding a block queue (bpsr/reduce.h).  The queue's
+ * table holds the iteration's partitions; block_of[h] is the block of the
+ * partition whose task handle is h (0 <= h < nhandles).  Per iteration:
+ *   byteps_prophet_loop_begin(l, consumer_stream)  resets the scheduler and
+ *       launches the block queue's consumer (one launch per iteration);
+ *   byteps_prophet_loop_push(l, &task)  one per partition as its bytes land
+ *       (their copies queued on release_stream, or finished), in any order —
+ *       the loop thread polls getTask and, at the end of each release group,
+ *       releases every block that became complete (one release_range per run
+ *       of consecutive blocks, on release_stream), then reports the group's
+ *       partitions finished;
+ *   byteps_prophet_loop_end(l, timeout_s)  waits until every block has been
+ *       released (timeout_s <= 0: no limit).  ETIMEOUT leaves the scheduler
+ *       holding the missing partitions' state: destroy the loop and the queue
+ *       (the block queue's own status() resynchronises its epochs).
+ * The loop thread makes HIP calls on the device current at create time.  The
+ * scheduler and block queue must outlive the loop and must not be driven
+ * directly while it runs. */
+typedef struct byteps_prophet_loop byteps_prophet_loop;
+int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,
+                               const int32_t* block_of, int32_t nhandles, int32_t nblocks,
+                               void* release_stream, byteps_prophet_loop** out);
+int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream);
+int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* t);
+int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s);
+int byteps_prophet_loop_destroy(byteps_prophet_loop* l);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,7 @@
 
 #include "bpsr/prophet.h"
 #include "bpsr_error.h"
+#include "bpsr_prophet_internal.h"
 
 namespace {
 
@@ -65,17 +66,23 @@ struct byteps_prophet_queue {
     return &tasks[grad].front();
   }
 
-  // one getTask() poll; returns true and fills *out when a task is released
-  bool poll(byteps_prophet_task* out, int32_t* ph) {
+  // one getTask() poll; returns true and fills *out when a task is released.
+  // *progressed (if given): whether the poll changed any state — a poll that
+  // returns no task may still advance collection or end a block, and the
+  // next poll can then release without new input.
+  bool poll(byteps_prophet_task* out, int32_t* ph, bool* progressed = nullptr) {
+    bool dummy;
+    bool& prog = progressed ? *progressed : dummy;
+    prog = true;
     if (nsched == 0) {  // :292-318, the FIFO (no ready events / tables here)
-      if (fifo.empty()) return false;
+      if (fifo.empty()) return prog = false;
       *out = fifo.front();
       fifo.pop_front();
       *ph = BYTEPS_PROPHET_FIFO;
       return true;
     }
     if (!dequeue) {  // collection, :221-241
-      if (!find(expected)) return false;
+      if (!find(expected)) return prog = false;
       if (!visited[expected]) {
         for (int32_t x = 0; x < tensor_part[expected]; ++x) {
           stack.push_back(expected);
@@ -95,7 +102,7 @@ struct byteps_prophet_queue {
       return false;
     }
     const byteps_prophet_task* t = find(stack.back());
-    if (!t) return false;
+    if (!t) return prog = false;
     if (!meetzero) {  // budget, :261-271 (strict)
       if (dynamic > (double)t->len) {
         dynamic -= (double)t->len;
@@ -105,7 +112,7 @@ struct byteps_prophet_queue {
         return false;
       }
     } else if (credit < t->len) {  // credit, :272-278
-      return false;
+      return prog = false;
     } else {
       credit -= t->len;
       phase = BYTEPS_PROPHET_CREDIT;
@@ -349,3 +356,11 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
 }
 
 }  // extern "C"
+
+namespace bpsr {
+int prophet_poll(byteps_prophet_queue* q, byteps_prophet_task* out, bool* progressed) {
+  std::lock_guard<std::mutex> g(q->mu);
+  int32_t ph = 0;
+  return q->poll(out, &ph, progressed) ? 1 : 0;
+}
+}  // namespace bpsr

@@ -1,0 +1,211 @@
+// The PUSH loop: Prophet's scheduler feeding the block queue from a native
+// thread (include/bpsr/prophet.h, byteps_prophet_loop_*).
+//
+// The reference runs its PUSH stage as a background loop (core_loops.cc
+// RunPushLoopOnce: getTask, send, FinishOrProceed -> reportFinish) over the
+// scheduled queue.  Here the "send" of a released partition is the device
+// fold of its block: the loop thread polls the scheduler whenever partitions
+// arrive, counts released partitions per block and, at the end of each
+// release group, releases every block that became complete — one
+// byteps_reduce_blockq_release_range per run of consecutive blocks, on the
+// release stream, behind the copies that landed the pushes — then reports the
+// group's partitions finished (credit back to the scheduler).
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "bpsr/prophet.h"
+#include "bpsr_error.h"
+#include "bpsr_internal.h"
+#include "bpsr_prophet_internal.h"
+
+struct byteps_prophet_loop {
+  byteps_prophet_queue* pq = nullptr;
+  byteps_reduce_blockq* bq = nullptr;
+  void* rel_stream = nullptr;
+  int device = 0;
+  std::vector<int32_t> block_of;    // per task handle
+  std::vector<int32_t> block_size;  // partitions per block
+  // iteration state, guarded by mu
+  std::mutex mu;
+  std::condition_variable cv;       // pushes -> thread
+  std::condition_variable done_cv;  // thread -> end()
+  bool active = false;
+  bool stop = false;
+  uint64_t pushes = 0, seen = 0;
+  std::vector<int32_t> left;        // partitions not yet released, per block
+  std::vector<char> released;       // block released this iteration
+  int32_t blocks_released = 0;
+  std::vector<char> got;            // task handle pushed this iteration
+  int err = 0;
+  std::thread th;
+
+  int nblocks() const { return (int)block_size.size(); }
+
+  // Release every complete, unreleased block, one range per run (under mu).
+  int release_complete() {
+    const int nb = nblocks();
+    for (int b = 0; b < nb;) {
+      if (released[b] || left[b] != 0) {
+        ++b;
+        continue;
+      }
+      int e = b;
+      while (e < nb && !released[e] && left[e] == 0) released[e++] = 1;
+      const int rc = byteps_reduce_blockq_release_range(bq, b, e - b, rel_stream);
+      if (rc) return rc;
+      blocks_released += e - b;
+      b = e;
+    }
+    return 0;
+  }
+
+  void run() {
+    (void)hipSetDevice(device);
+    std::vector<int64_t> group_lens;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || (active && pushes != seen); });
+      if (stop) return;
+      seen = pushes;
+      lk.unlock();
+      // drain the scheduler: a zero poll that made progress (collection,
+      // end of a block) may be followed by a release without new input
+      int rc = 0;
+      for (;;) {
+        byteps_prophet_task t;
+        bool prog = false;
+        if (bpsr::prophet_poll(pq, &t, &prog) == 1) {
+          lk.lock();
+          if (t.handle < block_of.size()) --left[block_of[t.handle]];
+          lk.unlock();
+          group_lens.push_back(t.len);
+          continue;
+        }
+        if (!group_lens.empty()) {  // a release group ended
+          lk.lock();
+          rc = release_complete();
+          lk.unlock();
+          for (int64_t len : group_lens) byteps_prophet_report_finish(pq, len);
+          group_lens.clear();
+          if (rc) break;
+          continue;  // credit came back: the next poll may release more
+        }
+        if (!prog) break;
+      }
+      lk.lock();
+      if (rc && !err) err = rc;
+      if (err || blocks_released == nblocks()) done_cv.notify_all();
+    }
+  }
+};
+
+extern "C" {
+
+int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,
+                               const int32_t* block_of, int32_t nhandles, int32_t nblocks,
+                               void* release_stream, byteps_prophet_loop** out) {
+  if (!pq || !bq || !block_of || !out || nhandles < 0 || nblocks < 1)
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "null argument, nhandles < 0 or nblocks < 1");
+  *out = nullptr;
+  auto* l = new (std::nothrow) byteps_prophet_loop;
+  if (!l) return bpsr::fail(BYTEPS_REDUCE_EARGS, "out of memory");
+  l->pq = pq;
+  l->bq = bq;
+  l->rel_stream = release_stream;
+  l->block_size.assign(nblocks, 0);
+  l->block_of.assign(block_of, block_of + nhandles);
+  for (int32_t h = 0; h < nhandles; ++h) {
+    if (block_of[h] < 0 || block_of[h] >= nblocks) {
+      delete l;
+      return bpsr::fail(BYTEPS_REDUCE_EARGS, "block_of[%d] = %d outside [0, %d)", h, block_of[h],
+                        nblocks);
+    }
+    ++l->block_size[block_of[h]];
+  }
+  hipError_t e = hipGetDevice(&l->device);
+  if (e != hipSuccess) {
+    delete l;
+    return bpsr::hip_fail(e, "hipGetDevice");
+  }
+  l->th = std::thread([l] { l->run(); });
+  *out = l;
+  return 0;
+}
+
+int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream) {
+  if (!l) return bpsr::fail(BYTEPS_REDUCE_EARGS, "null loop");
+  std::lock_guard<std::mutex> g(l->mu);
+  if (l->active) return bpsr::fail(BYTEPS_REDUCE_EARGS, "iteration already begun (end it first)");
+  uint64_t pend = 0;
+  byteps_prophet_pending(l->pq, &pend);
+  if (pend) return bpsr::fail(BYTEPS_REDUCE_EARGS, "scheduler holds %llu tasks", (unsigned long long)pend);
+  int rc = byteps_prophet_reset(l->pq);
+  if (rc) return rc;
+  if ((rc = byteps_reduce_blockq_launch(l->bq, consumer_stream))) return rc;
+  l->left = l->block_size;
+  l->released.assign(l->block_size.size(), 0);
+  l->blocks_released = 0;
+  l->got.assign(l->block_of.size(), 0);
+  l->err = 0;
+  l->active = true;
+  return l->release_complete();  // blocks without partitions
+}
+
+int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* t) {
+  if (!l || !t) return bpsr::fail(BYTEPS_REDUCE_EARGS, "null loop or task");
+  {
+    std::lock_guard<std::mutex> g(l->mu);
+    if (!l->active) return bpsr::fail(BYTEPS_REDUCE_EARGS, "no iteration begun");
+    if (t->handle >= l->block_of.size())
+      return bpsr::fail(BYTEPS_REDUCE_EARGS, "handle %llu outside the table (%zu partitions)",
+                        (unsigned long long)t->handle, l->block_of.size());
+    if (l->got[t->handle])
+      return bpsr::fail(BYTEPS_REDUCE_EARGS, "partition %llu pushed twice in one iteration",
+                        (unsigned long long)t->handle);
+    l->got[t->handle] = 1;
+  }
+  const int rc = byteps_prophet_add_task(l->pq, t);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(l->mu);
+  ++l->pushes;
+  l->cv.notify_one();
+  return 0;
+}
+
+int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s) {
+  if (!l) return bpsr::fail(BYTEPS_REDUCE_EARGS, "null loop");
+  std::unique_lock<std::mutex> lk(l->mu);
+  if (!l->active) return bpsr::fail(BYTEPS_REDUCE_EARGS, "no iteration begun");
+  const auto pred = [&] { return l->err != 0 || l->blocks_released == l->nblocks(); };
+  bool ok = true;
+  if (timeout_s > 0)
+    ok = l->done_cv.wait_for(lk, std::chrono::duration<double>(timeout_s), pred);
+  else
+    l->done_cv.wait(lk, pred);
+  l->active = false;
+  if (l->err) return l->err;
+  if (!ok)
+    return bpsr::fail(BYTEPS_REDUCE_ETIMEOUT,
+                      "iteration not complete after %.3f s: %d of %d blocks released", timeout_s,
+                      l->blocks_released, l->nblocks());
+  return 0;
+}
+
+int byteps_prophet_loop_destroy(byteps_prophet_loop* l) {
+  if (!l) return 0;
+  {
+    std::lock_guard<std::mutex> g(l->mu);
+    l->stop = true;
+    l->cv.notify_all();
+  }
+  if (l->th.joinable()) l->th.join();
+  delete l;
+  return 0;
+}
+
+}  // extern "C"

@@ -63,6 +63,8 @@ PROPHET_EXPORTS = (
     "byteps_prophet_get_task", "byteps_prophet_report_finish", "byteps_prophet_pending",
     "byteps_prophet_get_state", "byteps_prophet_reset", "byteps_prophet_release_groups",
     "byteps_prophet_profile", "byteps_prophet_estimate_net_b",
+    "byteps_prophet_loop_create", "byteps_prophet_loop_begin", "byteps_prophet_loop_push",
+    "byteps_prophet_loop_end", "byteps_prophet_loop_destroy",
 )
 
 _BOUND = None
@@ -86,6 +88,12 @@ def _lib():
         L.byteps_prophet_pending.argtypes = [vp, P(ctypes.c_uint64)]
         L.byteps_prophet_get_state.argtypes = [vp, P(_State)]
         L.byteps_prophet_reset.argtypes = [vp]
+        L.byteps_prophet_loop_create.argtypes = [vp, vp, P(ctypes.c_int32), ctypes.c_int32,
+                                                 ctypes.c_int32, vp, P(vp)]
+        L.byteps_prophet_loop_begin.argtypes = [vp, vp]
+        L.byteps_prophet_loop_push.argtypes = [vp, P(_Task)]
+        L.byteps_prophet_loop_end.argtypes = [vp, ctypes.c_double]
+        L.byteps_prophet_loop_destroy.argtypes = [vp]
         L.byteps_prophet_estimate_net_b.argtypes = [P(ctypes.c_int64)] * 3 + [
             ctypes.c_int32, P(ctypes.c_double)]
         L.byteps_prophet_profile.argtypes = [P(ctypes.c_int64), ctypes.c_int32,
@@ -170,6 +178,53 @@ class ProphetPushQueue:
         s = _State()
         _ck(self._L.byteps_prophet_get_state(self._h, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in _State._fields_}
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        return 0
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+class PushLoop:
+    """The PUSH loop as a native thread (byteps_prophet_loop_*; core_loops.cc
+    RunPushLoopOnce -> reportFinish): ``queue`` (a ProphetPushQueue) releases
+    partitions, the loop releases the blocks of ``blockq``
+    (``GpuReducer.make_blockq``) that they complete, one release_range per run
+    of consecutive blocks on ``release_stream``.  ``block_of[i]`` is the block
+    of table partition i; push each partition with its table index.
+    Per iteration: ``begin(consumer_stream)``, ``push(task, index)`` per
+    partition as its bytes land, ``end()``."""
+
+    def __init__(self, queue: ProphetPushQueue, blockq, block_of, release_stream=None):
+        self._L = _lib()
+        self.queue, self.blockq = queue, blockq
+        bo = (ctypes.c_int32 * max(len(block_of), 1))(*block_of)
+        h = ctypes.c_void_p()
+        _ck(self._L.byteps_prophet_loop_create(queue._h, blockq.handle, bo, len(block_of),
+                                               blockq.nblocks, _stream_ptr(release_stream),
+                                               ctypes.byref(h)))
+        self._h = h
+
+    def begin(self, consumer_stream=None) -> None:
+        _ck(self._L.byteps_prophet_loop_begin(self._h, _stream_ptr(consumer_stream)))
+
+    def push(self, task: PushTask, index: int) -> None:
+        c = _Task(task.grad, task.part, task.len, task.total_partnum, int(task.scheduled),
+                  task.key, int(index))
+        _ck(self._L.byteps_prophet_loop_push(self._h, ctypes.byref(c)))
+
+    def end(self, timeout_s: float = 10.0) -> None:
+        _ck(self._L.byteps_prophet_loop_end(self._h, float(timeout_s)))
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._L.byteps_prophet_loop_destroy(h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def profile_checkpoints(tic_us) -> tuple[tuple, tuple]:
@@ -275,4 +330,4 @@ def release_groups(queue: ProphetPushQueue, arrivals, finish_immediately: bool =
 
 __all__ = ["PushTask", "ProphetPushQueue", "BACKWARD_EXEC", "PHASE_CREDIT", "PHASE_FIFO",
            "model_checkpoints", "backward_arrivals", "release_groups", "profile_checkpoints",
-           "estimate_net_b", "queue_from_profile", "PROPHET_EXPORTS"]
+           "estimate_net_b", "queue_from_profile", "PushLoop", "PROPHET_EXPORTS"]

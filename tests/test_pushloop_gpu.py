@@ -1,0 +1,142 @@
+"""The native PUSH loop (byteps_prophet_loop_*): Prophet's scheduler feeding
+the block queue from a library thread, as core_loops.cc's PUSH loop feeds the
+network.  BASELINE config 3's shape — ResNet-50 fp16 gradients, 8 workers,
+165 BytePS partitions in the 12 Prophet blocks — with the partitions arriving
+from a feeder thread in backward order, at random small intervals, for three
+back-to-back iterations; every iteration's output is bit-exact with torch's
+own half-precision left fold (and that equals the oracle's fp16 rule, checked
+on windows).  Also: a partition pushed twice, a missing partition (ETIMEOUT,
+then the block queue's status clears), a schedule whose budgets cut blocks."""
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(240)]
+
+
+def _setup(net_b=10**6, credit=1 << 30, n_workers=8, seed=0):
+    from prophet_amd.buckets import partition_all, prophet_blocks, resnet50_param_sizes
+    from prophet_amd.dtypes import DType
+    from prophet_amd.prophet import ProphetPushQueue, PushTask, model_checkpoints
+    from prophet_amd.reducer import GpuReducer
+    dev = torch.device("cuda:0")
+    red = GpuReducer(device=0)
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    parts = partition_all(sizes)
+    toff = [0]
+    for n in sizes:
+        toff.append(toff[-1] + n)
+    total = toff[-1]
+    nparts = {}
+    for p in parts:
+        nparts[p.tensor] = nparts.get(p.tensor, 0) + 1
+    table, block_of = [], []
+    for b, blk in enumerate(prophet_blocks(len(sizes))):
+        tset = set(blk)
+        for p in parts:
+            if p.tensor in tset:
+                table.append(p)
+                block_of.append(b)
+    nb = max(block_of) + 1
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    w = [torch.randn(total // 2, device=dev, generator=gen).half().view(torch.uint8)
+         for _ in range(n_workers)]
+    out = torch.zeros(total, dtype=torch.uint8, device=dev)
+    blocks = [[] for _ in range(nb)]
+    for p, b in zip(table, block_of):
+        o = toff[p.tensor] + p.offset
+        blocks[b].append((out[o:o + p.len], [x[o:o + p.len] for x in w], p.len))
+    bq = red.make_blockq(blocks, DType.FLOAT16)
+    bq.config(wg_per_cu=0, timeout_s=1.0)
+    q = ProphetPushQueue(batch_size=64, net_b=net_b, credit=credit,
+                         checkpoints=model_checkpoints(len(sizes)))
+    # arrivals: backward order (highest gradient first), handle = table index
+    arrivals = sorted(range(len(table)), key=lambda i: (-table[i].tensor, table[i].part))
+    tasks = [(PushTask(table[i].tensor, table[i].part, table[i].len, nparts[table[i].tensor],
+                       (table[i].tensor << 16) + table[i].part), i) for i in arrivals]
+    ref = w[0].view(torch.float16).clone()
+    for x in w[1:]:
+        ref.add_(x.view(torch.float16))
+    return dict(red=red, bq=bq, q=q, block_of=block_of, tasks=tasks, out=out, ref=ref, w=w,
+                nb=nb)
+
+
+def _feed(loop, tasks, seed, skip=None):
+    rng = random.Random(seed)
+    for t, i in tasks:
+        if i == skip:
+            continue
+        if rng.random() < 0.1:
+            time.sleep(rng.random() * 0.0005)
+        loop.push(t, i)
+
+
+@pytest.mark.parametrize("net_b", [10**6, 1000], ids=["whole_blocks", "budget_cuts_blocks"])
+def test_push_loop_iterations_exact(net_b):
+    from prophet_amd.prophet import PushLoop
+    S = _setup(net_b=net_b)
+    cons = torch.cuda.Stream(priority=-100)
+    rel = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel)
+    for it in range(3):
+        S["out"].zero_()
+        torch.cuda.synchronize()
+        loop.begin(cons)
+        th = threading.Thread(target=_feed, args=(loop, S["tasks"], it))
+        th.start()
+        th.join()
+        loop.end(timeout_s=10.0)
+        torch.cuda.synchronize()
+        S["bq"].status(cons)
+        assert torch.equal(S["out"], S["ref"].view(torch.uint8)), f"iteration {it}"
+    loop.close()
+    # the fp16 rule of the oracle (cpu_reducer.cc:94-128) on two windows
+    from oracle.oracle import PortReducer
+    from prophet_amd.dtypes import DType
+    port = PortReducer(nthreads=4)
+    for a in (0, S["out"].numel() - (1 << 16)):
+        ln = 1 << 16
+        ins = [x[a:a + ln].cpu().numpy() for x in S["w"]]
+        want = np.zeros(ln, np.uint8)
+        port.sum_n(want, ins, ln, DType.FLOAT16)
+        assert np.array_equal(S["out"][a:a + ln].cpu().numpy(), want)
+
+
+def test_push_loop_errors_and_missing_partition():
+    from prophet_amd.prophet import PushLoop
+    from prophet_amd.reducer import ReduceError
+    S = _setup(seed=3)
+    cons = torch.cuda.Stream(priority=-100)
+    rel = torch.cuda.Stream()
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel)
+    t0, i0 = S["tasks"][0]
+    with pytest.raises(ReduceError, match="no iteration"):
+        loop.push(t0, i0)
+    loop.begin(cons)
+    with pytest.raises(ReduceError, match="already begun"):
+        loop.begin(cons)
+    loop.push(t0, i0)
+    with pytest.raises(ReduceError, match="twice"):
+        loop.push(t0, i0)
+    with pytest.raises(ReduceError, match="outside the table"):
+        loop.push(t0, 10_000)
+    # everything but the last partition of the last block: that block never
+    # completes -> end() times out; the consumer gives up after its own 1-s
+    # timeout and the block queue's status reports it once
+    last = S["tasks"][-1][1]
+    _feed(loop, S["tasks"][1:], 7, skip=last)
+    with pytest.raises(ReduceError) as e:
+        loop.end(timeout_s=0.5)
+    assert e.value.code == -5                      # BYTEPS_REDUCE_ETIMEOUT
+    loop.close()
+    time.sleep(1.5)
+    torch.cuda.synchronize()
+    with pytest.raises(ReduceError):
+        S["bq"].status(cons)
+    S["bq"].status(cons)                           # reported once, then clear
