@@ -180,6 +180,10 @@ int main(int argc, char** argv) {
     pc.backward_exec = ex.data();  // copied by create
     CKR(byteps_prophet_create(&pc, &sched));
   }
+  // the library's PUSH loop (byteps_prophet_loop_*): one scheduler + loop per
+  // input set (each set has its own block queue)
+  std::vector<byteps_prophet_queue*> lq(kSets, nullptr);
+  std::vector<byteps_prophet_loop*> loops(kSets, nullptr);
   std::vector<int> left(nb);
   double sched_us = 0;
   long sched_iters = 0, groups_seen = 0, release_calls = 0;
@@ -297,6 +301,15 @@ int main(int argc, char** argv) {
     sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     ++sched_iters;
   };
+  const Fn push_loop = [&](int i) {
+    const int k = i % kSets;
+    const auto t0 = std::chrono::steady_clock::now();
+    CKR(byteps_prophet_loop_begin(loops[k], cons));
+    for (const auto& t : tasks.arrivals) CKR(byteps_prophet_loop_push(loops[k], &t));
+    CKR(byteps_prophet_loop_end(loops[k], 5.0));
+    sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ++sched_iters;
+  };
   const Fn plan_no_blocks = [&](int i) {
     CKR(byteps_reduce_plan_launch(sets[i % kSets].plan_blocks, cons));
   };
@@ -310,7 +323,24 @@ int main(int argc, char** argv) {
                              {"blockq_live_release_2streams", &live_2streams},
                              {"blockq_live_release_ranges4", &live_ranges},
                              {"blockq_releases_first_other_stream", &release_first}};
-  if (sched) variants.push_back({"blockq_live_prophet_scheduler", &prophet_live});
+  if (sched) {
+    variants.push_back({"blockq_live_prophet_scheduler", &prophet_live});
+    byteps_prophet_config pc;
+    std::memset(&pc, 0, sizeof(pc));
+    const double ex[] = {16, 15, 9, 10, 12, 18, 15, 21, 30, 25, 20, 5, 0};
+    pc.batch_size = 64;
+    pc.net_b = 10000;
+    pc.credit = 16 << 20;
+    pc.checkpoints = tasks.cps.data();
+    pc.ncheckpoints = (int32_t)tasks.cps.size();
+    pc.backward_exec = ex;
+    for (int k = 0; k < kSets; ++k) {
+      CKR(byteps_prophet_create(&pc, &lq[k]));
+      CKR(byteps_prophet_loop_create(lq[k], sets[k].q, block_of.data(), (int32_t)block_of.size(),
+                                     nb, rel[0], &loops[k]));
+    }
+    variants.push_back({"blockq_prophet_push_loop", &push_loop});
+  }
   const double alg = (double)(N + 1) * (double)t.total;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -365,6 +395,10 @@ int main(int argc, char** argv) {
            sched_iters ? (double)groups_seen / sched_iters : 0.0,
            sched_iters ? (double)release_calls / sched_iters : 0.0);
     fflush(stdout);
+  }
+  for (int k = 0; k < kSets; ++k) {
+    if (loops[k]) byteps_prophet_loop_destroy(loops[k]);
+    if (lq[k]) byteps_prophet_destroy(lq[k]);
   }
   if (sched) byteps_prophet_destroy(sched);
   for (auto& s : sets) {
