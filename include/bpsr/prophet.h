@@ -177,13 +177,17 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  *       released (timeout_s <= 0: no limit).  ETIMEOUT leaves the scheduler
  *       holding the missing partitions' state: destroy the loop and the queue
  *       (the block queue's own status() resynchronises its epochs).
- * The loop thread makes HIP calls on the device current at create time.  The
+ * The loop thread makes HIP calls on the device current at create time.  With
+ * flags & BYTEPS_PROPHET_LOOP_INLINE there is no thread: each push drains the
+ * scheduler and issues the releases itself, in the caller's thread (no
+ * wake-up latency; the pushing threads then make the HIP calls).  The
  * scheduler and block queue must outlive the loop and must not be driven
  * directly while it runs. */
+enum { BYTEPS_PROPHET_LOOP_INLINE = 1 };
 typedef struct byteps_prophet_loop byteps_prophet_loop;
 int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,
                                const int32_t* block_of, int32_t nhandles, int32_t nblocks,
-                               void* release_stream, byteps_prophet_loop** out);
+                               void* release_stream, int flags, byteps_prophet_loop** out);
 int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream);
 int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* t);
 int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s);

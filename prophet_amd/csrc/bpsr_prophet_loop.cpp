@@ -42,6 +42,10 @@ struct byteps_prophet_loop {
   int32_t blocks_released = 0;
   std::vector<char> got;            // task handle pushed this iteration
   int err = 0;
+  bool inline_drain = false;   // BYTEPS_PROPHET_LOOP_INLINE: pushers drain
+  bool waiting = false;        // the loop thread sleeps on cv
+  std::mutex drain_mu;
+  std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
   std::thread th;
 
   int nblocks() const { return (int)block_size.size(); }
@@ -64,42 +68,52 @@ struct byteps_prophet_loop {
     return 0;
   }
 
+  // Drain the scheduler: poll until a zero poll made no progress (a zero poll
+  // may still advance collection or end a block, and the next may release);
+  // at each release group's end, release the complete blocks, then report the
+  // group's partitions finished.  One drainer at a time (drain_mu).
+  int drain() {
+    std::lock_guard<std::mutex> dg(drain_mu);
+    int rc = 0;
+    for (;;) {
+      byteps_prophet_task t;
+      bool prog = false;
+      if (bpsr::prophet_poll(pq, &t, &prog) == 1) {
+        std::lock_guard<std::mutex> g(mu);
+        if (t.handle < block_of.size()) --left[block_of[t.handle]];
+        group_lens.push_back(t.len);
+        continue;
+      }
+      if (!group_lens.empty()) {  // a release group ended
+        {
+          std::lock_guard<std::mutex> g(mu);
+          rc = release_complete();
+        }
+        for (int64_t len : group_lens) byteps_prophet_report_finish(pq, len);
+        group_lens.clear();
+        if (rc) break;
+        continue;  // credit came back: the next poll may release more
+      }
+      if (!prog) break;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    if (rc && !err) err = rc;
+    if (err || blocks_released == nblocks()) done_cv.notify_all();
+    return rc;
+  }
+
   void run() {
     (void)hipSetDevice(device);
-    std::vector<int64_t> group_lens;
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
+      waiting = true;
       cv.wait(lk, [&] { return stop || (active && pushes != seen); });
+      waiting = false;
       if (stop) return;
       seen = pushes;
       lk.unlock();
-      // drain the scheduler: a zero poll that made progress (collection,
-      // end of a block) may be followed by a release without new input
-      int rc = 0;
-      for (;;) {
-        byteps_prophet_task t;
-        bool prog = false;
-        if (bpsr::prophet_poll(pq, &t, &prog) == 1) {
-          lk.lock();
-          if (t.handle < block_of.size()) --left[block_of[t.handle]];
-          lk.unlock();
-          group_lens.push_back(t.len);
-          continue;
-        }
-        if (!group_lens.empty()) {  // a release group ended
-          lk.lock();
-          rc = release_complete();
-          lk.unlock();
-          for (int64_t len : group_lens) byteps_prophet_report_finish(pq, len);
-          group_lens.clear();
-          if (rc) break;
-          continue;  // credit came back: the next poll may release more
-        }
-        if (!prog) break;
-      }
+      drain();
       lk.lock();
-      if (rc && !err) err = rc;
-      if (err || blocks_released == nblocks()) done_cv.notify_all();
     }
   }
 };
@@ -108,7 +122,7 @@ extern "C" {
 
 int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,
                                const int32_t* block_of, int32_t nhandles, int32_t nblocks,
-                               void* release_stream, byteps_prophet_loop** out) {
+                               void* release_stream, int flags, byteps_prophet_loop** out) {
   if (!pq || !bq || !block_of || !out || nhandles < 0 || nblocks < 1)
     return bpsr::fail(BYTEPS_REDUCE_EARGS, "null argument, nhandles < 0 or nblocks < 1");
   *out = nullptr;
@@ -132,7 +146,8 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
     delete l;
     return bpsr::hip_fail(e, "hipGetDevice");
   }
-  l->th = std::thread([l] { l->run(); });
+  l->inline_drain = (flags & BYTEPS_PROPHET_LOOP_INLINE) != 0;
+  if (!l->inline_drain) l->th = std::thread([l] { l->run(); });
   *out = l;
   return 0;
 }
@@ -171,9 +186,10 @@ int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* 
   }
   const int rc = byteps_prophet_add_task(l->pq, t);
   if (rc) return rc;
+  if (l->inline_drain) return l->drain();
   std::lock_guard<std::mutex> g(l->mu);
   ++l->pushes;
-  l->cv.notify_one();
+  if (l->waiting) l->cv.notify_one();
   return 0;
 }
 

@@ -89,7 +89,7 @@ def _lib():
         L.byteps_prophet_get_state.argtypes = [vp, P(_State)]
         L.byteps_prophet_reset.argtypes = [vp]
         L.byteps_prophet_loop_create.argtypes = [vp, vp, P(ctypes.c_int32), ctypes.c_int32,
-                                                 ctypes.c_int32, vp, P(vp)]
+                                                 ctypes.c_int32, vp, ctypes.c_int, P(vp)]
         L.byteps_prophet_loop_begin.argtypes = [vp, vp]
         L.byteps_prophet_loop_push.argtypes = [vp, P(_Task)]
         L.byteps_prophet_loop_end.argtypes = [vp, ctypes.c_double]
@@ -194,16 +194,18 @@ class PushLoop:
     of consecutive blocks on ``release_stream``.  ``block_of[i]`` is the block
     of table partition i; push each partition with its table index.
     Per iteration: ``begin(consumer_stream)``, ``push(task, index)`` per
-    partition as its bytes land, ``end()``."""
+    partition as its bytes land, ``end()``.  ``inline=True``: no loop thread,
+    each push drains the scheduler and issues the releases itself."""
 
-    def __init__(self, queue: ProphetPushQueue, blockq, block_of, release_stream=None):
+    def __init__(self, queue: ProphetPushQueue, blockq, block_of, release_stream=None,
+                 inline: bool = False):
         self._L = _lib()
         self.queue, self.blockq = queue, blockq
         bo = (ctypes.c_int32 * max(len(block_of), 1))(*block_of)
         h = ctypes.c_void_p()
         _ck(self._L.byteps_prophet_loop_create(queue._h, blockq.handle, bo, len(block_of),
                                                blockq.nblocks, _stream_ptr(release_stream),
-                                               ctypes.byref(h)))
+                                               1 if inline else 0, ctypes.byref(h)))
         self._h = h
 
     def begin(self, consumer_stream=None) -> None:

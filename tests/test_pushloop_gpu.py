@@ -76,14 +76,15 @@ def _feed(loop, tasks, seed, skip=None):
         loop.push(t, i)
 
 
+@pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
 @pytest.mark.parametrize("net_b", [10**6, 1000], ids=["whole_blocks", "budget_cuts_blocks"])
-def test_push_loop_iterations_exact(net_b):
+def test_push_loop_iterations_exact(net_b, inline):
     from prophet_amd.prophet import PushLoop
     S = _setup(net_b=net_b)
     cons = torch.cuda.Stream(priority=-100)
     rel = torch.cuda.Stream()
     torch.cuda.synchronize()
-    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel)
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline)
     for it in range(3):
         S["out"].zero_()
         torch.cuda.synchronize()

@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
   // the library's PUSH loop (byteps_prophet_loop_*): one scheduler + loop per
   // input set (each set has its own block queue)
   std::vector<byteps_prophet_queue*> lq(kSets, nullptr);
-  std::vector<byteps_prophet_loop*> loops(kSets, nullptr);
+  std::vector<byteps_prophet_loop*> loops(kSets, nullptr), iloops(kSets, nullptr);
   std::vector<int> left(nb);
   double sched_us = 0;
   long sched_iters = 0, groups_seen = 0, release_calls = 0;
@@ -301,6 +301,15 @@ int main(int argc, char** argv) {
     sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     ++sched_iters;
   };
+  const Fn push_loop_inline = [&](int i) {
+    const int k = i % kSets;
+    const auto t0 = std::chrono::steady_clock::now();
+    CKR(byteps_prophet_loop_begin(iloops[k], cons));
+    for (const auto& t : tasks.arrivals) CKR(byteps_prophet_loop_push(iloops[k], &t));
+    CKR(byteps_prophet_loop_end(iloops[k], 5.0));
+    sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ++sched_iters;
+  };
   const Fn push_loop = [&](int i) {
     const int k = i % kSets;
     const auto t0 = std::chrono::steady_clock::now();
@@ -337,9 +346,12 @@ int main(int argc, char** argv) {
     for (int k = 0; k < kSets; ++k) {
       CKR(byteps_prophet_create(&pc, &lq[k]));
       CKR(byteps_prophet_loop_create(lq[k], sets[k].q, block_of.data(), (int32_t)block_of.size(),
-                                     nb, rel[0], &loops[k]));
+                                     nb, rel[0], 0, &loops[k]));
+      CKR(byteps_prophet_loop_create(lq[k], sets[k].q, block_of.data(), (int32_t)block_of.size(),
+                                     nb, rel[0], BYTEPS_PROPHET_LOOP_INLINE, &iloops[k]));
     }
     variants.push_back({"blockq_prophet_push_loop", &push_loop});
+    variants.push_back({"blockq_prophet_push_loop_inline", &push_loop_inline});
   }
   const double alg = (double)(N + 1) * (double)t.total;
   hipEvent_t e0, e1;
@@ -398,6 +410,7 @@ int main(int argc, char** argv) {
   }
   for (int k = 0; k < kSets; ++k) {
     if (loops[k]) byteps_prophet_loop_destroy(loops[k]);
+    if (iloops[k]) byteps_prophet_loop_destroy(iloops[k]);
     if (lq[k]) byteps_prophet_destroy(lq[k]);
   }
   if (sched) byteps_prophet_destroy(sched);
