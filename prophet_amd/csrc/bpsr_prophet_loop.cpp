@@ -12,7 +12,10 @@
 // group's partitions finished (credit back to the scheduler).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -36,14 +39,16 @@ struct byteps_prophet_loop {
   std::condition_variable done_cv;  // thread -> end()
   bool active = false;
   bool stop = false;
-  uint64_t pushes = 0, seen = 0;
+  std::atomic<uint64_t> pushes{0};
+  uint64_t seen = 0;
   std::vector<int32_t> left;        // partitions not yet released, per block
   std::vector<char> released;       // block released this iteration
   int32_t blocks_released = 0;
   std::vector<char> got;            // task handle pushed this iteration
   int err = 0;
   bool inline_drain = false;   // BYTEPS_PROPHET_LOOP_INLINE: pushers drain
-  bool waiting = false;        // the loop thread sleeps on cv
+  std::atomic<bool> waiting{false};  // the loop thread sleeps on cv
+  int spin_us = 200;           // poll this long for new pushes before sleeping
   std::mutex drain_mu;
   std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
   std::thread th;
@@ -102,17 +107,28 @@ struct byteps_prophet_loop {
     return rc;
   }
 
+  // Like the reference's loops (core_loops.cc polls its queues with a 1-us
+  // sleep), the thread polls for new pushes for spin_us after each drain
+  // before it sleeps: a futex wake-up per release group costs more than the
+  // group's own work.
   void run() {
     (void)hipSetDevice(device);
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      waiting = true;
-      cv.wait(lk, [&] { return stop || (active && pushes != seen); });
-      waiting = false;
+      waiting.store(true);
+      cv.wait(lk, [&] { return stop || (active && pushes.load() != seen); });
+      waiting.store(false);
       if (stop) return;
-      seen = pushes;
       lk.unlock();
-      drain();
+      for (;;) {
+        seen = pushes.load();
+        drain();
+        const auto t0 = std::chrono::steady_clock::now();
+        while (pushes.load() == seen &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us))
+          std::this_thread::yield();
+        if (pushes.load() == seen) break;
+      }
       lk.lock();
     }
   }
@@ -147,6 +163,7 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
     return bpsr::hip_fail(e, "hipGetDevice");
   }
   l->inline_drain = (flags & BYTEPS_PROPHET_LOOP_INLINE) != 0;
+  if (const char* v = getenv("BPSR_LOOP_SPIN_US")) l->spin_us = atoi(v) < 0 ? 0 : atoi(v);
   if (!l->inline_drain) l->th = std::thread([l] { l->run(); });
   *out = l;
   return 0;
@@ -187,9 +204,11 @@ int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* 
   const int rc = byteps_prophet_add_task(l->pq, t);
   if (rc) return rc;
   if (l->inline_drain) return l->drain();
-  std::lock_guard<std::mutex> g(l->mu);
-  ++l->pushes;
-  if (l->waiting) l->cv.notify_one();
+  l->pushes.fetch_add(1);
+  if (l->waiting.load()) {  // the thread sleeps: wake it (else it is polling)
+    std::lock_guard<std::mutex> g(l->mu);
+    l->cv.notify_one();
+  }
   return 0;
 }
 
