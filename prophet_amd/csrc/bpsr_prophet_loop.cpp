@@ -48,7 +48,6 @@ struct byteps_prophet_loop {
   int err = 0;
   bool inline_drain = false;   // BYTEPS_PROPHET_LOOP_INLINE: pushers drain
   std::atomic<bool> waiting{false};  // the loop thread sleeps on cv
-  int spin_us = 200;           // poll this long for new pushes before sleeping
   std::mutex drain_mu;
   std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
   std::thread th;
@@ -107,10 +106,6 @@ struct byteps_prophet_loop {
     return rc;
   }
 
-  // Like the reference's loops (core_loops.cc polls its queues with a 1-us
-  // sleep), the thread polls for new pushes for spin_us after each drain
-  // before it sleeps: a futex wake-up per release group costs more than the
-  // group's own work.
   void run() {
     (void)hipSetDevice(device);
     std::unique_lock<std::mutex> lk(mu);
@@ -119,16 +114,9 @@ struct byteps_prophet_loop {
       cv.wait(lk, [&] { return stop || (active && pushes.load() != seen); });
       waiting.store(false);
       if (stop) return;
+      seen = pushes.load();
       lk.unlock();
-      for (;;) {
-        seen = pushes.load();
-        drain();
-        const auto t0 = std::chrono::steady_clock::now();
-        while (pushes.load() == seen &&
-               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us))
-          std::this_thread::yield();
-        if (pushes.load() == seen) break;
-      }
+      drain();
       lk.lock();
     }
   }
@@ -163,7 +151,6 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
     return bpsr::hip_fail(e, "hipGetDevice");
   }
   l->inline_drain = (flags & BYTEPS_PROPHET_LOOP_INLINE) != 0;
-  if (const char* v = getenv("BPSR_LOOP_SPIN_US")) l->spin_us = atoi(v) < 0 ? 0 : atoi(v);
   if (!l->inline_drain) l->th = std::thread([l] { l->run(); });
   *out = l;
   return 0;
