@@ -705,6 +705,15 @@ def main(argv=None):
         # Parent: start one process per GPU before anything touches the GPU.
         sys.exit(launch_ranks(args.gpus, argv))
 
+    # stdout carries exactly one line, the JSON result: whatever the libraries
+    # write to fd 1 (gloo's connection notes, runtime chatter) goes to stderr
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(obj) -> None:
+        os.write(line_fd, (json.dumps(obj) + "\n").encode())
+
     import torch
     import torch.distributed as dist
 
@@ -892,7 +901,7 @@ def main(argv=None):
                 line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)
             except Exception as e:  # report, never hide
                 line["cpu_baseline"] = {"error": repr(e)}
-        print(json.dumps(line), flush=True)
+        emit(line)
         return
     # N > 1: the headline line is complete; the config-4 legs run after it
     # under a watchdog, so a stuck or failing collective can cost only those
@@ -904,7 +913,7 @@ def main(argv=None):
     def emit_and_maybe_exit(exit_now: bool):
         with lock:
             if rank == 0 and not state["printed"]:
-                print(json.dumps(line), flush=True)
+                emit(line)
                 state["printed"] = True
         if exit_now:
             os._exit(0)

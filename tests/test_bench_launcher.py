@@ -24,9 +24,10 @@ def _run_bench(n, extra=()):
            "--sets", "2", "--no-cpu-baseline", "--scaling-elems", "10007", *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    return json.loads(lines[0])
+    # stdout is exactly the one JSON line: library chatter (gloo's connection
+    # notes on rank 0) is routed to stderr
+    assert len(r.stdout.strip().splitlines()) == 1, r.stdout
+    return json.loads(r.stdout)
 
 
 @pytest.mark.parametrize("n", [1, 2, 3])
