@@ -141,3 +141,51 @@ def test_push_loop_errors_and_missing_partition():
     with pytest.raises(ReduceError):
         S["bq"].status(cons)
     S["bq"].status(cons)                           # reported once, then clear
+
+
+@pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
+def test_push_loop_empty_block_and_fifo_tasks(inline):
+    """A table whose middle block has no partitions (released at begin), and
+    partitions whose tensors do not match Z_keyword (FIFO tasks, released only
+    while no scheduled task is queued, scheduled_queue.cc:292-318): every
+    block still folds, bit-exact, over two iterations."""
+    from prophet_amd.dtypes import DType
+    from prophet_amd.prophet import ProphetPushQueue, PushLoop, PushTask
+    from prophet_amd.reducer import GpuReducer
+    red = GpuReducer(device=0)
+    dev = torch.device("cuda:0")
+    N, n = 5, 70_001
+    lens = [n, 3 * n, 2 * n + 7, n]          # elements per partition (fp32)
+    grads = [3, 2, 1, 0]                      # gradient of each partition
+    fifo = [False, False, True, False]        # partition 2 is not Prophet-scheduled
+    block_of = [0, 0, 2, 2]                   # block 1 is empty
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    ins = [[torch.randn(L, device=dev, generator=gen) for L in lens] for _ in range(N)]
+    outs = [torch.zeros(L, device=dev) for L in lens]
+    blocks = [[], [], []]
+    for i, L in enumerate(lens):
+        blocks[block_of[i]].append((outs[i], [ins[k][i] for k in range(N)], L * 4))
+    bq = red.make_blockq(blocks, DType.FLOAT32)
+    bq.config(wg_per_cu=0, timeout_s=1.0)
+    q = ProphetPushQueue(batch_size=64, net_b=10**6, credit=1 << 30, checkpoints=(-1, 1, 3),
+                         backward_exec=(5, 5, 0))
+    cons, rel = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
+    loop = PushLoop(q, bq, block_of, release_stream=rel, inline=inline)
+    for it in range(2):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        loop.begin(cons)
+        for i in range(len(lens)):
+            loop.push(PushTask(grads[i], 0, lens[i] * 4, 1, grads[i] << 16,
+                               scheduled=not fifo[i]), i)
+        loop.end(timeout_s=5.0)
+        torch.cuda.synchronize()
+        bq.status(cons)
+        for i in range(len(lens)):
+            ref = ins[0][i].clone()
+            for k in range(1, N):
+                ref.add_(ins[k][i])
+            assert torch.equal(outs[i], ref), (it, i)
+    loop.close()
