@@ -145,20 +145,22 @@ def test_push_loop_errors_and_missing_partition():
 
 @pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
 def test_push_loop_empty_block_and_fifo_tasks(inline):
-    """A table whose middle block has no partitions (released at begin), and
-    partitions whose tensors do not match Z_keyword (FIFO tasks, released only
-    while no scheduled task is queued, scheduled_queue.cc:292-318): every
-    block still folds, bit-exact, over two iterations."""
+    """A table whose middle block has no partitions (released at begin), and a
+    partition whose tensor does not match Z_keyword (a FIFO task, released
+    only once no scheduled task is queued, scheduled_queue.cc:292-318; its
+    index lies outside the scheduled model — a model gradient that is not
+    scheduled would stall collection in the reference too): every block still
+    folds, bit-exact, over two iterations."""
     from prophet_amd.dtypes import DType
     from prophet_amd.prophet import ProphetPushQueue, PushLoop, PushTask
     from prophet_amd.reducer import GpuReducer
     red = GpuReducer(device=0)
     dev = torch.device("cuda:0")
     N, n = 5, 70_001
-    lens = [n, 3 * n, 2 * n + 7, n]          # elements per partition (fp32)
-    grads = [3, 2, 1, 0]                      # gradient of each partition
-    fifo = [False, False, True, False]        # partition 2 is not Prophet-scheduled
-    block_of = [0, 0, 2, 2]                   # block 1 is empty
+    lens = [n, 3 * n, 2 * n + 7, n, 5 * n]    # elements per partition (fp32)
+    grads = [3, 2, 1, 0, 77]                  # gradient of each partition
+    fifo = [False, False, False, False, True]  # the last is not Prophet-scheduled
+    block_of = [0, 0, 2, 2, 2]                # block 1 is empty
     gen = torch.Generator(device=dev)
     gen.manual_seed(11)
     ins = [[torch.randn(L, device=dev, generator=gen) for L in lens] for _ in range(N)]
