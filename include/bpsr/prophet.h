@@ -180,7 +180,10 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  * The loop thread makes HIP calls on the device current at create time.  With
  * flags & BYTEPS_PROPHET_LOOP_INLINE there is no thread: each push drains the
  * scheduler and issues the releases itself, in the caller's thread (no
- * wake-up latency; the pushing threads then make the HIP calls).  The
+ * wake-up latency; the pushing threads then make the HIP calls).  Inline, a
+ * pushing thread must not block on the device (hipDeviceSynchronize, hipFree,
+ * a synchronous copy) between begin and its last push: the consumer waits
+ * for releases only that thread would issue, until its timeout.  The
  * scheduler and block queue must outlive the loop and must not be driven
  * directly while it runs. */
 enum { BYTEPS_PROPHET_LOOP_INLINE = 1 };

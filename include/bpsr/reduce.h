@@ -181,7 +181,12 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * up (timeout, ETIMEOUT; the grid always drains).  Launch the consumer on a
  * stream of higher priority than the streams that copy and release
  * (hipStreamCreateWithPriority): priorities get separate hardware queues.
- * Releases on the launch stream itself, before the launch, are always safe. */
+ * Releases on the launch stream itself, before the launch, are always safe.
+ * Likewise on the host: between a live launch and its last release, the
+ * thread that issues the releases must not block on the device
+ * (hipDeviceSynchronize, hipFree — including byteps_reduce_blockq_destroy or
+ * plan_destroy of another object — or a synchronous copy): the consumer is
+ * waiting for the releases that thread has not issued yet. */
 typedef struct byteps_reduce_blockq byteps_reduce_blockq;
 int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
                                 const int* block_end, int nblocks, int dtype, int mode,

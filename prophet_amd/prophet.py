@@ -194,14 +194,17 @@ class PushLoop:
     of consecutive blocks on ``release_stream``.  ``block_of[i]`` is the block
     of table partition i; push each partition with its table index.
     Per iteration: ``begin(consumer_stream)``, ``push(task, index)`` per
-    partition as its bytes land, ``end()``.  ``inline`` (default): no loop
-    thread, each push drains the scheduler and issues the releases itself —
-    measured as fast as a hand-written loop; ``inline=False``: a library
-    thread does it (the reference's shape; the hand-off costs ~40 % at
-    config 3)."""
+    partition as its bytes land, ``end()``.  By default a library thread
+    drains the scheduler and issues the releases (the reference's shape).
+    ``inline=True``: each push does it in the caller's thread — as fast as a
+    hand-written loop, but then that thread must not block
+    on the device (``torch.cuda.synchronize``, a ``hipFree`` — which Python's
+    garbage collector can trigger at any allocation) between ``begin`` and its
+    last push: the consumer would wait for releases the blocked thread cannot
+    issue, until its timeout."""
 
     def __init__(self, queue: ProphetPushQueue, blockq, block_of, release_stream=None,
-                 inline: bool = True):
+                 inline: bool = False):
         self._L = _lib()
         self.queue, self.blockq = queue, blockq
         bo = (ctypes.c_int32 * max(len(block_of), 1))(*block_of)

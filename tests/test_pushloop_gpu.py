@@ -85,6 +85,8 @@ def test_push_loop_iterations_exact(net_b, inline):
     rel = torch.cuda.Stream()
     torch.cuda.synchronize()
     loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline)
+    import gc
+    gc.collect()      # inline: no GC-triggered hipFree may run inside an iteration
     for it in range(3):
         S["out"].zero_()
         torch.cuda.synchronize()
@@ -141,6 +143,11 @@ def test_push_loop_errors_and_missing_partition():
     with pytest.raises(ReduceError):
         S["bq"].status(cons)
     S["bq"].status(cons)                           # reported once, then clear
+    # free the block queue now (its destroy synchronises the device): left to
+    # the garbage collector — `e` keeps this frame alive in a cycle — it could
+    # run inside a later test's live iteration and stall an inline loop
+    del e
+    S["bq"].close()
 
 
 @pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
@@ -174,6 +181,8 @@ def test_push_loop_empty_block_and_fifo_tasks(inline):
                          backward_exec=(5, 5, 0))
     cons, rel = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
     loop = PushLoop(q, bq, block_of, release_stream=rel, inline=inline)
+    import gc
+    gc.collect()      # inline: no GC-triggered hipFree may run inside an iteration
     for it in range(2):
         for o in outs:
             o.zero_()
