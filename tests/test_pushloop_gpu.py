@@ -187,13 +187,23 @@ def test_push_loop_empty_block_and_fifo_tasks(inline):
         for o in outs:
             o.zero_()
         torch.cuda.synchronize()
+        times = []
+        t0 = time.perf_counter()
         loop.begin(cons)
+        times.append(("begin", time.perf_counter() - t0))
         for i in range(len(lens)):
+            t0 = time.perf_counter()
             loop.push(PushTask(grads[i], 0, lens[i] * 4, 1, grads[i] << 16,
                                scheduled=not fifo[i]), i)
+            times.append((f"push{i}", time.perf_counter() - t0))
+        t0 = time.perf_counter()
         loop.end(timeout_s=5.0)
+        times.append(("end", time.perf_counter() - t0))
         torch.cuda.synchronize()
-        bq.status(cons)
+        try:
+            bq.status(cons)
+        except Exception as exc:
+            raise AssertionError(f"iteration {it}: {exc}; host call times {times}") from exc
         for i in range(len(lens)):
             ref = ins[0][i].clone()
             for k in range(1, N):
