@@ -202,6 +202,12 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
                                        void* stream);
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream);
 int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
+/* Debug (synchronises the device): out = launch epoch, nblocks, the sticky
+ * error word, the host's release epoch per block, the device release words,
+ * the device block_first table (nblocks + 1), and 1 if the device tile table
+ * still equals what was uploaded.  Returns the count written (needs
+ * cap >= 4 + 3 * nblocks). */
+int byteps_reduce_blockq_debug(byteps_reduce_blockq* q, uint32_t* out, int cap);
 
 /* CpuReducer::copy(dst, src, len), cpu_reducer.cc:209-220 (device to device). */
 int byteps_reduce_copy(void* dst, const void* src, size_t len, void* stream);

@@ -587,6 +587,7 @@ struct byteps_reduce_blockq {
   std::mutex mu;
   uint32_t launch_epoch = 0;
   std::vector<uint32_t> rel_epoch;  // per block: epoch of its latest release
+  std::vector<char> host_table;     // what was uploaded (byteps_reduce_blockq_debug)
 };
 
 static void blockq_free(byteps_reduce_blockq* q) {
@@ -635,6 +636,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   q->gate_occ = gate_occ;
   q->ti = ti;
   q->rel_epoch.assign((size_t)nblocks, 0u);
+  q->host_table = host;
   int khz = 0;
   hipError_t e = hipGetDevice(&q->device);
   if (e == hipSuccess)
@@ -777,6 +779,31 @@ int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
   return fail(BYTEPS_REDUCE_ETIMEOUT,
               "block queue: a block was not released within %.3f s; the launch stopped early",
               q->timeout_s);
+}
+
+int byteps_reduce_blockq_debug(byteps_reduce_blockq* q, uint32_t* out, int cap) {
+  if (!q || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  const int nb = q->nblocks;
+  const int need = 3 + 3 * nb + 1;
+  if (cap < need) return fail(BYTEPS_REDUCE_EARGS, "cap %d < %d", cap, need);
+  hipError_t e = hipDeviceSynchronize();
+  std::vector<uint32_t> dev(2 * (size_t)nb + 1);
+  if (e == hipSuccess) e = hipMemcpy(dev.data(), q->flags, dev.size() * 4, hipMemcpyDeviceToHost);
+  uint32_t err = 0;
+  if (e == hipSuccess) e = hipMemcpy(&err, &q->ctl->err, 4, hipMemcpyDeviceToHost);
+  std::vector<char> tab(q->host_table.size());
+  if (e == hipSuccess && !tab.empty())
+    e = hipMemcpy(tab.data(), q->dev_table, tab.size(), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "blockq debug");
+  std::lock_guard<std::mutex> g(q->mu);
+  int k = 0;
+  out[k++] = q->launch_epoch;
+  out[k++] = (uint32_t)nb;
+  out[k++] = err;
+  for (int b = 0; b < nb; ++b) out[k++] = q->rel_epoch[b];
+  for (size_t i = 0; i < dev.size(); ++i) out[k++] = dev[i];   // words, then block_first
+  out[k++] = tab == q->host_table ? 1u : 0u;
+  return k;
 }
 
 int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q) {

@@ -50,6 +50,7 @@ EXPORTS = (
     "byteps_reduce_plan_create", "byteps_reduce_plan_launch", "byteps_reduce_plan_destroy",
     "byteps_reduce_blockq_create", "byteps_reduce_blockq_config", "byteps_reduce_blockq_launch",
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
+    "byteps_reduce_blockq_debug",
     "byteps_reduce_blockq_release_range",
 )
 
@@ -104,6 +105,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_release_range.argtypes = [_vp, _int, _int, _vp]
     L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
+    L.byteps_reduce_blockq_debug.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint32), _int]
     _LIB = L
     return L
 
@@ -296,6 +298,18 @@ class BlockQueue:
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))
+
+    def debug(self) -> dict:
+        """byteps_reduce_blockq_debug (synchronises the device)."""
+        nb = self.nblocks
+        buf = (ctypes.c_uint32 * (4 + 3 * nb + 8))()
+        k = self.lib.byteps_reduce_blockq_debug(self.handle, buf, len(buf))
+        if k < 0:
+            _check(k)
+        v = list(buf[:k])
+        return {"launch_epoch": v[0], "nblocks": v[1], "err": v[2],
+                "rel_epoch": v[3:3 + nb], "words": v[3 + nb:3 + 2 * nb],
+                "block_first": v[3 + 2 * nb:4 + 3 * nb], "table_intact": bool(v[-1])}
 
     def close(self) -> None:
         if self.handle:

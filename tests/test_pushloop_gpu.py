@@ -203,7 +203,8 @@ def test_push_loop_empty_block_and_fifo_tasks(inline):
         try:
             bq.status(cons)
         except Exception as exc:
-            raise AssertionError(f"iteration {it}: {exc}; host call times {times}") from exc
+            raise AssertionError(f"iteration {it}: {exc}; host call times {times}; "
+                                 f"block queue {bq.debug()}") from exc
         for i in range(len(lens)):
             ref = ins[0][i].clone()
             for k in range(1, N):
