@@ -588,9 +588,33 @@ struct byteps_reduce_blockq {
   uint32_t launch_epoch = 0;
   std::vector<uint32_t> rel_epoch;  // per block: epoch of its latest release
   std::vector<char> host_table;     // what was uploaded (byteps_reduce_blockq_debug)
+  // The consumer runs on a stream of its own with an explicit all-CU mask —
+  // the runtime gives such a stream a dedicated hardware queue — ordered into
+  // the caller's stream by a fork/join event pair.  A live release must never
+  // sit behind the spinning consumer in a shared in-order hardware queue, and
+  // stream priority alone does not guarantee separate queues (measured:
+  // torch's pooled high- and normal-priority streams shared one for some pool
+  // indices, tools/pushloop_diag.py).
+  bool own_queue = true;
+  hipStream_t own = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
+static hipError_t blockq_own_stream(byteps_reduce_blockq* q) {
+  if (q->own) return hipSuccess;
+  std::vector<uint32_t> mask((size_t)(q->cus + 31) / 32, 0u);
+  for (int c = 0; c < q->cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+  hipError_t e = hipExtStreamCreateWithCUMask(&q->own, (uint32_t)mask.size(), mask.data());
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&q->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&q->join_ev, hipEventDisableTiming);
+  return e;
+}
+
 static void blockq_free(byteps_reduce_blockq* q) {
+  if (q->own) (void)hipStreamSynchronize(q->own);
+  if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
+  if (q->join_ev) (void)hipEventDestroy(q->join_ev);
+  if (q->own) (void)hipStreamDestroy(q->own);
   if (q->dev_table) (void)hipFree(q->dev_table);
   if (q->flags) (void)hipFree(q->flags);
   if (q->ctl) (void)hipFree(q->ctl);
@@ -637,6 +661,7 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   q->ti = ti;
   q->rel_epoch.assign((size_t)nblocks, 0u);
   q->host_table = host;
+  if (const char* v = getenv("BPSR_BQ_OWN_QUEUE")) q->own_queue = atoi(v) != 0;
   int khz = 0;
   hipError_t e = hipGetDevice(&q->device);
   if (e == hipSuccess)
@@ -644,7 +669,10 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   if (e == hipSuccess)
     e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, q->device);
   q->clock_khz = khz > 0 ? (uint64_t)khz : 100000;
-  const size_t flag_bytes = sizeof(uint32_t) * (2 * (size_t)nblocks + 1);
+  // The release words and the control word get allocations of their own,
+  // padded to whole 256-B lines: nothing else may share their cache lines.
+  const size_t flag_bytes =
+      (sizeof(uint32_t) * (2 * (size_t)nblocks + 1) + 255) & ~(size_t)255;
   if (e == hipSuccess && ti.tiles > 0) e = hipMalloc(&q->dev_table, ti.bytes);
   if (e == hipSuccess && ti.tiles > 0)
     e = hipMemcpy(q->dev_table, host.data(), ti.bytes, hipMemcpyHostToDevice);
@@ -653,8 +681,8 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   if (e == hipSuccess)
     e = hipMemcpy(q->flags + nblocks, first.data(), sizeof(uint32_t) * (nblocks + 1),
                   hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->ctl), sizeof(BlockqCtl));
-  if (e == hipSuccess) e = hipMemset(q->ctl, 0, sizeof(BlockqCtl));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->ctl), 256);
+  if (e == hipSuccess) e = hipMemset(q->ctl, 0, 256);
   if (e == hipSuccess) e = hipDeviceSynchronize();  // words zeroed before any stream uses them
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&q->host_err), sizeof(uint32_t));
@@ -720,7 +748,21 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     // residency cap through LDS (the kernel's own static LDS included)
     lds = ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255;
   }
-  hipError_t e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, s);
+  // Outside a capture the consumer runs on the queue's own hardware queue,
+  // forked from and joined back into `s` (a captured launch is pre-released
+  // by rule, so it may run on the capturing stream itself).
+  const bool fork = q->own_queue && cap != hipStreamCaptureStatusActive;
+  hipError_t e = hipSuccess;
+  hipStream_t ls = s;
+  if (fork) {
+    e = blockq_own_stream(q);
+    if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(q->own, q->fork_ev, 0);
+    ls = q->own;
+  }
+  if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, ls);
+  if (fork && e == hipSuccess) e = hipEventRecord(q->join_ev, q->own);
+  if (fork && e == hipSuccess) e = hipStreamWaitEvent(s, q->join_ev, 0);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
 }
 

@@ -16,8 +16,25 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+_HIP = None
+
+
+def cu_mask_stream(torch):
+    """A stream with an explicit all-CU mask: the runtime gives such a stream a
+    hardware queue of its own (no multiplexing with other streams)."""
+    import ctypes
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    mask = (ctypes.c_uint32 * 8)(*([0xFFFFFFFF] * 8))
+    rc = _HIP.hipExtStreamCreateWithCUMask(ctypes.byref(s), 8, mask)
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(s.value)
+
+
 def small_case(torch, red, dt_name="f32", N=5, empty=True, fifo=True, inline=False, occ=0,
-               timeout=1.0, sync_before=True):
+               timeout=1.0, sync_before=True, cons_kind="pool_high"):
     from prophet_amd.dtypes import DType
     from prophet_amd.prophet import ProphetPushQueue, PushLoop, PushTask
     from prophet_amd.reducer import ReduceError
@@ -41,7 +58,8 @@ def small_case(torch, red, dt_name="f32", N=5, empty=True, fifo=True, inline=Fal
     bq.config(wg_per_cu=occ, timeout_s=timeout)
     q = ProphetPushQueue(batch_size=64, net_b=10**6, credit=1 << 30, checkpoints=(-1, 1, 3),
                          backward_exec=(5, 5, 0))
-    cons, rel = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
+    rel = torch.cuda.Stream()
+    cons = cu_mask_stream(torch) if cons_kind == "cu_mask" else torch.cuda.Stream(priority=-100)
     loop = PushLoop(q, bq, block_of, release_stream=rel, inline=inline)
     if sync_before:
         torch.cuda.synchronize()
@@ -104,6 +122,7 @@ def main():
                 ("fp16", {"dt_name": "f16"}), ("N8", {"N": 8}), ("inline", {"inline": True}),
                 ("timeout5s", {"timeout": 5.0}), ("persistent_occ1", {"occ": 1}),
                 ("as_test_last", {})]
+    variants += [(f"cu_mask_consumer_{k}", {"cons_kind": "cu_mask"}) for k in range(8)]
     for name, kw in variants:
         t0 = time.perf_counter()
         r = small_case(torch, red, **kw)
