@@ -579,8 +579,9 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                               for p in bp] for bp in by_block], DType.FLOAT16)
         q.config(wg_per_cu=0, timeout_s=1.0)
         queues.append(q)
-    # the consumer outranks the release stream: its own hardware queue
-    live_s = torch.cuda.Stream(device=dev, priority=-100)
+    # the library's consumer stream: a hardware queue of its own, so a release
+    # never waits behind the spinning consumer (include/bpsr/reduce.h)
+    live_s = queues[0].stream()
     rel_s = torch.cuda.Stream(device=dev)
     nb = len(by_block)
 

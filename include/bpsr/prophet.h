@@ -166,7 +166,8 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  * table holds the iteration's partitions; block_of[h] is the block of the
  * partition whose task handle is h (0 <= h < nhandles).  Per iteration:
  *   byteps_prophet_loop_begin(l, consumer_stream)  resets the scheduler and
- *       launches the block queue's consumer (one launch per iteration);
+ *       launches the block queue's consumer (one launch per iteration; NULL:
+ *       on the library's consumer stream, byteps_reduce_blockq_stream);
  *   byteps_prophet_loop_push(l, &task)  one per partition as its bytes land
  *       (their copies queued on release_stream, or finished), in any order —
  *       the loop thread polls getTask and, at the end of each release group,

@@ -178,10 +178,16 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * hardware queues: HIP multiplexes streams onto a few in-order hardware queues
  * per process (GPU_MAX_HW_QUEUES, 4 by default), and a release queued behind
  * the running consumer in a shared queue cannot run until the consumer gives
- * up (timeout, ETIMEOUT; the grid always drains).  Launch the consumer on a
- * stream of higher priority than the streams that copy and release
- * (hipStreamCreateWithPriority): priorities get separate hardware queues.
- * Releases on the launch stream itself, before the launch, are always safe.
+ * up (timeout, ETIMEOUT; the grid always drains).  Stream priority does not
+ * guarantee separate queues (measured), so the consumer always runs on the
+ * library's consumer stream for the device — an all-CU-masked stream, which
+ * the runtime gives a hardware queue of its own (byteps_reduce_blockq_stream).
+ * Launching on that stream costs nothing extra and orders launches and status
+ * calls there; launching on any other stream forks onto it and joins back
+ * (two events — ~0.14 ms per iteration at config 3, so launch on the consumer
+ * stream when iterations run back to back).  A launch inside a hipGraph
+ * capture stays on the capturing stream (pre-released by rule).  Releases on
+ * the launch stream itself, before the launch, are always safe.
  * Likewise on the host: between a live launch and its last release, the
  * thread that issues the releases must not block on the device
  * (hipDeviceSynchronize, hipFree — including byteps_reduce_blockq_destroy or
@@ -202,6 +208,8 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
                                        void* stream);
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream);
 int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
+/* The device's consumer stream (see above); owned by the library. */
+int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream);
 /* Debug (synchronises the device): out = launch epoch, nblocks, the sticky
  * error word, the host's release epoch per block, the device release words,
  * the device block_first table (nblocks + 1), and 1 if the device tile table

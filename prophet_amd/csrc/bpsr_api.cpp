@@ -588,33 +588,54 @@ struct byteps_reduce_blockq {
   uint32_t launch_epoch = 0;
   std::vector<uint32_t> rel_epoch;  // per block: epoch of its latest release
   std::vector<char> host_table;     // what was uploaded (byteps_reduce_blockq_debug)
-  // The consumer runs on a stream of its own with an explicit all-CU mask —
-  // the runtime gives such a stream a dedicated hardware queue — ordered into
-  // the caller's stream by a fork/join event pair.  A live release must never
-  // sit behind the spinning consumer in a shared in-order hardware queue, and
-  // stream priority alone does not guarantee separate queues (measured:
-  // torch's pooled high- and normal-priority streams shared one for some pool
+  // The consumer runs on the device's consumer stream (an explicit all-CU
+  // mask: the runtime gives such a stream a hardware queue of its own),
+  // forked from and joined into the caller's stream unless the caller
+  // launches on that stream itself.  A live release must never sit behind
+  // the spinning consumer in a shared in-order hardware queue, and stream
+  // priority alone does not guarantee separate queues (measured: torch's
+  // pooled high- and normal-priority streams shared one for some pool
   // indices, tools/pushloop_diag.py).
   bool own_queue = true;
-  hipStream_t own = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
 };
 
-static hipError_t blockq_own_stream(byteps_reduce_blockq* q) {
-  if (q->own) return hipSuccess;
-  std::vector<uint32_t> mask((size_t)(q->cus + 31) / 32, 0u);
-  for (int c = 0; c < q->cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-  hipError_t e = hipExtStreamCreateWithCUMask(&q->own, (uint32_t)mask.size(), mask.data());
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&q->fork_ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&q->join_ev, hipEventDisableTiming);
+// One consumer stream per device, created on first use, never destroyed:
+// every block queue's consumer on a device runs on it (in launch order).
+static std::mutex g_consumer_mu;
+static hipStream_t g_consumer[64];
+
+static hipError_t consumer_stream(int device, int cus, hipStream_t* out) {
+  if (device < 0 || device >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> g(g_consumer_mu);
+  if (!g_consumer[device]) {
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    hipError_t e = hipExtStreamCreateWithCUMask(&g_consumer[device], (uint32_t)mask.size(),
+                                                mask.data());
+    if (cur != device && cur >= 0) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      g_consumer[device] = nullptr;
+      return e;
+    }
+  }
+  *out = g_consumer[device];
+  return hipSuccess;
+}
+
+static hipError_t blockq_events(byteps_reduce_blockq* q) {
+  hipError_t e = hipSuccess;
+  if (!q->fork_ev) e = hipEventCreateWithFlags(&q->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess && !q->join_ev) e = hipEventCreateWithFlags(&q->join_ev, hipEventDisableTiming);
   return e;
 }
 
 static void blockq_free(byteps_reduce_blockq* q) {
-  if (q->own) (void)hipStreamSynchronize(q->own);
   if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
   if (q->join_ev) (void)hipEventDestroy(q->join_ev);
-  if (q->own) (void)hipStreamDestroy(q->own);
   if (q->dev_table) (void)hipFree(q->dev_table);
   if (q->flags) (void)hipFree(q->flags);
   if (q->ctl) (void)hipFree(q->ctl);
@@ -751,17 +772,18 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   // Outside a capture the consumer runs on the queue's own hardware queue,
   // forked from and joined back into `s` (a captured launch is pre-released
   // by rule, so it may run on the capturing stream itself).
-  const bool fork = q->own_queue && cap != hipStreamCaptureStatusActive;
+  hipStream_t own = nullptr;
   hipError_t e = hipSuccess;
-  hipStream_t ls = s;
+  if (q->own_queue && cap != hipStreamCaptureStatusActive) e = consumer_stream(q->device, q->cus, &own);
+  const bool fork = own && s != own;
+  hipStream_t ls = own ? own : s;
   if (fork) {
-    e = blockq_own_stream(q);
+    e = blockq_events(q);
     if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(q->own, q->fork_ev, 0);
-    ls = q->own;
+    if (e == hipSuccess) e = hipStreamWaitEvent(own, q->fork_ev, 0);
   }
   if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, ls);
-  if (fork && e == hipSuccess) e = hipEventRecord(q->join_ev, q->own);
+  if (fork && e == hipSuccess) e = hipEventRecord(q->join_ev, own);
   if (fork && e == hipSuccess) e = hipStreamWaitEvent(s, q->join_ev, 0);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
 }
@@ -821,6 +843,15 @@ int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
   return fail(BYTEPS_REDUCE_ETIMEOUT,
               "block queue: a block was not released within %.3f s; the launch stopped early",
               q->timeout_s);
+}
+
+int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream) {
+  if (!q || !stream) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  hipStream_t s = nullptr;
+  hipError_t e = consumer_stream(q->device, q->cus, &s);
+  if (e != hipSuccess) return hip_fail(e, "consumer stream");
+  *stream = reinterpret_cast<void*>(s);
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_reduce_blockq_debug(byteps_reduce_blockq* q, uint32_t* out, int cap) {

@@ -165,6 +165,7 @@ int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream) {
   if (pend) return bpsr::fail(BYTEPS_REDUCE_EARGS, "scheduler holds %llu tasks", (unsigned long long)pend);
   int rc = byteps_prophet_reset(l->pq);
   if (rc) return rc;
+  if (!consumer_stream && (rc = byteps_reduce_blockq_stream(l->bq, &consumer_stream))) return rc;
   if ((rc = byteps_reduce_blockq_launch(l->bq, consumer_stream))) return rc;
   l->left = l->block_size;
   l->released.assign(l->block_size.size(), 0);

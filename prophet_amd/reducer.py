@@ -50,7 +50,7 @@ EXPORTS = (
     "byteps_reduce_plan_create", "byteps_reduce_plan_launch", "byteps_reduce_plan_destroy",
     "byteps_reduce_blockq_create", "byteps_reduce_blockq_config", "byteps_reduce_blockq_launch",
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
-    "byteps_reduce_blockq_debug",
+    "byteps_reduce_blockq_debug", "byteps_reduce_blockq_stream",
     "byteps_reduce_blockq_release_range",
 )
 
@@ -106,6 +106,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     L.byteps_reduce_blockq_debug.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint32), _int]
+    L.byteps_reduce_blockq_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     _LIB = L
     return L
 
@@ -298,6 +299,14 @@ class BlockQueue:
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))
+
+    def stream(self):
+        """The device's consumer stream (byteps_reduce_blockq_stream) as a
+        torch ExternalStream: launch here to skip the fork/join onto it."""
+        import torch
+        p = _vp()
+        _check(self.lib.byteps_reduce_blockq_stream(self.handle, ctypes.byref(p)))
+        return torch.cuda.ExternalStream(p.value)
 
     def debug(self) -> dict:
         """byteps_reduce_blockq_debug (synchronises the device)."""

@@ -81,7 +81,7 @@ def _feed(loop, tasks, seed, skip=None):
 def test_push_loop_iterations_exact(net_b, inline):
     from prophet_amd.prophet import PushLoop
     S = _setup(net_b=net_b)
-    cons = torch.cuda.Stream(priority=-100)
+    cons = S["bq"].stream()              # the library's consumer stream
     rel = torch.cuda.Stream()
     torch.cuda.synchronize()
     loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline)

@@ -234,7 +234,7 @@ def cfg3(red, dev, N=8, sets=3):
     # own, so the releases on rel_stream never sit behind it in a shared queue
     # (include/bpsr/reduce.h; under rocprofv3 with both at normal priority the
     # first live launch of each queue waited out its 5-s timeout).
-    live_stream = torch.cuda.Stream(priority=-100)
+    live_stream = bqs[0][0].stream()     # the library's consumer stream
     nblk = len(by_block)
 
     def blockq_live(i, occ=0):

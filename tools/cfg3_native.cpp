@@ -218,7 +218,13 @@ int main(int argc, char** argv) {
   int lo = 0, hi = 0;
   CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   hipStream_t cons, rel[2];
-  CK(hipStreamCreateWithPriority(&cons, hipStreamNonBlocking, hi));  // own hardware queue
+  if (getenv("CFG3_PRIORITY_CONSUMER")) {  // A/B: a caller stream (fork/join onto the library's)
+    CK(hipStreamCreateWithPriority(&cons, hipStreamNonBlocking, hi));
+  } else {  // the library's consumer stream: a hardware queue of its own
+    void* cs = nullptr;
+    CKR(byteps_reduce_blockq_stream(sets[0].q, &cs));
+    cons = reinterpret_cast<hipStream_t>(cs);
+  }
   CK(hipStreamCreateWithFlags(&rel[0], hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&rel[1], hipStreamNonBlocking));
   for (auto& s : sets) CKR(byteps_reduce_plan_launch(s.plan_ref, cons));
