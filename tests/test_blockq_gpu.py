@@ -335,3 +335,44 @@ def test_release_range_and_capture_rule(red, dev):
     assert ei.value.code == EARGS
     torch.cuda.synchronize()
     q.close()
+
+
+def test_live_release_never_behind_consumer_any_stream_pair():
+    """Regression: stream priority does not separate hardware queues — with
+    torch's pooled streams the 5th and 9th (high, normal) pairs of a process
+    shared one, and a live release queued behind the spinning consumer timed
+    out (tools/pushloop_diag.py).  The consumer now always runs on the
+    library's consumer stream (its own hardware queue), forked from the
+    caller's stream: for 12 successive pool pairs, launch on the high-priority
+    stream, release on the normal one after the consumer started — every
+    iteration completes, bit-exact."""
+    import time as _time
+    from prophet_amd.dtypes import DType
+    from prophet_amd.reducer import GpuReducer
+    red = GpuReducer(device=0)
+    dev = torch.device("cuda:0")
+    n, N = 1 << 16, 4
+    ins = [[torch.randn(n, device=dev) for _ in range(N)] for _ in range(2)]
+    outs = [torch.zeros(n, device=dev) for _ in range(2)]
+    bq = red.make_blockq([[(outs[b], ins[b], n * 4)] for b in range(2)], DType.FLOAT32)
+    bq.config(wg_per_cu=0, timeout_s=1.0)
+    refs = []
+    for b in range(2):
+        r = ins[b][0].clone()
+        for x in ins[b][1:]:
+            r.add_(x)
+        refs.append(r)
+    for i in range(12):
+        cons = torch.cuda.Stream(priority=-100)
+        rel = torch.cuda.Stream()
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        bq.launch(cons)
+        _time.sleep(0.002)
+        bq.release(0, rel)
+        bq.release(1, rel)
+        torch.cuda.synchronize()
+        bq.status(cons)                               # raises on a timeout
+        assert all(torch.equal(o, r) for o, r in zip(outs, refs)), i
+    bq.close()
