@@ -211,3 +211,24 @@ def test_push_loop_empty_block_and_fifo_tasks(inline):
                 ref.add_(ins[k][i])
             assert torch.equal(outs[i], ref), (it, i)
     loop.close()
+
+
+def test_diagnosis_sequence_all_cases_pass():
+    """The sequence that exposed the shared hardware queue (tools/
+    pushloop_diag.py: a config-3 iteration, then small tables with one factor
+    changed at a time; before the consumer had a queue of its own the 5th and
+    9th cases timed out every time, profiles/r02_pushloop_diag_before.jsonl)
+    runs clean, in a process of its own."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "pushloop_diag.py")],
+                       capture_output=True, text=True, timeout=200, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    cases = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(cases) >= 12
+    bad = [c["case"] for c in cases if '"status_ok": false' in json.dumps(c)
+           or '"exact": false' in json.dumps(c)]
+    assert not bad, bad
