@@ -175,7 +175,9 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  *       of consecutive blocks, on release_stream), then reports the group's
  *       partitions finished;
  *   byteps_prophet_loop_end(l, timeout_s)  waits until every block has been
- *       released (timeout_s <= 0: no limit).  ETIMEOUT leaves the scheduler
+ *       released (timeout_s <= 0: no limit); with the loop thread, a task the
+ *       scheduler refuses (e.g. a gradient outside the model) is reported
+ *       here, since the thread adds the pushes.  ETIMEOUT leaves the scheduler
  *       holding the missing partitions' state: destroy the loop and the queue
  *       (the block queue's own status() resynchronises its epochs).
  * The loop thread makes HIP calls on the device current at create time.  With

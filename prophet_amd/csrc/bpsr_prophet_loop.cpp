@@ -50,6 +50,10 @@ struct byteps_prophet_loop {
   std::atomic<bool> waiting{false};  // the loop thread sleeps on cv
   std::mutex drain_mu;
   std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
+  // thread mode: pushes land in an inbox the loop thread empties into the
+  // scheduler itself, so pushers and the drain never contend on its lock
+  std::mutex inbox_mu;
+  std::vector<byteps_prophet_task> inbox, taken;
   std::thread th;
 
   int nblocks() const { return (int)block_size.size(); }
@@ -116,7 +120,21 @@ struct byteps_prophet_loop {
       if (stop) return;
       seen = pushes.load();
       lk.unlock();
-      drain();
+      {
+        std::lock_guard<std::mutex> g(inbox_mu);
+        taken.swap(inbox);
+      }
+      int rc = 0;
+      for (const auto& t : taken)
+        if (!rc) rc = byteps_prophet_add_task(pq, &t);
+      taken.clear();
+      if (rc) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!err) err = rc;
+        done_cv.notify_all();
+      } else {
+        drain();
+      }
       lk.lock();
     }
   }
@@ -162,6 +180,10 @@ int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream) {
   if (l->active) return bpsr::fail(BYTEPS_REDUCE_EARGS, "iteration already begun (end it first)");
   uint64_t pend = 0;
   byteps_prophet_pending(l->pq, &pend);
+  {
+    std::lock_guard<std::mutex> ig(l->inbox_mu);
+    pend += l->inbox.size();
+  }
   if (pend) return bpsr::fail(BYTEPS_REDUCE_EARGS, "scheduler holds %llu tasks", (unsigned long long)pend);
   int rc = byteps_prophet_reset(l->pq);
   if (rc) return rc;
@@ -189,9 +211,15 @@ int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* 
                         (unsigned long long)t->handle);
     l->got[t->handle] = 1;
   }
-  const int rc = byteps_prophet_add_task(l->pq, t);
-  if (rc) return rc;
-  if (l->inline_drain) return l->drain();
+  if (l->inline_drain) {
+    const int rc = byteps_prophet_add_task(l->pq, t);
+    if (rc) return rc;
+    return l->drain();
+  }
+  {
+    std::lock_guard<std::mutex> g(l->inbox_mu);
+    l->inbox.push_back(*t);
+  }
   l->pushes.fetch_add(1);
   if (l->waiting.load()) {  // the thread sleeps: wake it (else it is polling)
     std::lock_guard<std::mutex> g(l->mu);
