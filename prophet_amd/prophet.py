@@ -195,9 +195,10 @@ class PushLoop:
     of table partition i; push each partition with its table index.
     Per iteration: ``begin(consumer_stream)``, ``push(task, index)`` per
     partition as its bytes land, ``end()``.  By default a library thread
-    drains the scheduler and issues the releases (the reference's shape).
-    ``inline=True``: each push does it in the caller's thread — as fast as a
-    hand-written loop, but then that thread must not block
+    drains the scheduler and issues the releases (the reference's shape; at
+    config 3 as fast as a hand-written loop).
+    ``inline=True``: each push does it in the caller's thread — fewer host
+    cycles and no thread hand-off, but then that thread must not block
     on the device (``torch.cuda.synchronize``, a ``hipFree`` — which Python's
     garbage collector can trigger at any allocation) between ``begin`` and its
     last push: the consumer would wait for releases the blocked thread cannot
