@@ -30,7 +30,7 @@ def _run_bench(n, extra=()):
     return json.loads(r.stdout)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_launcher_one_line_n_ranks(n):
     line = _run_bench(n)
     assert line["n_gpus"] == n
