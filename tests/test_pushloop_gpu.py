@@ -232,3 +232,30 @@ def test_diagnosis_sequence_all_cases_pass():
     bad = [c["case"] for c in cases if '"status_ok": false' in json.dumps(c)
            or '"exact": false' in json.dumps(c)]
     assert not bad, bad
+
+
+def test_push_loop_thread_keeps_releasing_while_pusher_frees():
+    """Thread mode: the pushing thread may block on the device right after its
+    last push — here it destroys a plan (hipFree synchronises the device)
+    while the loop thread still has releases to issue.  The loop thread's
+    launches are not held up by the blocked thread, so the consumer completes
+    instead of waiting out its timeout."""
+    from prophet_amd.dtypes import DType
+    from prophet_amd.prophet import PushLoop
+    S = _setup(seed=5)
+    red = S["red"]
+    rel = torch.cuda.Stream()
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=False)
+    x = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    for it in range(3):
+        torch.cuda.synchronize()
+        loop.begin()
+        for t, i in S["tasks"]:
+            loop.push(t, i)
+        plan = red.make_plan([(x, [x, x], x.numel())], DType.UINT8)
+        plan.close()                                  # hipFree while releases are pending
+        loop.end(timeout_s=10.0)
+        torch.cuda.synchronize()
+        S["bq"].status()
+        assert torch.equal(S["out"], S["ref"].view(torch.uint8)), it
+    loop.close()
