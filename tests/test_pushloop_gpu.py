@@ -246,13 +246,13 @@ def test_push_loop_thread_keeps_releasing_while_pusher_frees():
     red = S["red"]
     rel = torch.cuda.Stream()
     loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=False)
-    x = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    x, y, z = (torch.zeros(1 << 20, dtype=torch.uint8, device="cuda") for _ in range(3))
     for it in range(3):
         torch.cuda.synchronize()
         loop.begin()
         for t, i in S["tasks"]:
             loop.push(t, i)
-        plan = red.make_plan([(x, [x, x], x.numel())], DType.UINT8)
+        plan = red.make_plan([(x, [y, z], x.numel())], DType.UINT8)
         plan.close()                                  # hipFree while releases are pending
         loop.end(timeout_s=10.0)
         torch.cuda.synchronize()
