@@ -6,9 +6,10 @@ uniform(-100, 100) values drawn with one seed (identical on every rank), cast
 to int32 / int64 / float32 / float64, and push_pulls them in place; the result
 must equal tensor * size within the reference's ladder — 0 when size <= 3 or
 for integers, 1e-4 below 10 ranks, 5e-4 below 15 — compared exactly as the
-reference does: max(result - tensor * size), signed, in the tensor's dtype.  Ranks are worker threads talking to the
-GPU-resident server through pushpull.Worker (InitTensor keys, partitions,
-Cantor request word), tensors on the device.  The bits are also checked
+reference does: max(result - tensor * size), signed, in the tensor's dtype.
+Ranks are worker threads talking to the GPU-resident server through
+pushpull.Worker (InitTensor keys, partitions, Cantor request word), tensors on
+the device.  The bits are also checked
 against the oracle's left fold of the same inputs, which is the stricter
 parity bar."""
 import itertools
