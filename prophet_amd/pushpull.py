@@ -139,6 +139,18 @@ class Worker:
         for key, off, ln in ctx.parts:
             self.frontend.pull(key, _slice(out, off, ln), ln)
 
+    def broadcast(self, name: str, tensor, root_rank: int, output=None):
+        """Broadcast as BytePS does it (byteps/torch/__init__.py:264-272: "push +
+        pull ... the non-root tensors all 0", no averaging): the root pushes its
+        tensor, every other rank pushes zeros, everyone pulls the sum into
+        ``output`` (a new buffer like ``tensor`` if not given; the source is
+        left untouched, as test_mxnet.py:116-158 requires).  The tensor must
+        have been through ``init_tensor``."""
+        src = tensor if self.rank == root_rank else _zeros_like(tensor)
+        out = _zeros_like(tensor) if output is None else output
+        self.push_pull(name, src, output=out)
+        return out
+
     def push_pull_iteration(self, tensors: dict, scheduler=None) -> list:
         """One training iteration: every declared tensor, gradients arriving in
         backward order (highest declared index first).  With a Prophet
@@ -173,6 +185,14 @@ def _nbytes(x) -> int:
     if hasattr(x, "nbytes") and not hasattr(x, "data_ptr"):
         return int(x.nbytes)                               # numpy
     return int(x.numel() * x.element_size())               # torch
+
+
+def _zeros_like(x):
+    if hasattr(x, "data_ptr"):                             # torch
+        import torch
+        return torch.zeros_like(x)
+    import numpy as np
+    return np.zeros_like(x)
 
 
 def _slice(x, off: int, ln: int):

@@ -89,3 +89,48 @@ def test_byteps_push_pull_inplace_known_answer(size):
                 diff = float(np.max(got - multiplied))
                 assert diff <= thr, (name, dtype, r, diff, thr)
     srv.close()
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_byteps_broadcast(size):
+    """tests/test_mxnet.py:116-158 on this build: every (dtype, dim, root rank)
+    — tensor = ones * rank, broadcast from root_rank through push_pull with
+    zeros on the non-root ranks (byteps/torch/__init__.py:264-272); the
+    result equals ones * root_rank on every rank, bit for bit, and the source
+    tensors are not modified."""
+    from prophet_amd.pushpull import ServerFrontend, Worker
+    from prophet_amd.server import PSServer
+    srv = PSServer(size, engine_lanes=2)
+    fe = ServerFrontend(srv)
+    workers = [Worker(r, fe) for r in range(size)]
+    cases = [(f"{len_}", dtype, dim, root)
+             for len_, (dtype, dim, root) in enumerate(
+                 itertools.product(DTYPES, [1, 2, 3], range(size)))]
+    src = {(r, c[0]): (torch.ones(SHAPES[c[2]], device="cuda") * r).to(DTYPES[c[1]][2])
+           for r in range(size) for c in cases}
+    results, errors = {}, []
+
+    def run(w):
+        try:
+            for name, dtype, dim, root in cases:
+                w.declare(name)
+                w.init_tensor(name, src[(w.rank, name)], DTYPES[dtype][0])
+            for name, dtype, dim, root in cases:
+                results[(w.rank, name)] = w.broadcast(name, src[(w.rank, name)], root)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=run, args=(w,)) for w in workers]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=180)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for name, dtype, dim, root in cases:
+        want = (torch.ones(SHAPES[dim], device="cuda") * root).to(DTYPES[dtype][2])
+        for r in range(size):
+            assert torch.equal(results[(r, name)], want), (name, dtype, dim, root, r)
+            mine = (torch.ones(SHAPES[dim], device="cuda") * r).to(DTYPES[dtype][2])
+            assert torch.equal(src[(r, name)], mine), "broadcast modified its source"
+    srv.close()
