@@ -113,3 +113,27 @@ def test_prophet_iteration_order():
     assert pushed == want
     for i, n in enumerate(sizes):
         assert (tensors[f"g{i}"] == i).all()          # one worker: the sum is itself
+
+
+def test_broadcast_is_push_pull_with_zeros():
+    """byteps/torch/__init__.py:264-272: non-root ranks push zeros, everyone
+    pulls the root's tensor; sources untouched."""
+    N, root = 3, 1
+    srv = FakeServer(N)
+    fe = ServerFrontend(srv)
+    workers = [Worker(r, fe, partition_bytes=64) for r in range(N)]
+    src = {r: np.full(50, 10 * r + 1, np.int32) for r in range(N)}
+    out = {}
+
+    def run(w):
+        w.init_tensor("p", src[w.rank], DType.INT32)
+        out[w.rank] = w.broadcast("p", src[w.rank], root)
+
+    ts = [threading.Thread(target=run, args=(w,)) for w in workers]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=30)
+    for r in range(N):
+        assert np.array_equal(out[r], src[root])
+        assert np.array_equal(src[r], np.full(50, 10 * r + 1, np.int32))
