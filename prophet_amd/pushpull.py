@@ -38,8 +38,10 @@ class ServerFrontend:
     """The handler in front of the GPU-resident server: decodes the request
     word, checks one key per request (server.cc:150-171) and forwards."""
 
-    def __init__(self, server):
+    def __init__(self, server, size: int | None = None):
         self.server = server
+        cfg = getattr(server, "cfg", None)
+        self.size = size if size is not None else (cfg.num_workers if cfg is not None else None)
 
     def push(self, cmd: int, key: int, worker: int, data, nbytes: int) -> None:
         req, dtype = depair_command(cmd)
@@ -118,11 +120,14 @@ class Worker:
         return ctx
 
     # ---------------------------------------------------------------- push_pull
-    def push_pull(self, name: str, tensor, output=None, order=None) -> None:
+    def push_pull(self, name: str, tensor, output=None, order=None,
+                  average: bool = False) -> None:
         """EnqueueTensor + the PUSH/PULL stages for one tensor: push every
         partition (in ``order`` — a list of partition indices — if given), then
         pull every partition into ``output`` (default: ``tensor`` itself, in
-        place, as byteps_push_pull does)."""
+        place, as byteps_push_pull does).  ``average``: divide the sum by the
+        number of workers afterwards, as byteps/torch's push_pull(average=True)
+        does (floating dtypes only)."""
         ctx = self.contexts[name]
         if not ctx.initialized:
             raise RuntimeError(f"{name}: init_tensor first")
@@ -138,6 +143,11 @@ class Worker:
             self.frontend.push(cmd, key, self.rank, _slice(tensor, off, ln), ln)
         for key, off, ln in ctx.parts:
             self.frontend.pull(key, _slice(out, off, ln), ln)
+        if average:
+            size = getattr(self.frontend, "size", None)
+            if not size:
+                raise ValueError("average: the frontend does not know the worker count")
+            _divide_(out, size)
 
     def broadcast(self, name: str, tensor, root_rank: int, output=None):
         """Broadcast as BytePS does it (byteps/torch/__init__.py:264-272: "push +
@@ -185,6 +195,19 @@ def _nbytes(x) -> int:
     if hasattr(x, "nbytes") and not hasattr(x, "data_ptr"):
         return int(x.nbytes)                               # numpy
     return int(x.numel() * x.element_size())               # torch
+
+
+def _divide_(x, size: int) -> None:
+    """In-place x /= size for a floating tensor or array."""
+    if hasattr(x, "data_ptr"):                             # torch
+        if not x.is_floating_point():
+            raise ValueError("average needs a floating dtype")
+        x.div_(size)
+        return
+    import numpy as np
+    if not np.issubdtype(x.dtype, np.floating):
+        raise ValueError("average needs a floating dtype")
+    x /= size
 
 
 def _zeros_like(x):

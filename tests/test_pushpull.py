@@ -137,3 +137,45 @@ def test_broadcast_is_push_pull_with_zeros():
     for r in range(N):
         assert np.array_equal(out[r], src[root])
         assert np.array_equal(src[r], np.full(50, 10 * r + 1, np.int32))
+
+
+def test_average_divides_by_worker_count():
+    """push_pull(average=True) as byteps/torch's: the sum / size; integer
+    tensors refuse (no true division in place)."""
+    class FloatFake(FakeServer):
+        def push(self, key, worker, data, dtype, nbytes=None):
+            with self.cv:
+                self.pending.setdefault(key, {})[worker] = data.view(np.float32).copy()
+                if len(self.pending[key]) == self.n:
+                    vals = list(self.pending.pop(key).values())
+                    self.store[key] = vals[-1] if key not in self.inited else sum(vals)
+                    self.inited.add(key)
+                    self.cv.notify_all()
+                elif key not in self.inited:
+                    self.cv.wait_for(lambda: key in self.inited)
+
+        def pull(self, key, out, nbytes=None):
+            with self.cv:
+                self.cv.wait_for(lambda: key not in self.pending)
+                out.view(np.float32)[:] = self.store[key]
+
+    N = 4
+    srv = FloatFake(N)
+    fe = ServerFrontend(srv, size=N)
+    workers = [Worker(r, fe, partition_bytes=64) for r in range(N)]
+    vals = {r: np.full(40, float(r + 1), np.float32) for r in range(N)}
+
+    def run(w):
+        w.init_tensor("g", vals[w.rank], DType.FLOAT32)
+        w.push_pull("g", vals[w.rank], average=True)
+
+    ts = [threading.Thread(target=run, args=(w,)) for w in workers]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=30)
+    for r in range(N):
+        assert np.array_equal(vals[r], np.full(40, 2.5, np.float32))
+    from prophet_amd.pushpull import _divide_
+    with pytest.raises(ValueError):
+        _divide_(np.zeros(3, np.int32), 2)
