@@ -78,6 +78,9 @@ class Worker:
             raise ValueError("partition bound must be positive")
         self.contexts: dict[str, Context] = {}
         self._declared: list[str] = []
+        self._pool = None
+        self._handles: dict[int, tuple] = {}
+        self._next_handle = 0
 
     # ------------------------------------------------------------ declare/init
     def declare(self, name: str) -> int:
@@ -148,6 +151,33 @@ class Worker:
             if not size:
                 raise ValueError("average: the frontend does not know the worker count")
             _divide_(out, size)
+
+    # byteps/torch/ops.py: push_pull_async -> handle, poll(handle),
+    # synchronize(handle).  Calls run in call order on the worker's own
+    # thread (BytePS's loops also take a worker's tensors one after another).
+    def push_pull_async(self, name: str, tensor, output=None, average: bool = False) -> int:
+        from concurrent.futures import ThreadPoolExecutor
+        if self._pool is None:
+            self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"bps{self.rank}")
+        out = tensor if output is None else output
+        fut = self._pool.submit(self.push_pull, name, tensor, out, None, average)
+        self._next_handle += 1
+        self._handles[self._next_handle] = (fut, out)
+        return self._next_handle
+
+    def poll(self, handle: int) -> bool:
+        return self._handles[handle][0].done()
+
+    def synchronize(self, handle: int):
+        """Wait for the push_pull and return its output (errors re-raised)."""
+        fut, out = self._handles.pop(handle)
+        fut.result()
+        return out
+
+    def close(self) -> None:
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
 
     def broadcast(self, name: str, tensor, root_rank: int, output=None):
         """Broadcast as BytePS does it (byteps/torch/__init__.py:264-272: "push +

@@ -179,3 +179,34 @@ def test_average_divides_by_worker_count():
     from prophet_amd.pushpull import _divide_
     with pytest.raises(ValueError):
         _divide_(np.zeros(3, np.int32), 2)
+
+
+def test_push_pull_async_handles():
+    """push_pull_async / poll / synchronize (byteps/torch/ops.py): several
+    tensors in flight per worker, results as the synchronous call's."""
+    N = 3
+    srv = FakeServer(N)
+    fe = ServerFrontend(srv, size=N)
+    workers = [Worker(r, fe, partition_bytes=64) for r in range(N)]
+    names = [f"t{i}" for i in range(4)]
+    vals = {(r, n): np.arange(30, dtype=np.int32) * (r + 1) + i
+            for r in range(N) for i, n in enumerate(names)}
+
+    def run(w):
+        for n in names:
+            w.init_tensor(n, vals[(w.rank, n)], DType.INT32)
+        hs = [w.push_pull_async(n, vals[(w.rank, n)]) for n in names]
+        assert all(isinstance(w.poll(h), bool) for h in hs)
+        for h in hs:
+            w.synchronize(h)
+        w.close()
+
+    ts = [threading.Thread(target=run, args=(w,)) for w in workers]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=30)
+    for i, n in enumerate(names):
+        want = sum(np.arange(30, dtype=np.int32) * (r + 1) + i for r in range(N))
+        for r in range(N):
+            assert np.array_equal(vals[(r, n)], want)
