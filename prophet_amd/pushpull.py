@@ -16,6 +16,9 @@ byteps/server/server.cc, with an in-process transport:
   its offset of the output — optionally in the order the Prophet PUSH
   scheduler releases partitions (scheduled_queue.cc:217-296,
   ``prophet_amd.prophet.ProphetPushQueue``);
+* ``push_pull(average=True)``, ``push_pull_async`` / ``poll`` /
+  ``synchronize`` and ``broadcast`` (push_pull with zeros on the non-root
+  ranks) — the byteps/torch API shapes (ops.py, __init__.py:244-272);
 * the server front end decodes the request word like ``BytePSHandler``
   (``DepairDataHandleType``, server.h:77-88, of ``GetCommandType``'s Cantor
   pairing, common.cc:99-102) and hands the bytes to ``PSServer``.
