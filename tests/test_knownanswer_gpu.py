@@ -41,8 +41,9 @@ def _threshold(size, dtype):
     return None                          # the reference stops checking (`break`)
 
 
+@pytest.mark.parametrize("mode", ["sync", "async"])
 @pytest.mark.parametrize("size", [2, 3, 8, 14])
-def test_byteps_push_pull_inplace_known_answer(size):
+def test_byteps_push_pull_inplace_known_answer(size, mode):
     from prophet_amd.pushpull import ServerFrontend, Worker
     from prophet_amd.server import PSServer
     srv = PSServer(size, engine_lanes=4)
@@ -64,8 +65,14 @@ def test_byteps_push_pull_inplace_known_answer(size):
                 w.declare(name)
             for name, dtype, _ in cases:
                 w.init_tensor(name, tensors[(w.rank, name)], DTYPES[dtype][0])
-            for name, dtype, _ in cases:
-                w.push_pull(name, tensors[(w.rank, name)])
+            if mode == "sync":
+                for name, dtype, _ in cases:
+                    w.push_pull(name, tensors[(w.rank, name)])
+            else:                   # push_pull_async + synchronize (byteps/torch/ops.py)
+                hs = [w.push_pull_async(name, tensors[(w.rank, name)]) for name, _, _ in cases]
+                for h in hs:
+                    w.synchronize(h)
+                w.close()
         except Exception as e:  # surfaced below
             errors.append(repr(e))
 
