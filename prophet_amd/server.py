@@ -76,6 +76,14 @@ def _buf(x):
         return x.ctypes.data, x.nbytes, HOST
     if hasattr(x, "data_ptr"):
         loc = DEVICE if x.device.type == "cuda" else HOST
+        if loc == DEVICE:
+            # The server copies on streams of its own: whatever torch queued
+            # for this tensor on the calling thread's current stream (the
+            # kernel that produced a push, a fill of a pull's destination)
+            # must be done first.  Work on other torch streams is the
+            # caller's to order.
+            import torch
+            torch.cuda.current_stream(x.device).synchronize()
         return int(x.data_ptr()), x.numel() * x.element_size(), loc
     raise TypeError(f"unsupported buffer {type(x)!r}")
 
