@@ -599,6 +599,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     # probe: one live iteration must complete before anything is timed (a
     # profiler that serialises dispatches would strand the consumer; it then
     # gives up after its 1-s timeout and status() raises, ending this leg)
+    torch.cuda.synchronize()        # the inputs (torch's stream) before any consumer
     live(0)
     torch.cuda.synchronize()
     queues[0].status(live_s)

@@ -183,7 +183,9 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * library's consumer stream for the device — an all-CU-masked stream, which
  * the runtime gives a hardware queue of its own (byteps_reduce_blockq_stream).
  * Launching on that stream costs nothing extra and orders launches and status
- * calls there; launching on any other stream forks onto it and joins back
+ * calls there (work on other streams that reads the outputs must then wait for
+ * it, e.g. on an event recorded there); launching on any other stream forks
+ * onto it and joins back
  * (two events — ~0.14 ms per iteration at config 3, so launch on the consumer
  * stream when iterations run back to back).  A launch inside a hipGraph
  * capture stays on the capturing stream (pre-released by rule).  Releases on
