@@ -216,6 +216,10 @@ class PushLoop:
         self._h = h
 
     def begin(self, consumer_stream=None) -> None:
+        """Reset the scheduler and launch the iteration's consumer on
+        ``consumer_stream`` (None: the library's consumer stream — then
+        ``end`` orders the current torch stream after the consumer)."""
+        self._on_library_stream = consumer_stream is None
         _ck(self._L.byteps_prophet_loop_begin(self._h, _stream_ptr(consumer_stream)))
 
     def push(self, task: PushTask, index: int) -> None:
@@ -224,7 +228,13 @@ class PushLoop:
         _ck(self._L.byteps_prophet_loop_push(self._h, ctypes.byref(c)))
 
     def end(self, timeout_s: float = 10.0) -> None:
+        """Wait until every block has been released; with the consumer on the
+        library's stream, the current torch stream then waits for it (on the
+        device), so later torch work sees the folded outputs."""
         _ck(self._L.byteps_prophet_loop_end(self._h, float(timeout_s)))
+        if getattr(self, "_on_library_stream", False):
+            import torch
+            torch.cuda.current_stream().wait_stream(self.blockq.stream())
 
     def close(self) -> None:
         h = getattr(self, "_h", None)
