@@ -133,8 +133,9 @@ def test_live_release_after_dma(red, dev, occ):
     tab = Table(dev, dt, blocks)
     q = red.make_blockq(tab.blocks, dt)
     q.config(wg_per_cu=occ, timeout_s=5.0)
-    # the consumer on a high-priority stream: its own hardware queue, so the
-    # copy stream's DMA and releases never queue behind it (include/bpsr/reduce.h)
+    # launched on a caller's stream: the library forks the consumer onto its
+    # own consumer stream (a hardware queue of its own, include/bpsr/reduce.h),
+    # so the copy stream's DMA and releases never queue behind it
     comp, copy = torch.cuda.Stream(priority=-100), torch.cuda.Stream()
     for it in range(2):
         pushes, wants = tab.host_inputs(1000 * it + 3)
@@ -268,7 +269,7 @@ def test_bad_tables_rejected(red, dev):
 @SHAPES
 def test_epochs_back_to_back_iterations(red, dev, shape):
     """Epoch-numbered releases: three iterations enqueued without a host
-    sync — consumer k on a high-priority stream, its releases on a side stream,
+    sync — consumer k launched from a caller's stream, its releases on a side stream,
     the next iteration's launch queued right behind — every launch folds its
     own iteration's data (each iteration rewrites the inputs by a device copy
     ordered after the previous launch and before its releases)."""

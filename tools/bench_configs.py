@@ -230,11 +230,10 @@ def cfg3(red, dev, N=8, sets=3):
         bq_variants.append((f"prophet_blockq_{nm}_hipgraph", blockq_graph(occ)))
 
     rel_stream = torch.cuda.Stream()
-    # The live consumer runs on a high-priority stream: a hardware queue of its
-    # own, so the releases on rel_stream never sit behind it in a shared queue
-    # (include/bpsr/reduce.h; under rocprofv3 with both at normal priority the
-    # first live launch of each queue waited out its 5-s timeout).
-    live_stream = bqs[0][0].stream()     # the library's consumer stream
+    # The live consumer runs on the library's consumer stream: a hardware queue
+    # of its own, so the releases on rel_stream never sit behind it in a shared
+    # queue (include/bpsr/reduce.h; stream priority alone did not guarantee it).
+    live_stream = bqs[0][0].stream()
     nblk = len(by_block)
 
     def blockq_live(i, occ=0):
