@@ -238,6 +238,15 @@ int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s) {
     ok = l->done_cv.wait_for(lk, std::chrono::duration<double>(timeout_s), pred);
   else
     l->done_cv.wait(lk, pred);
+  if (ok) {
+    // The last block can be released while its drainer is still reporting
+    // the group's partitions finished (outside mu): let that drain return
+    // before the next begin() resets the scheduler, so no credit of this
+    // iteration lands in the next one.  drain_mu is taken before mu.
+    lk.unlock();
+    { std::lock_guard<std::mutex> dg(l->drain_mu); }
+    lk.lock();
+  }
   l->active = false;
   if (l->err) return l->err;
   if (!ok)

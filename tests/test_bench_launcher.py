@@ -50,6 +50,31 @@ def test_launcher_one_line_n_ranks(n):
         assert sc["scatter"]["scatter_fold_ms"] > 0
 
 
+def test_torchrun_launch_one_line():
+    """The driver's own multi-GPU form: ``python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus N`` (ranks from the environment, no self-launch)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "2",
+           "--warmup", "1", "--workers", "3", "--bucket-mib", "0.0625", "--sets", "2",
+           "--no-cpu-baseline", "--scaling-elems", "10007"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["config"]["devices"]) == 2
+    assert line["scaling_cfg4"]["scatter"]["exact_vs_torch_fold"] is True
+
+
 def test_launcher_failing_rank_fails_the_run():
     env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
