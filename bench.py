@@ -26,6 +26,11 @@ owned slice (max over ranks), the G=1 time of the whole set measured in the
 same run, strong-scaling speedup/efficiency, and, for N > 1, the RCCL P2P
 scatter from a landing GPU plus the all-gather return leg.
 
+``e2e_cfg5`` (every N, GPU runs): BASELINE config 5 from host memory — 16
+workers' 256 MiB bf16 pushes in pinned host buffers, each GPU streaming its
+key-space slice H2D -> fold -> D2H over its own PCIe link: the PCIe-inclusive
+node rate the north star asks to record (never ``value``).
+
 Prints ONE JSON line (rank 0).  Metric: GiB/s = N_workers * B / t / 2^30 per
 step, summed over GPUs.  ``roofline`` prices the dominant kernel at
 (N_workers + 1) * B algorithmic HBM bytes per launch against 8.0 TB/s;
@@ -90,6 +95,10 @@ def parse(argv=None):
                    help="N = 1: skip the fp16 run of the headline workload")
     p.add_argument("--no-cfg3", action="store_true",
                    help="N = 1: skip the config-3 (ResNet-50 fp16 Prophet blocks) object")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="skip the config-5 host-resident (PCIe-inclusive) object")
+    p.add_argument("--e2e-bucket-mib", type=int, default=256,
+                   help="config-5 object: bucket MiB per worker (16 workers; BASELINE: 256)")
     p.add_argument("--no-scatter", action="store_true",
                    help="N > 1: skip the RCCL scatter + all-gather leg of `scaling`")
     p.add_argument("--scaling-elems", type=int, default=0,
@@ -536,6 +545,72 @@ def fp16_leg(dev, red, N: int, B: int, steps: int, sets: int = 3) -> dict:
 
 
 # --------------------------------------------------------------------------
+# config 5: host-resident pushes, PCIe-inclusive, sharded over the GPUs
+
+
+def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int = 256 << 20,
+            reps: int = 3) -> dict:
+    """BASELINE config 5 end to end, key-space sharded: 16 workers' 256 MiB
+    bf16 pushes (4 GiB) start in pinned host memory, as ps-lite receive
+    buffers would (server.cc:174); each GPU streams ITS slice of every push
+    (owner_ranges, core_loops.cc:208-211) host -> HBM -> fold -> host through
+    ``StreamingReducer`` (H2D, fold and D2H on three streams; ``reduce_from_host``
+    with the aggregate pulled back), over its own PCIe link, no collective.
+    Node rate = all pushed bytes / (max over ranks of the blocking call).
+    PCIe-inclusive: never ``value``.  Exactness: strided windows of the pulled
+    slice against torch's own bf16 left fold (fp32 add, RNE to bf16 per add)
+    of the same windows on the device."""
+    import torch
+    import torch.distributed as dist
+    from prophet_amd.dtypes import DType
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.shard import owner_ranges
+    from prophet_amd.stream import StreamingReducer
+    E = bucket_bytes // 2
+    lo, hi = owner_ranges(E, world)[rank]
+    m = hi - lo
+    nb = 2 * m
+    gen = torch.Generator(device=dev)
+    pushes = []
+    for k in range(n_workers):
+        gen.manual_seed(9000 + 16 * rank + k)
+        h = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+        h.view(torch.bfloat16).copy_(torch.randn(m, device=dev, generator=gen).bfloat16())
+        pushes.append(h)
+    out = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    sr = StreamingReducer(n_workers, device=dev, reducer=GpuReducer(device=dev.index))
+    multi = world > 1 and dist.is_initialized()
+    torch.cuda.synchronize()
+    sr.reduce(pushes, out, nb, DType.BFLOAT16)          # warm-up (pages, streams)
+    times = []
+    for _ in range(reps):
+        if multi:
+            dist.barrier()
+        t0 = time.perf_counter()
+        sr.reduce(pushes, out, nb, DType.BFLOAT16)
+        times.append(time.perf_counter() - t0)
+    t = _max_over_ranks(dist, dev, [statistics.median(times)])[0]
+    ok = True
+    win = 1 << 16
+    for w0 in range(0, m, max(win, m // 8)):
+        w1 = min(m, w0 + win)
+        ref = pushes[0].view(torch.bfloat16)[w0:w1].to(dev)
+        for h in pushes[1:]:
+            ref.add_(h.view(torch.bfloat16)[w0:w1].to(dev))
+        ok = ok and bool(torch.equal(ref.view(torch.int16).cpu(),
+                                     out.view(torch.bfloat16)[w0:w1].view(torch.int16)))
+    ok = _all_true(dist, dev, ok)
+    total = n_workers * bucket_bytes
+    return {"workload": (f"config 5: {n_workers}-way bf16, {n_workers} x {bucket_bytes >> 20} MiB "
+                         f"pinned host pushes ({total / GIB:.0f} GiB), key-space sharded over "
+                         f"{world} GPU(s), streamed H2D + fold + D2H, aggregate back in host memory"),
+            "node_e2e_GiBps": round(total / t / GIB, 1),
+            "per_gpu_e2e_GiBps": round(n_workers * nb / t / GIB, 1),
+            "ms": round(t * 1e3, 2), "reps": reps, "pcie_inclusive": True,
+            "exact_vs_torch_fold_windows": ok}
+
+
+# --------------------------------------------------------------------------
 # config 3: ResNet-50 fp16 Prophet blocks through the block queue
 
 
@@ -885,6 +960,12 @@ def main(argv=None):
                         fold=None if cuda else _torch_fold)
                 except Exception as e:  # report, never hide
                     line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
+        if cuda and not args.no_e2e:
+            try:
+                line["e2e_cfg5"] = e2e_leg(dev, world, rank,
+                                           bucket_bytes=args.e2e_bucket_mib << 20)
+            except Exception as e:  # report, never hide
+                line["e2e_cfg5"] = {"error": repr(e)}
 
     if world == 1:
         extra_legs()

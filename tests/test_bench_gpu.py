@@ -19,12 +19,15 @@ def test_bench_two_ranks_rehearsed_on_one_gpu():
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rehearse-one-gpu",
            "--steps", "5", "--warmup", "2", "--bucket-mib", "16", "--no-cpu-baseline",
-           "--scaling-elems", "4000037"]
+           "--scaling-elems", "4000037", "--e2e-bucket-mib", "16"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
+    e2e = line["e2e_cfg5"]
+    assert "error" not in e2e, e2e
+    assert e2e["exact_vs_torch_fold_windows"] is True and e2e["node_e2e_GiBps"] > 0
     assert line["n_gpus"] == 2 and len(line["config"]["devices"]) == 2
     assert "rehearsal" in line["device"]
     assert line["check_vs_torch_fold"] is True
@@ -43,7 +46,8 @@ def test_bench_one_gpu_line_has_every_object():
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
-           "--bucket-mib", "16", "--no-cpu-baseline", "--scaling-elems", "4000037"]
+           "--bucket-mib", "16", "--no-cpu-baseline", "--scaling-elems", "4000037",
+           "--e2e-bucket-mib", "16"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -60,3 +64,6 @@ def test_bench_one_gpu_line_has_every_object():
     assert c3["exact_vs_torch_fold"] is True
     for k in ("live", "pre_released"):
         assert 0 < c3[k]["frac_of_roofline"] < 1
+    e2e = line["e2e_cfg5"]
+    assert "error" not in e2e, e2e
+    assert e2e["exact_vs_torch_fold_windows"] is True and e2e["pcie_inclusive"] is True
