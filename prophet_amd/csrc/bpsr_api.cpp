@@ -87,7 +87,8 @@ static std::mutex g_tuning_mu;
 static Tuning& tuning_storage() {
   static Tuning tu = [] {
     // tools/sweep.py, tools/occ_sweep.py, tools/cfg3_probe.py (profiles/)
-    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1, 4, 2};
+    Tuning t{2, 1, 1 << 20, 1, 2, 0, 4096, 4096, 1, 4, 2, kWtMaxBytes};
+    if (const char* v = getenv("BPSR_WT_MAX_MIB")) t.wt_max_bytes = (uint64_t)atoll(v) << 20;
     if (const char* v = getenv("BPSR_COPY_OCC")) t.copy_occ = atoi(v);
     if (const char* v = getenv("BPSR_COPY_VPT")) t.copy_vpt = atoi(v);
     if (t.copy_occ < 0 || t.copy_occ > 8) t.copy_occ = 4;
@@ -793,7 +794,7 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(own, q->fork_ev, 0);
   }
-  if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, tu.nt != 0, lds, gated, q->dtype, q->mode, ls);
+  if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16), lds, gated, q->dtype, q->mode, ls);
   if (fork && e == hipSuccess) e = hipEventRecord(q->join_ev, own);
   if (fork && e == hipSuccess) e = hipStreamWaitEvent(s, q->join_ev, 0);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");

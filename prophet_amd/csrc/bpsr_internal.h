@@ -124,6 +124,7 @@ struct Tuning {
   int auto_n;    // residency/tile size by source count (bpsr_api.cpp tuning_for_n)
   int copy_occ;  // workgroups per CU of long copies (0 = hardware)
   int copy_vpt;  // copy tile: kBlock * copy_vpt 16-B vectors
+  uint64_t wt_max_bytes;  // nt folds below this many bytes per source store write-through
 };
 
 // Residency cap through the dynamic LDS request: a CU has 160 KiB of LDS, so
@@ -193,7 +194,7 @@ inline int fold_grid(const FoldGeom& g, const Tuning& tu, int vpt) {
   hipError_t launch_fold_##NAME(const FoldArgs& a, const Tuning& tu, hipStream_t s);      \
   hipError_t launch_batched_##NAME(const BatchLaunch& L, int vpt, const Tuning& tu,      \
                                    hipStream_t s);                                        \
-  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
+  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, int pol, size_t lds,    \
                                   bool gated, hipStream_t s);
 BPSR_DECLARE_LAUNCHERS(f32)
 BPSR_DECLARE_LAUNCHERS(f64)
@@ -209,7 +210,7 @@ hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
                        hipStream_t s);
 hipError_t launch_batched(const BatchLaunch& L, int vpt, int dtype, int mode, const Tuning& tu,
                           hipStream_t s);
-hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, bool gated,
+hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bool gated,
                          int dtype, int mode, hipStream_t s);
 hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s);
@@ -224,6 +225,17 @@ inline int fold_vpt(uint64_t nvec, int vpt) {
   // (profiles/r01_thr_fold.jsonl).
   if (vpt == 2 && tiles(4) >= kMinTiles && tiles(4) < 2 * kMinTiles) vpt = 4;
   return vpt;
+}
+// Cache policy of a fold's buffer instructions (the kernels' NT template
+// argument): plain; nt loads and stores; or nt loads with write-through (sc1)
+// stores.  Write-through leaves no dirty output lines in the XCDs' L2s for the
+// end-of-kernel release to flush, which mid-size launches feel as a fixed cost
+// (DESIGN.md §4.1); long sweeps stream faster with nt stores.
+constexpr int kPolPlain = 0, kPolNt = 1, kPolWt = 2;
+constexpr uint64_t kWtMaxBytes = 96ull << 20;  // per source (Tuning default)
+inline int cache_pol(const Tuning& tu, uint64_t bytes_per_src) {
+  if (!tu.nt) return kPolPlain;
+  return bytes_per_src < tu.wt_max_bytes ? kPolWt : kPolNt;
 }
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s);

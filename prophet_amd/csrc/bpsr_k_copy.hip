@@ -112,22 +112,22 @@ hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count
   return hipGetLastError();
 }
 
-hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, bool nt, size_t lds, bool g, int dtype,
+hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bool g, int dtype,
                          int mode, hipStream_t s) {
   const bool acc = mode == kModeAccumF32;
   switch (dtype) {
-    case kFloat32: return launch_blockq_f32(Q, vpt, nt, lds, g, s);
-    case kFloat64: return launch_blockq_f64(Q, vpt, nt, lds, g, s);
+    case kFloat32: return launch_blockq_f32(Q, vpt, pol, lds, g, s);
+    case kFloat64: return launch_blockq_f64(Q, vpt, pol, lds, g, s);
     case kFloat16:
-      return acc ? launch_blockq_f16acc(Q, vpt, nt, lds, g, s)
-                 : launch_blockq_f16(Q, vpt, nt, lds, g, s);
+      return acc ? launch_blockq_f16acc(Q, vpt, pol, lds, g, s)
+                 : launch_blockq_f16(Q, vpt, pol, lds, g, s);
     case kBFloat16:
-      return acc ? launch_blockq_bf16acc(Q, vpt, nt, lds, g, s)
-                 : launch_blockq_bf16(Q, vpt, nt, lds, g, s);
+      return acc ? launch_blockq_bf16acc(Q, vpt, pol, lds, g, s)
+                 : launch_blockq_bf16(Q, vpt, pol, lds, g, s);
     case kUInt8:
-    case kInt8: return launch_blockq_i8(Q, vpt, nt, lds, g, s);
-    case kInt32: return launch_blockq_i32(Q, vpt, nt, lds, g, s);
-    case kInt64: return launch_blockq_i64(Q, vpt, nt, lds, g, s);
+    case kInt8: return launch_blockq_i8(Q, vpt, pol, lds, g, s);
+    case kInt32: return launch_blockq_i32(Q, vpt, pol, lds, g, s);
+    case kInt64: return launch_blockq_i64(Q, vpt, pol, lds, g, s);
     default: return hipErrorInvalidValue;
   }
 }

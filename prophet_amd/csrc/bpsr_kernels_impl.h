@@ -102,7 +102,7 @@ __device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* s
 // NS > 0: exactly NS sources; NS < 0: at most -NS (<= 8) sources, n at run
 // time, one load group with compile-time indices (so `srcs` may be a register
 // array); NS == 0: any n.  `xsrcs` (memory) serves the exact NaN replay.
-template <class Op, int VPT, bool NT, int NS, bool GUARD>
+template <class Op, int VPT, int NT, int NS, bool GUARD>
 __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
                                                const unsigned char* const* xsrcs, int n,
                                                unsigned char* dst, uint64_t vec_off,
@@ -125,7 +125,7 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
         const unsigned char* base = srcs[k0 + g] + off0;
 #pragma unroll
         for (int j = 0; j < VPT; ++j)
-          x[g][j] = valid[j] ? ld16<NT>(base + j * kStep) : vec16{{0, 0, 0, 0}};
+          x[g][j] = valid[j] ? ld16<(NT != 0)>(base + j * kStep) : vec16{{0, 0, 0, 0}};
       }
     }
 #pragma unroll
@@ -153,9 +153,9 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
     vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (valid[j] && Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, NT>(xsrcs, ns, off0 + j * kStep);
+        out = fold_vector_exact<Op, (NT != 0)>(xsrcs, ns, off0 + j * kStep);
     }
-    if (valid[j]) st16<NT>(dst + off0 + j * kStep, out);
+    if (valid[j]) st16<(NT != 0)>(dst + off0 + j * kStep, out);
   }
 }
 
@@ -170,12 +170,13 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <class Op, int VPT, bool NT, int NS, class Mid = NoMid>
+template <class Op, int VPT, int NT, int NS, class Mid = NoMid>
 __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs,
                                                    const unsigned char* const* xsrcs, int n,
                                                    unsigned char* dst, uint64_t byte0, int lane,
                                                    const Mid& mid = Mid()) {
-  constexpr int kAux = NT ? 2 : 0;               // 2 = nt
+  constexpr int kAux = NT ? 2 : 0;               // loads: 2 = nt
+  constexpr int kStAux = NT == kPolWt ? 16 : kAux;  // stores: 16 = sc1 (write-through)
   constexpr int kTileBytes = kBlock * VPT * 16;
   constexpr int NSA = NS < 0 ? -NS : NS;
   constexpr int G = NSA > 0 ? cmin(NSA, 32 / VPT) : cmin(8, 32 / VPT);
@@ -227,13 +228,13 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
     vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, NT>(xsrcs, ns, byte0 + voff + j * kBlock * 16);
+        out = fold_vector_exact<Op, (NT != 0)>(xsrcs, ns, byte0 + voff + j * kBlock * 16);
     }
-    __builtin_amdgcn_raw_buffer_store_b128(bitcast<u4>(out), rd, voff + j * kBlock * 16, 0, kAux);
+    __builtin_amdgcn_raw_buffer_store_b128(bitcast<u4>(out), rd, voff + j * kBlock * 16, 0, kStAux);
   }
 }
 
-template <class Op, int VPT, bool NT, int NS>
+template <class Op, int VPT, int NT, int NS>
 __device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int n,
                                           unsigned char* dst, uint64_t vec_off, uint64_t v0,
                                           uint64_t nvec, int lane) {
@@ -308,7 +309,7 @@ __device__ __forceinline__ void pin_args(const FoldArgs& a) {
   }
 }
 
-template <class Op, int VPT, bool NT, int NS>
+template <class Op, int VPT, int NT, int NS>
 __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
   pin_args<NS>(a);
   // decided at entry, while the arguments are in SGPRs (no reload after the loop)
@@ -346,7 +347,7 @@ struct RecRegs {
   const unsigned char* p[8];
 };
 
-template <class Op, int VPT, bool NT, class Mid = NoMid>
+template <class Op, int VPT, int NT, class Mid = NoMid>
 __device__ __forceinline__ void run_record(const RecRegs& r, const unsigned char* const* msrcs,
                                            const BatchEntry* entries, const Mid& mid = Mid()) {
   if (r.kind == kTileElem) {
@@ -417,7 +418,7 @@ __device__ __forceinline__ RecRegs regs_from_words(const uint32_t* w) {
 }
 
 // Batched: workgroup b runs record b of the launch.
-template <class Op, int VPT, bool NT>
+template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
   const unsigned char* rec = L.recs + (uint64_t)blockIdx.x * L.rec_stride;
   run_record<Op, VPT, NT>(load_record(rec),
@@ -451,7 +452,7 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <class Op, int VPT, bool NT>
+template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
   // record slots alternate: iteration i reads slot i&1 and stages the next
   // record into the other one, so no wave overwrites a record still being read
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
 // before its loads; one whose tile is released reads data no workgroup of
 // this launch has touched since the launch's own acquire (blocks do not share
 // lines), so it needs none.
-template <class Op, int VPT, bool NT>
+template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
   const uint32_t t = blockIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
 
 // ------------------------------------------------------------- launchers ----
 
-template <class Op, int VPT, bool NT, int NS>
+template <class Op, int VPT, int NT, int NS>
 static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
   static KernelAttr attr;
   const hipError_t lds_ok =
@@ -583,7 +584,7 @@ static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_
   return hipGetLastError();
 }
 
-template <class Op, int VPT, bool NT>
+template <class Op, int VPT, int NT>
 static hipError_t launch_fold_vpt(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
   switch (a.n) {  // compile-time source counts for the common worker counts
     case 2: return launch_fold_ns<Op, VPT, NT, 2>(a, tu, s);
@@ -593,38 +594,48 @@ static hipError_t launch_fold_vpt(const FoldArgs& a, const Tuning& tu, hipStream
   }
 }
 
+template <class Op, int NT>
+static hipError_t launch_fold_pol(const FoldArgs& a, int vpt, const Tuning& tu, hipStream_t s) {
+  switch (vpt) {
+    case 1: return launch_fold_vpt<Op, 1, NT>(a, tu, s);
+    case 4: return launch_fold_vpt<Op, 4, NT>(a, tu, s);
+    default: return launch_fold_vpt<Op, 2, NT>(a, tu, s);
+  }
+}
+
 template <class Op>
 static hipError_t launch_fold_op(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
   const int vpt = fold_vpt(a.g.nvec, tu.vpt);
-  if (tu.nt) {
-    switch (vpt) {
-      case 1: return launch_fold_vpt<Op, 1, true>(a, tu, s);
-      case 4: return launch_fold_vpt<Op, 4, true>(a, tu, s);
-      default: return launch_fold_vpt<Op, 2, true>(a, tu, s);
-    }
-  }
-  switch (vpt) {
-    case 1: return launch_fold_vpt<Op, 1, false>(a, tu, s);
-    case 4: return launch_fold_vpt<Op, 4, false>(a, tu, s);
-    default: return launch_fold_vpt<Op, 2, false>(a, tu, s);
+  switch (cache_pol(tu, a.g.nvec * 16)) {
+    case kPolNt: return launch_fold_pol<Op, kPolNt>(a, vpt, tu, s);
+    case kPolWt: return launch_fold_pol<Op, kPolWt>(a, vpt, tu, s);
+    default: return launch_fold_pol<Op, kPolPlain>(a, vpt, tu, s);
   }
 }
 
 template <class Op, int VPT>
 static hipError_t launch_batched_vpt(const BatchLaunch& L, const Tuning& tu, hipStream_t s) {
-  static KernelAttr attr_nt, attr_t;
-  const hipError_t ok_nt =
-      allow_lds(attr_nt, reinterpret_cast<const void*>(&batched_kernel<Op, VPT, true>));
-  const hipError_t ok_t =
-      allow_lds(attr_t, reinterpret_cast<const void*>(&batched_kernel<Op, VPT, false>));
-  if (ok_nt != hipSuccess) return ok_nt;
-  if (ok_t != hipSuccess) return ok_t;
+  static KernelAttr attr[3];
+  const void* k[3] = {reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolPlain>),
+                      reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolNt>),
+                      reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolWt>)};
+  for (int i = 0; i < 3; ++i) {
+    const hipError_t ok = allow_lds(attr[i], k[i]);
+    if (ok != hipSuccess) return ok;
+  }
   if (L.tiles == 0) return hipSuccess;
   const size_t lds = occ_lds_bytes(launch_occ(tu, L.tiles, true));
-  if (tu.nt)
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, true>), dim3(L.tiles), dim3(kBlock), lds, s, L);
-  else
-    hipLaunchKernelGGL((batched_kernel<Op, VPT, false>), dim3(L.tiles), dim3(kBlock), lds, s, L);
+  switch (cache_pol(tu, (uint64_t)L.tiles * VPT * kBlock * 16)) {
+    case kPolNt:
+      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolNt>), dim3(L.tiles), dim3(kBlock), lds, s, L);
+      break;
+    case kPolWt:
+      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolWt>), dim3(L.tiles), dim3(kBlock), lds, s, L);
+      break;
+    default:
+      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolPlain>), dim3(L.tiles), dim3(kBlock), lds, s,
+                         L);
+  }
   return hipGetLastError();
 }
 
@@ -638,7 +649,7 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
   }
 }
 
-template <class Op, int VPT, bool NT>
+template <class Op, int VPT, int NT>
 static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated, hipStream_t s) {
   if (gated) {
     static KernelAttr attr_g;
@@ -658,17 +669,24 @@ static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated,
   return hipGetLastError();
 }
 
+template <class Op, int VPT>
+static hipError_t launch_blockq_vpt(const BlockqLaunch& Q, int pol, size_t lds, bool gated,
+                                    hipStream_t s) {
+  switch (pol) {
+    case kPolNt: return launch_blockq_k<Op, VPT, kPolNt>(Q, lds, gated, s);
+    case kPolWt: return launch_blockq_k<Op, VPT, kPolWt>(Q, lds, gated, s);
+    default: return launch_blockq_k<Op, VPT, kPolPlain>(Q, lds, gated, s);
+  }
+}
+
 template <class Op>
-static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,
+static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, int pol, size_t lds,
                                    bool gated, hipStream_t s) {
   if (Q.grid == 0) return hipSuccess;
-  switch (vpt * 2 + (nt ? 1 : 0)) {
-    case 2: return launch_blockq_k<Op, 1, false>(Q, lds, gated, s);
-    case 3: return launch_blockq_k<Op, 1, true>(Q, lds, gated, s);
-    case 4: return launch_blockq_k<Op, 2, false>(Q, lds, gated, s);
-    case 8: return launch_blockq_k<Op, 4, false>(Q, lds, gated, s);
-    case 9: return launch_blockq_k<Op, 4, true>(Q, lds, gated, s);
-    default: return launch_blockq_k<Op, 2, true>(Q, lds, gated, s);
+  switch (vpt) {
+    case 1: return launch_blockq_vpt<Op, 1>(Q, pol, lds, gated, s);
+    case 4: return launch_blockq_vpt<Op, 4>(Q, pol, lds, gated, s);
+    default: return launch_blockq_vpt<Op, 2>(Q, pol, lds, gated, s);
   }
 }
 
@@ -684,8 +702,8 @@ static hipError_t launch_blockq_op(const BlockqLaunch& Q, int vpt, bool nt, size
                                    hipStream_t s) {                                       \
     return launch_batched_op<OP>(L, vpt, tu, s);                                          \
   }                                                                                       \
-  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, bool nt, size_t lds,    \
+  hipError_t launch_blockq_##NAME(const BlockqLaunch& Q, int vpt, int pol, size_t lds,    \
                                   bool gated, hipStream_t s) {                            \
-    return launch_blockq_op<OP>(Q, vpt, nt, lds, gated, s);                               \
+    return launch_blockq_op<OP>(Q, vpt, pol, lds, gated, s);                               \
   }                                                                                       \
   }

@@ -180,6 +180,8 @@ int main(int argc, char** argv) {
       {"n8_v2_wg1cu_l3s2", L<3, 2, 2, false, 8, false, 160>},
       {"n8_v2_wg1cu_l2s3", L<2, 3, 2, false, 8, false, 160>},
       {"n8_v2_wg1cu_l2s0", L<2, 0, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l2s17", L<2, 17, 2, false, 8, false, 160>},
+      {"n8_v2_wg1cu_l2s19", L<2, 19, 2, false, 8, false, 160>},
   };
   std::vector<V> vs = {
       {"n8", L<2, 2, 4, false, 8>},
