@@ -77,7 +77,7 @@ for s in $STEPS; do
     cfg1trace) run cfg1_trace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
              -d "$OUT/cfg1trace" -o cfg1 -- ./tools/cfg1_native 4 6 ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 ;;
+             -d "$OUT/prof" -o bench -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 --no-e2e ;;
     skew)  for k in 4096 8192 16384 24576 49152 81920 1064960; do
              run skew_$k 200 python bench.py --steps 100 --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 --skew $k || exit 1
            done

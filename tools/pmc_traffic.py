@@ -24,7 +24,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL_KEY = "fold_kernel"
+# the headline kernel only: other fold instantiations in the same run (the
+# bench line's fp16, config-3/4/5 objects, when not disabled) must not enter
+# the median
+KERNEL_KEY = "fold_kernel<bpsr::OpF32, 2, 1, 8>"
 
 
 def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[float], dict]:
@@ -40,6 +43,13 @@ def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[flo
             bench_line = json.loads(line)
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 pass {counter} failed rc={r.returncode}\n{r.stderr[-3000:]}")
+    with open(os.path.join(d, "bench_line.json"), "w") as fh:
+        json.dump(bench_line, fh)
+    return collect(counter, d), bench_line
+
+
+def collect(counter: str, d: str) -> list[float]:
+    """Per-dispatch counter sums of the headline kernel from a pass's CSVs."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -53,7 +63,7 @@ def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[flo
                     continue
                 key = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
-    return list(vals.values()), bench_line
+    return list(vals.values())
 
 
 def main():
@@ -62,13 +72,24 @@ def main():
     p.add_argument("--commit", action="store_true")
     p.add_argument("--session", default=os.environ.get("BPSR_SESSION", ""),
                    help="session tag recorded with the numbers (bench line traffic_source)")
+    p.add_argument("--reaggregate", action="store_true",
+                   help="re-read the passes already under --out (no profiling run)")
     p.add_argument("bench_args", nargs="*",
                    default=["--steps", "12", "--warmup", "2", "--no-cpu-baseline",
-                            "--no-scaling", "--no-cfg3", "--no-fp16"])
+                            "--no-scaling", "--no-cfg3", "--no-fp16", "--no-e2e"])
     a = p.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    fetch, bl = run_pass("FETCH_SIZE", a.out, a.bench_args)
-    write, _ = run_pass("WRITE_SIZE", a.out, a.bench_args)
+    if a.reaggregate:
+        fetch = collect("FETCH_SIZE", os.path.join(a.out, "fetch_size"))
+        write = collect("WRITE_SIZE", os.path.join(a.out, "write_size"))
+        bl = {}
+        blf = os.path.join(a.out, "fetch_size", "bench_line.json")
+        if os.path.exists(blf):
+            with open(blf) as fh:
+                bl = json.load(fh)
+    else:
+        fetch, bl = run_pass("FETCH_SIZE", a.out, a.bench_args)
+        write, _ = run_pass("WRITE_SIZE", a.out, a.bench_args)
     cfg = bl.get("config", {})
     sys.path.insert(0, ROOT)
     import bench
