@@ -257,6 +257,35 @@ def test_batched_large_table_vpt4_equals_torch(red, dev):
         assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
 
 
+@pytest.mark.parametrize("mib", [95, 97])
+@pytest.mark.parametrize("batched", [False, True], ids=["fold", "batched"])
+def test_store_policy_threshold_equals_torch(red, dev, mib, batched):
+    """Both sides of the write-through threshold (96 MiB per source,
+    bpsr_internal.h cache_pol): below it the kernels store with sc1, above
+    it with nt — same bytes either way.  3 fp32 sources, ragged lengths (a
+    partial last tile and element work), single fold and a 2-bucket table."""
+    g = torch.Generator(device=dev).manual_seed(mib)
+    N = 3
+    parts = [((mib << 20) // 4) + 5] if not batched else [((mib << 20) // 8) + 3, ((mib << 20) // 8) + 9]
+    buckets, checks = [], []
+    for ne in parts:
+        srcs = [torch.randn(ne, device=dev, generator=g) for _ in range(N)]
+        dst = torch.empty_like(srcs[0])
+        buckets.append((dst, srcs, ne * 4))
+        checks.append((dst, srcs))
+    if batched:
+        red.sum_batched(buckets, DType.FLOAT32)
+    else:
+        dst, srcs, nb = buckets[0]
+        red.sum_n(dst, srcs, nb, DType.FLOAT32)
+    torch.cuda.synchronize()
+    for dst, srcs in checks:
+        want = srcs[0].clone()
+        for s in srcs[1:]:
+            want.add_(s)
+        assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
+
+
 @pytest.mark.parametrize("dt", [DType.FLOAT16, DType.BFLOAT16], ids=lambda d: DType(d).name)
 def test_accum_f32_mode_within_one_ulp(red, dev, dt):
     from prophet_amd.reducer import MODE_ACCUM_F32
