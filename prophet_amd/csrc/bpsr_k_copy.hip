@@ -16,18 +16,29 @@ namespace bpsr {
 // keep the HBM queues full: 4 per CU with 8 KiB tiles measured 0.80 of the
 // roofline at 256 MiB vs 0.75 for the old grid-stride copy and 0.67 for
 // torch's (profiles/r01_copy_sweep.jsonl; Tuning::copy_occ / copy_vpt).
-template <int VPT>
+// Cache policy as for the folds (cache_pol): write-through stores below
+// Tuning::wt_max_bytes, nt above (the copy always reads nt).
+template <int VPT, int NT>
 static hipError_t launch_copy_vpt(const FoldArgs& a0, const Tuning& tu, hipStream_t s) {
   static KernelAttr attr;
   const hipError_t lds_ok =
-      allow_lds(attr, reinterpret_cast<const void*>(&fold_kernel<OpI8, VPT, true, 1>));
+      allow_lds(attr, reinterpret_cast<const void*>(&fold_kernel<OpI8, VPT, NT, 1>));
   if (lds_ok != hipSuccess) return lds_ok;
   FoldArgs a = a0;
   a.grid = (uint32_t)fold_grid(a.g, tu, VPT);
   const int occ = a.grid >= tu.occ_min_tiles ? tu.copy_occ : 0;
-  hipLaunchKernelGGL((fold_kernel<OpI8, VPT, true, 1>), dim3(a.grid), dim3(kBlock),
+  hipLaunchKernelGGL((fold_kernel<OpI8, VPT, NT, 1>), dim3(a.grid), dim3(kBlock),
                      occ_lds_bytes(occ), s, a);
   return hipGetLastError();
+}
+
+template <int NT>
+static hipError_t launch_copy_pol(const FoldArgs& a, int vpt, const Tuning& tu, hipStream_t s) {
+  switch (vpt) {
+    case 1: return launch_copy_vpt<1, NT>(a, tu, s);
+    case 2: return launch_copy_vpt<2, NT>(a, tu, s);
+    default: return launch_copy_vpt<4, NT>(a, tu, s);
+  }
 }
 
 hipError_t allow_lds(KernelAttr& once, const void* kernel, int bytes) {
@@ -52,11 +63,10 @@ hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
   int vpt = tu.copy_vpt;
   while (vpt > 1 && (a.g.nvec + (uint64_t)kBlock * vpt - 1) / ((uint64_t)kBlock * vpt) < kMinTiles)
     vpt >>= 1;
-  switch (vpt) {
-    case 1: return launch_copy_vpt<1>(a, tu, s);
-    case 2: return launch_copy_vpt<2>(a, tu, s);
-    default: return launch_copy_vpt<4>(a, tu, s);
-  }
+  Tuning tn = tu;
+  tn.nt = 1;  // the copy reads non-temporal whatever the fold tuning says
+  if (cache_pol(tn, a.g.nvec * 16) == kPolWt) return launch_copy_pol<kPolWt>(a, vpt, tu, s);
+  return launch_copy_pol<kPolNt>(a, vpt, tu, s);
 }
 
 hipError_t launch_fold(const FoldArgs& a, int dtype, int mode, const Tuning& tu,
