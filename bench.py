@@ -53,6 +53,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LEAD_CYCLES = 2_000_000  # spin ahead of a timed block (~1 ms of GPU clock)
 GIB = float(1 << 30)
 METRIC = "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs"
 # --dtype name -> (byteps DataType id, torch dtype name); ids: common.h:52-65 (+ bf16 = 11)
@@ -312,11 +313,17 @@ class _Clock:
             torch.cuda.synchronize()
 
     def time(self, fn, reps: int) -> float:
-        """ms per call of fn(i) over reps calls (after the caller's warm-up)."""
+        """ms per call of fn(i) over reps calls (after the caller's warm-up).
+        A short spin kernel goes first on the stream, so the host has queued
+        the start event and the first launches by the time the GPU reaches
+        them: the measured span holds device work only, not the host's issue
+        latency of the first launch (≈ 2 % of ten 0.1-ms folds)."""
         if self.cuda:
             import torch
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(self.stream):
+                torch.cuda._sleep(LEAD_CYCLES)
             e0.record(self.stream)
             for i in range(reps):
                 fn(i)
@@ -360,7 +367,7 @@ def _left_fold_equal(out, srcs) -> bool:
 # config 4: VGG-16 set sharded over the GPUs
 
 
-def scaling_leg(dev, world: int, rank: int, n_workers: int, fold, reps: int = 10,
+def scaling_leg(dev, world: int, rank: int, n_workers: int, fold, reps: int = 20,
                 n_elems: int | None = None, sets: int = 2) -> dict:
     """BASELINE config 4, device-resident part: every worker's fp32 VGG-16
     gradient vector is cut by the reference's reduce-scatter ownership

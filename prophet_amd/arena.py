@@ -11,8 +11,13 @@ allocations, tools/sweep.py; DESIGN.md "HBM layout").
 """
 from __future__ import annotations
 
-DEFAULT_SKEW = 16 * 1024   # bytes between consecutive slots beyond the (4 KiB-rounded) bucket
-ALIGN = 4096
+DEFAULT_SKEW = 16 * 1024   # bytes between consecutive slots beyond the (64 KiB-rounded) bucket
+# Buckets are rounded up to 64 KiB before the skew, so the skew's class
+# modulo the channel interleave does not depend on the bucket size: with 4 KiB
+# rounding a bucket of 8 KiB mod 16 KiB (config 4's VGG-16 shards) turned the
+# 16 KiB skew into an effective 24 KiB, a skew class measured 5-6 % slower
+# (DESIGN.md §5 "Arena skew"; r02s94: 99.3 vs 95.4 us for the G = 8 shard).
+ALIGN = 64 * 1024
 
 
 class BucketArena:

@@ -312,22 +312,27 @@ __device__ __forceinline__ void pin_args(const FoldArgs& a) {
 template <class Op, int VPT, int NT, int NS>
 __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs a) {
   pin_args<NS>(a);
-  // decided at entry, while the arguments are in SGPRs (no reload after the loop)
-  const int elem_mode = a.g.nvec == 0 ? 2 : (blockIdx.x == a.grid - 1 ? 1 : 0);
   // One tile per workgroup (the launcher sizes the grid to the tile count):
   // workgroups are dispatched in tile order, so the chip sweeps every operand
   // as one tight window (a persistent tile-stride loop measured 10-20 % slower).
+  // The slow pieces — the guarded partial last tile and the element work
+  // (unaligned head, tail, fp16 F16C tail, trailing bytes) — go to workgroup 0,
+  // first off the dispatcher, so they overlap the sweep instead of trailing it
+  // (as the last workgroup they extended every unaligned launch by its latency);
+  // the full tiles follow in address order.
   const uint64_t tile_vecs = (uint64_t)kBlock * VPT;
-  const uint64_t tile = blockIdx.x;
-  if ((tile + 1) * tile_vecs <= a.g.nvec)
+  const uint64_t full = a.g.nvec / tile_vecs;
+  const bool partial = full * tile_vecs < a.g.nvec;
+  const uint64_t bid = blockIdx.x;
+  // decided at entry, while the arguments are in SGPRs (no reload after the loop)
+  const int elem_mode = a.g.nvec == 0 ? 2 : (bid == 0 ? 1 : 0);
+  const uint64_t tile = partial ? (bid == 0 ? full : bid - 1) : bid;
+  if (tile < full)
     fold_tile_full_buf<Op, VPT, NT, NS>(a.srcs, a.srcs, a.n, a.dst,
                                         a.g.vec_off + tile * tile_vecs * 16, threadIdx.x);
   else if (tile * tile_vecs < a.g.nvec)
     fold_tile_body<Op, VPT, NT, NS, true>(a.srcs, a.srcs, a.n, a.dst, a.g.vec_off,
                                           tile * tile_vecs, a.g.nvec, threadIdx.x);
-  // Element work (unaligned head, tail, fp16 F16C tail, trailing bytes) is a
-  // handful of elements unless there is no vector range at all: give it to the
-  // last workgroup only, so no other workgroup pays the extra argument loads.
   if (elem_mode == 2)
     fold_elements<Op>(a.srcs, a.n, a.dst, a.g, a.aligned != 0,
                       (uint64_t)blockIdx.x * kBlock + threadIdx.x, (uint64_t)a.grid * kBlock);

@@ -25,7 +25,7 @@
 namespace bpsr {
 namespace {
 
-constexpr size_t kSlotAlign = 4096;
+constexpr size_t kSlotAlign = 64 * 1024;  // bucket rounding before the skew (prophet_amd/arena.py)
 constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots
 constexpr int kMaxDebugLog = 4096;
 // pull_many issues the copies of the rounds found finished once this many

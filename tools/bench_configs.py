@@ -45,6 +45,8 @@ def timed(fn, reps, stream):
     torch.cuda.synchronize()
     ts = []
     for r in range(3):
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(2_000_000)   # the host queues ahead of the GPU (bench.py _Clock)
         e0.record(stream)
         for i in range(reps):
             fn(i)
