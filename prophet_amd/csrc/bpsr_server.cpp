@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -83,7 +84,10 @@ struct KeyState {
   uint64_t key = 0;
   std::mutex mu;
   std::condition_variable cv;
-  bool allocated = false;
+  // Set once, last, by allocate() (under mu) after the slots, store, events
+  // and lane exist; those never change afterwards, so the pull and
+  // receive-slot paths may test it and read them before taking mu.
+  std::atomic<bool> allocated{false};
   bool inited = false;        // store initialised (round 0 done)
   size_t len = 0;
   int dtype = 0;
