@@ -26,6 +26,10 @@ owned slice (max over ranks), the G=1 time of the whole set measured in the
 same run, strong-scaling speedup/efficiency, and, for N > 1, the RCCL P2P
 scatter from a landing GPU plus the all-gather return leg.
 
+``local_reduce`` (N > 1): the worker's local reduce across the GPUs — every
+rank's full VGG-16-sized gradient summed by rank-order P2P reduce-scatter +
+HIP fold + all-gather, with RCCL's own all_reduce timed beside it.
+
 ``e2e_cfg5`` (every N, GPU runs): BASELINE config 5 from host memory — 16
 workers' 256 MiB bf16 pushes in pinned host buffers, each GPU streaming its
 key-space slice H2D -> fold -> D2H over its own PCIe link: the PCIe-inclusive
@@ -87,7 +91,7 @@ def parse(argv=None):
     p.add_argument("--layout", default="arena", choices=["arena", "separate"],
                    help="worker slots in one skewed HBM arena, or separate allocations")
     p.add_argument("--skew", type=int, default=-1,
-                   help="arena: bytes between consecutive slots beyond the 4 KiB-rounded "
+                   help="arena: bytes between consecutive slots beyond the 64 KiB-rounded "
                         "bucket (default: prophet_amd.arena.DEFAULT_SKEW)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-scaling", action="store_true",
@@ -506,6 +510,75 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
             "allgather_ms": round(t_gather * 1e3, 3),
             "node_fold_GiBps": round(n_workers * E * 4 / t_scatter / GIB, 1),
             "exact_vs_torch_fold": ok}
+
+
+def local_reduce_leg(dev, world: int, rank: int, reps: int = 5, n_elems: int | None = None,
+                     fold=None) -> dict:
+    """The worker's local reduce (core_loops.cc:184-263),
+    N > 1 only: every GPU holds its own full fp32 VGG-16 gradient vector and
+    all of them are summed across the node.  ``ShardedReducer.allreduce`` =
+    RCCL grouped P2P of every slice to its owner (the reduce-scatter
+    ownership of core_loops.cc:208-211), the HIP fold of the slices in RANK
+    order, then the all-gather return leg — bit-reproducible, unlike a ring.
+    RCCL's own ``all_reduce`` on the same bytes is timed beside it for
+    reference (its summation order follows the ring).  Exactness: strided
+    windows of the result against torch's left fold, in rank order, of every
+    rank's vector regenerated from its seed."""
+    import torch
+    import torch.distributed as dist
+    from prophet_amd.buckets import vgg16_param_sizes
+    from prophet_amd.shard import ShardedReducer
+    E = n_elems or sum(vgg16_param_sizes())
+    sr = ShardedReducer(E, fold=fold)   # fold=None: the HIP fold (tests inject a CPU one)
+    cuda = dev.type == "cuda"
+
+    def vec(r):
+        g = torch.Generator(device=dev)
+        g.manual_seed(6100 + r)
+        return torch.randn(E, device=dev, generator=g)
+    local = vec(rank)
+    out = torch.empty(E, device=dev)
+    recv = [torch.empty(sr.owned, device=dev) for _ in range(world)]
+    owned = torch.empty(sr.owned, device=dev)
+    ring = local.clone()
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    def timed(fn):
+        fn()
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        sync()
+        dist.barrier()
+        return _max_over_ranks(dist, dev, [(time.perf_counter() - t0) / reps])[0]
+
+    t_det = timed(lambda: sr.allreduce(local, out, recv, owned))
+    t_ring = timed(lambda: dist.all_reduce(ring))
+    ok = True
+    win = 1 << 16
+    starts = sorted({0, E // 3, E // 2, max(0, E - win)})
+    for w0 in starts:
+        w1 = min(E, w0 + win)
+        want = None
+        for r in range(world):          # the left fold in rank order
+            x = vec(r)[w0:w1]
+            want = x.clone() if want is None else want.add_(x)
+        ok = ok and bool(torch.equal(want.view(torch.int32), out[w0:w1].view(torch.int32)))
+    ok = _all_true(dist, dev, ok)
+    nbytes = E * 4
+    return {"workload": (f"worker local reduce: {world} GPUs each holding a {nbytes} B fp32 "
+                         f"(VGG-16-sized) gradient; rank-order P2P reduce-scatter + HIP fold + "
+                         f"all-gather (ShardedReducer.allreduce) vs RCCL all_reduce"),
+            "allreduce_ms": round(t_det * 1e3, 3),
+            "busbw_GBps": round(2 * (world - 1) / world * nbytes / t_det / 1e9, 1),
+            "rccl_allreduce_ms": round(t_ring * 1e3, 3),
+            "rccl_busbw_GBps": round(2 * (world - 1) / world * nbytes / t_ring / 1e9, 1),
+            "exact_vs_rank_order_fold": ok, "reps": reps}
 
 
 # --------------------------------------------------------------------------
@@ -970,6 +1043,13 @@ def main(argv=None):
                         fold=None if cuda else _torch_fold)
                 except Exception as e:  # report, never hide
                     line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
+        if world > 1 and not args.no_scatter:
+            try:
+                line["local_reduce"] = local_reduce_leg(
+                    dev, world, rank, n_elems=args.scaling_elems or None,
+                    fold=None if cuda else _torch_fold)
+            except Exception as e:  # report, never hide
+                line["local_reduce"] = {"error": repr(e)}
         if cuda and not args.no_e2e:
             try:
                 line["e2e_cfg5"] = e2e_leg(dev, world, rank,

@@ -48,6 +48,9 @@ def test_launcher_one_line_n_ranks(n):
     else:
         assert sc["scatter"]["exact_vs_torch_fold"] is True
         assert sc["scatter"]["scatter_fold_ms"] > 0
+        lr = line["local_reduce"]
+        assert "error" not in lr, lr
+        assert lr["exact_vs_rank_order_fold"] is True and lr["allreduce_ms"] > 0
 
 
 def test_torchrun_launch_one_line():
