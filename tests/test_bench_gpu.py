@@ -67,3 +67,44 @@ def test_bench_one_gpu_line_has_every_object():
     e2e = line["e2e_cfg5"]
     assert "error" not in e2e, e2e
     assert e2e["exact_vs_torch_fold_windows"] is True and e2e["pcie_inclusive"] is True
+
+
+def _lr_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        r = bench.local_reduce_leg(torch.device("cuda", 0), world, rank, reps=1,
+                                   n_elems=1_000_003)
+        q.put((rank, r))
+        dist.destroy_process_group()
+    except Exception as e:  # reported to the parent
+        q.put((rank, {"error": repr(e)}))
+
+
+def test_local_reduce_leg_two_gloo_ranks_on_one_gpu():
+    """The N > 1 ``local_reduce`` object's code path on one GPU: two gloo
+    ranks (CUDA tensors through gloo's P2P), each folding its owned slice with
+    the HIP fold in rank order; windows bit-exact against the rank-order left
+    fold of both regenerated vectors (timings here are not measurements)."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_lr_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert "error" not in out[r], out[r]
+        assert out[r]["exact_vs_rank_order_fold"] is True
