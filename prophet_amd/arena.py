@@ -18,6 +18,7 @@ DEFAULT_SKEW = 16 * 1024   # bytes between consecutive slots beyond the (64 KiB-
 # 16 KiB skew into an effective 24 KiB, a skew class measured 5-6 % slower
 # (DESIGN.md §5 "Arena skew"; r02s94: 99.3 vs 95.4 us for the G = 8 shard).
 ALIGN = 64 * 1024
+SMALL = 1 << 20      # below this, 4 KiB rounding (latency-bound, keep small slots small)
 
 
 class BucketArena:
@@ -26,7 +27,8 @@ class BucketArena:
     def __init__(self, n_slots: int, bucket_bytes: int, device, skew: int = DEFAULT_SKEW):
         import torch
         self.bucket_bytes = int(bucket_bytes)
-        self.stride = (self.bucket_bytes + ALIGN - 1) // ALIGN * ALIGN + int(skew)
+        align = ALIGN if self.bucket_bytes >= SMALL else 4096
+        self.stride = (self.bucket_bytes + align - 1) // align * align + int(skew)
         self.n_slots = n_slots
         self.slab = torch.empty(self.stride * n_slots, dtype=torch.uint8, device=device)
 

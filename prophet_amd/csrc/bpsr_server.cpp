@@ -204,7 +204,11 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   if (elem_size(dtype) == 0) return fail(BYTEPS_REDUCE_EDTYPE, "Unsupported data type: %d", dtype);
   if (len == 0) return fail(BYTEPS_REDUCE_EARGS, "init tensor size not larger than 0");
   const int N = s->cfg.num_workers;
-  ks->stride = (len + kSlotAlign - 1) / kSlotAlign * kSlotAlign + kSlotSkew;
+  // buckets of 1 MiB and more round to 64 KiB (the skew's class must not
+  // depend on len, prophet_amd/arena.py); smaller ones to 4 KiB (small keys
+  // are latency-bound, and many of them should not cost 80 KiB a slot)
+  const size_t align = len >= (1u << 20) ? kSlotAlign : 4096;
+  ks->stride = (len + align - 1) / align * align + kSlotSkew;
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, ks->stride * (size_t)(N + 1));
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(key arena)");
