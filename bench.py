@@ -706,7 +706,9 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     it is released (byteps_reduce_blockq_*).  ``live``: the
     launch, then the 12 per-block releases from a second stream (as the push
     path issues them behind each block's pushes); ``pre_released``: every block
-    released before the launch.  Device time per iteration from HIP events on
+    released before the launch; ``live_host_releases``: the launch, then the 12
+    releases from the host (byteps_reduce_blockq_release_host — the pushes are
+    resident, as after an RDMA write into HBM), no stream work per release.  Device time per iteration from HIP events on
     the consumer's stream (median of ``reps`` runs of ``iters`` back-to-back
     iterations over ``sets`` rotated input sets), host time of the issuing
     loop, exactness against torch's own left fold."""
@@ -724,7 +726,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
         tset = set(blk)
         by_block.append([p for p in parts if p.tensor in tset])
     gen = torch.Generator(device=dev)
-    data, queues = [], []
+    data, queues, hqueues = [], [], []
     for i in range(sets):
         w = []
         for k in range(N):
@@ -737,6 +739,12 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                               for p in bp] for bp in by_block], DType.FLOAT16)
         q.config(wg_per_cu=0, timeout_s=1.0)
         queues.append(q)
+        hq = red.make_blockq([[(out[toff[p.tensor] + p.offset:][:p.len],
+                                [x[toff[p.tensor] + p.offset:][:p.len] for x in w], p.len)
+                               for p in bp] for bp in by_block], DType.FLOAT16)
+        hq.config(wg_per_cu=0, timeout_s=1.0)
+        hq.host_releases(True)
+        hqueues.append(hq)
     # the library's consumer stream: a hardware queue of its own, so a release
     # never waits behind the spinning consumer (include/bpsr/reduce.h)
     live_s = queues[0].stream()
@@ -754,6 +762,12 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
         q.release(-1, live_s)
         q.launch(live_s)
 
+    def live_host(i):   # the pushes are resident: releases straight from the host
+        q = hqueues[i % sets]
+        q.launch(live_s)
+        for b in range(nb):
+            q.release_host(b)
+
     # probe: one live iteration must complete before anything is timed (a
     # profiler that serialises dispatches would strand the consumer; it then
     # gives up after its 1-s timeout and status() raises, ending this leg)
@@ -766,7 +780,8 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                         f"{len(parts)} partitions in {nb} Prophet blocks, block queue "
                         "(one consumer launch per iteration)"),
            "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
-    for name, fn in (("live", live), ("pre_released", pre_released)):
+    for name, fn in (("live", live), ("pre_released", pre_released),
+                     ("live_host_releases", live_host)):
         for i in range(30):
             fn(i)
         torch.cuda.synchronize()
@@ -787,20 +802,21 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                      "spread": round((max(ts) - min(ts)) / ms, 4),
                      "frac_of_roofline": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "host_us_per_iter": round(statistics.median(hs), 1)}
-    for q in queues:
+    for q in queues + hqueues:
         q.status(live_s)
     ok = True
-    for i, (w, out) in enumerate(data):
-        out.zero_()
-        torch.cuda.synchronize()
-        live(i)
-        torch.cuda.synchronize()
-        ref = w[0].view(torch.float16).clone()
-        for x in w[1:]:
-            ref.add_(x.view(torch.float16))
-        ok = ok and bool(torch.equal(ref.view(torch.uint8), out))
+    for fn in (live, live_host):
+        for i, (w, out) in enumerate(data):
+            out.zero_()
+            torch.cuda.synchronize()
+            fn(i)
+            torch.cuda.synchronize()
+            ref = w[0].view(torch.float16).clone()
+            for x in w[1:]:
+                ref.add_(x.view(torch.float16))
+            ok = ok and bool(torch.equal(ref.view(torch.uint8), out))
     res["exact_vs_torch_fold"] = ok
-    for q in queues:
+    for q in queues + hqueues:
         q.close()
     return res
 

@@ -210,6 +210,20 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
                                        void* stream);
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream);
 int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
+/* Host releases (data already visible to the device, e.g. landed by RDMA into
+ * HBM or written by finished device work): after
+ * byteps_reduce_blockq_host_releases(q, 1), every launch carries one helper
+ * workgroup that forwards release words written by the HOST into the device
+ * words, and byteps_reduce_blockq_release_host(q, f, c) releases blocks
+ * [f, f + c) with a store to pinned host memory — no stream, no kernel, no
+ * copy per release (a release kernel running beside the consumer costs it
+ * ~0.4 us each).  The caller guarantees the blocks' data is
+ * complete and visible before the call; epochs, timeout and status as above;
+ * stream releases may still be mixed in.  Dispatch-ordered consumer only
+ * (wg_per_cu = 0); not with a captured launch.  on = 0 turns it off for later
+ * launches. */
+int byteps_reduce_blockq_host_releases(byteps_reduce_blockq* q, int on);
+int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int count);
 /* The device's consumer stream (see above); owned by the library. */
 int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream);
 /* Debug (synchronises the device): out = launch epoch, nblocks, the sticky

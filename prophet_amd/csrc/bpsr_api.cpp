@@ -605,6 +605,11 @@ struct byteps_reduce_blockq {
   uint32_t* rel_src = nullptr;  // pinned [kRelRing][nblocks]
   static constexpr int kRelRing = 16;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  // Host releases (byteps_reduce_blockq_host_releases): pinned, coherent
+  // words the host writes and the launch's helper workgroup forwards.
+  uint32_t* hflags = nullptr;
+  uint32_t* hflags_dev = nullptr;
+  bool host_rel = false;
 };
 
 // One consumer stream per device, created on first use, never destroyed:
@@ -648,6 +653,7 @@ static void blockq_free(byteps_reduce_blockq* q) {
   if (q->ctl) (void)hipFree(q->ctl);
   if (q->host_err) (void)hipHostFree(q->host_err);
   if (q->rel_src) (void)hipHostFree(q->rel_src);
+  if (q->hflags) (void)hipHostFree(q->hflags);
   delete q;
 }
 
@@ -730,6 +736,8 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
 int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
   if (wg_per_cu > 8) return fail(BYTEPS_REDUCE_EARGS, "wg_per_cu %d > 8", wg_per_cu);
+  if (wg_per_cu > 0 && q->host_rel)
+    return fail(BYTEPS_REDUCE_EARGS, "host releases need the dispatch-ordered consumer");
   if (wg_per_cu >= 0) q->occ = wg_per_cu;
   if (timeout_s > 0) q->timeout_s = timeout_s;
   return BYTEPS_REDUCE_OK;
@@ -761,7 +769,8 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.nblocks = (uint32_t)q->nblocks;
   Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
   Q.epoch = epoch;
-  Q.pad = 0;
+  Q.helper = 0;
+  Q.hflags = nullptr;
   const Tuning tu = tuning_for_n(q->ti.nmax);
   const bool gated = q->occ == 0;
   size_t lds;
@@ -772,6 +781,11 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     // (at hardware occupancy — 3 of these workgroups per CU — a live release
     // behind H2D copies on another stream never arrived).
     Q.grid = q->ti.tiles;
+    if (q->host_rel && cap != hipStreamCaptureStatusActive) {
+      Q.helper = 1;  // workgroup 0 forwards host releases (forward_host_releases)
+      Q.hflags = q->hflags_dev;
+      Q.grid += 1;
+    }
     int occ = launch_occ(tu, q->ti.tiles, true);
     if (occ == 0 || occ > q->gate_occ) occ = q->gate_occ;
     lds = occ_lds_bytes(occ);
@@ -831,6 +845,55 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
     if (e != hipSuccess) return hip_fail(e, "block release");
     for (int k = b; k < run; ++k) q->rel_epoch[k] = ep;
     b = run;
+  }
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_host_releases(byteps_reduce_blockq* q, int on) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  std::lock_guard<std::mutex> g(q->mu);
+  if (!on) {
+    q->host_rel = false;
+    return BYTEPS_REDUCE_OK;
+  }
+  if (q->occ != 0)
+    return fail(BYTEPS_REDUCE_EARGS, "host releases need the dispatch-ordered consumer "
+                                     "(byteps_reduce_blockq_config wg_per_cu = 0)");
+  if (!q->hflags) {
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, sizeof(uint32_t) * (size_t)q->nblocks,
+                                 hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc(host release words)");
+    void* d = nullptr;
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(p);
+      return hip_fail(e, "hipHostGetDevicePointer(host release words)");
+    }
+    q->hflags = static_cast<uint32_t*>(p);
+    q->hflags_dev = static_cast<uint32_t*>(d);
+    // 0 = never released from the host (the helper skips such words)
+    for (int b = 0; b < q->nblocks; ++b)
+      __atomic_store_n(q->hflags + b, 0u, __ATOMIC_RELEASE);
+  }
+  q->host_rel = true;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int count) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (first < 0 || count < 0 || first > q->nblocks || count > q->nblocks - first)
+    return fail(BYTEPS_REDUCE_EARGS, "blocks [%d, %d+%d) outside [0, %d)", first, first, count,
+                q->nblocks);
+  std::lock_guard<std::mutex> g(q->mu);
+  if (!q->host_rel)
+    return fail(BYTEPS_REDUCE_EARGS, "host releases not enabled (byteps_reduce_blockq_host_releases)");
+  // Each block's word carries its own next epoch (as release_range); the
+  // caller's data is complete before the call, so a release store suffices.
+  for (int b = first; b < first + count; ++b) {
+    const uint32_t ep = q->rel_epoch[b] + 1;
+    q->rel_epoch[b] = ep;
+    __atomic_store_n(q->hflags + b, ep, __ATOMIC_RELEASE);
   }
   return BYTEPS_REDUCE_OK;
 }

@@ -105,7 +105,8 @@ struct BlockqLaunch {
   uint32_t grid;            // launched (persistent) workgroups
   uint64_t timeout_ticks;   // wall_clock64() ticks a workgroup waits for a release
   uint32_t epoch;           // this launch's epoch (>= 1)
-  uint32_t pad;
+  uint32_t helper;          // 1: workgroup 0 forwards host release words (hflags)
+  const uint32_t* hflags;   // host-written release words (pinned, device view)
 };
 // Released for epoch e: the block's word holds e or a later epoch (wrap-safe).
 __host__ __device__ inline bool epoch_reached(uint32_t have, uint32_t e) {

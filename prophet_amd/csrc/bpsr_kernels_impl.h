@@ -537,9 +537,48 @@ __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
 // before its loads; one whose tile is released reads data no workgroup of
 // this launch has touched since the launch's own acquire (blocks do not share
 // lines), so it needs none.
+// Host releases (byteps_reduce_blockq_release_host): workgroup 0 of a launch
+// with Q.helper forwards the host-written words into the device words the
+// tiles poll, one system-scope load per block and lane, `s_sleep` between
+// sweeps, until every block holds this launch's epoch (or the sticky error /
+// the timeout ends the launch).  One wave works; the others return at once.
+// Vector atomics only (the release words are written through the vector
+// path, as blockq_release_kernel does).
+__device__ __forceinline__ void forward_host_releases(const BlockqLaunch& Q) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    bool pending = false;
+    for (uint32_t base = 0; base < Q.nblocks; base += 64) {
+      const uint32_t b = base + lane;
+      if (b < Q.nblocks) {
+        uint32_t d = ld_sys(Q.flags + b);
+        const uint32_t h = ld_sys(Q.hflags + b);
+        if (h != 0 && !epoch_reached(d, h)) {
+          __hip_atomic_fetch_max(Q.flags + b, h, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          d = h;
+        }
+        pending = pending || !epoch_reached(d, Q.epoch);
+      }
+    }
+    if (__ballot(pending) == 0) return;
+    if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    if (wall_clock64() - t0 > Q.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
-  const uint32_t t = blockIdx.x;
+  if (Q.helper && blockIdx.x == 0) {  // dispatched first: resident for the whole launch
+    forward_host_releases(Q);
+    return;
+  }
+  const uint32_t t = blockIdx.x - Q.helper;
   const uint32_t lane = threadIdx.x & 63u;
   const unsigned char* rec = Q.L.recs + (uint64_t)t * Q.L.rec_stride;
   // the words (vector load) and the record (scalar loads) travel together

@@ -51,7 +51,8 @@ EXPORTS = (
     "byteps_reduce_blockq_create", "byteps_reduce_blockq_config", "byteps_reduce_blockq_launch",
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
     "byteps_reduce_blockq_debug", "byteps_reduce_blockq_stream",
-    "byteps_reduce_blockq_release_range",
+    "byteps_reduce_blockq_release_range", "byteps_reduce_blockq_host_releases",
+    "byteps_reduce_blockq_release_host",
 )
 
 
@@ -104,6 +105,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_release.argtypes = [_vp, _int, _vp]
     L.byteps_reduce_blockq_release_range.argtypes = [_vp, _int, _int, _vp]
     L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
+    L.byteps_reduce_blockq_host_releases.argtypes = [_vp, _int]
+    L.byteps_reduce_blockq_release_host.argtypes = [_vp, _int, _int]
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     L.byteps_reduce_blockq_debug.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint32), _int]
     L.byteps_reduce_blockq_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
@@ -296,6 +299,16 @@ class BlockQueue:
         """Release blocks [first, first + count) with one kernel."""
         _check(self.lib.byteps_reduce_blockq_release_range(self.handle, int(first), int(count),
                                                            _stream_of(self.first, stream)))
+
+    def host_releases(self, on: bool = True) -> None:
+        """Later launches carry a helper workgroup that forwards host
+        releases (``release_host``); dispatch-ordered consumer only."""
+        _check(self.lib.byteps_reduce_blockq_host_releases(self.handle, 1 if on else 0))
+
+    def release_host(self, first: int, count: int = 1) -> None:
+        """Release blocks [first, first + count) from the host: no stream, no
+        kernel.  Their data must already be complete and visible to the device."""
+        _check(self.lib.byteps_reduce_blockq_release_host(self.handle, int(first), int(count)))
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))

@@ -377,3 +377,117 @@ def test_live_release_never_behind_consumer_any_stream_pair():
         bq.status(cons)                               # raises on a timeout
         assert all(torch.equal(o, r) for o, r in zip(outs, refs)), i
     bq.close()
+
+
+# ------------------------------------------------- host releases (no stream) --
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16, DType.INT32],
+                         ids=lambda d: DType(d).name)
+def test_host_releases_live_three_iterations(red, dev, dt):
+    """Data resident, consumer launched first, then every block released from
+    the HOST in a shuffled order (byteps_reduce_blockq_release_host, forwarded
+    by the launch's helper workgroup): bit-exact with the oracle, 3 epochs."""
+    tab = Table(dev, dt, MIXED, offsets=True)
+    q = red.make_blockq(tab.blocks, dt)
+    q.host_releases(True)
+    rng = np.random.default_rng(5)
+    for it in range(3):
+        pushes, wants = tab.host_inputs(300 * it + 11)
+        tab.upload(pushes)
+        torch.cuda.synchronize()          # data complete and visible: host releases allowed
+        q.launch()
+        for b in rng.permutation(len(MIXED)):
+            q.release_host(int(b))
+        q.status()
+        torch.cuda.synchronize()
+        tab.check(wants)
+    q.close()
+
+
+def test_host_releases_after_device_copies_and_mixed_with_stream_releases(red, dev):
+    """Blocks 0-1 land by device copies on a side stream and are released from
+    the host once an event says they landed; blocks 2-4 are released on the
+    stream as before.  Both kinds in one launch, exact; then a pre-released
+    iteration (releases before the launch) through the host path."""
+    dt = DType.FLOAT32
+    tab = Table(dev, dt, MIXED)
+    q = red.make_blockq(tab.blocks, dt)
+    q.host_releases(True)
+    pushes, wants = tab.host_inputs(901)
+    staged = [[p.to(dev) for p in ps] for ps in pushes]
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    q.launch()
+    ev = torch.cuda.Event()
+    with torch.cuda.stream(side):
+        for (dst, srcs, L, *_), st in zip(tab.views, staged):
+            for s_, x in zip(srcs, st):
+                if L:
+                    s_.copy_(x)
+        ev.record(side)
+    q.release_range(2, 3, side)            # stream-ordered, behind the copies
+    ev.synchronize()                       # host knows blocks 0-1 landed
+    q.release_host(0, 2)
+    q.status()
+    torch.cuda.synchronize()
+    tab.check(wants)
+    pushes, wants = tab.host_inputs(902)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    q.release_host(0, len(MIXED))         # before the launch
+    q.launch()
+    q.status()
+    torch.cuda.synchronize()
+    tab.check(wants)
+    q.close()
+
+
+def test_host_release_missing_times_out_and_recovers(red, dev):
+    from prophet_amd.reducer import ETIMEOUT, ReduceError
+    dt = DType.FLOAT32
+    blocks = [[(500_000, 8, "normal")], [(123_457, 8, "normal")], [(400_000, 8, "normal")]]
+    tab = Table(dev, dt, blocks)
+    q = red.make_blockq(tab.blocks, dt)
+    q.config(timeout_s=0.2)
+    q.host_releases(True)
+    pushes, wants = tab.host_inputs(78)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    q.launch()
+    q.release_host(0, 2)                  # block 2 never
+    with pytest.raises(ReduceError) as ei:
+        q.status()
+    assert ei.value.code == ETIMEOUT
+    for i in (0, 1):
+        assert np.array_equal(tab.views[i][0].cpu().numpy(), wants[i])
+    q.status()                            # cleared
+    q.launch()
+    q.release_host(0, 3)
+    q.status()
+    tab.check(wants)
+    q.close()
+
+
+def test_host_releases_rules(red, dev):
+    """Persistent consumers refuse host releases (and vice versa); releasing
+    from the host before enabling it, or outside the table, is EARGS."""
+    from prophet_amd.reducer import EARGS, ReduceError
+    dt = DType.FLOAT32
+    tab = Table(dev, dt, [[(4096, 2, "normal")], [(4096, 2, "normal")]])
+    q = red.make_blockq(tab.blocks, dt)
+    with pytest.raises(ReduceError) as ei:
+        q.release_host(0)
+    assert ei.value.code == EARGS
+    q.config(wg_per_cu=1)
+    with pytest.raises(ReduceError):
+        q.host_releases(True)
+    q.config(wg_per_cu=0)
+    q.host_releases(True)
+    with pytest.raises(ReduceError):
+        q.config(wg_per_cu=2)
+    with pytest.raises(ReduceError):
+        q.release_host(1, 2)
+    q.host_releases(False)
+    q.config(wg_per_cu=1)
+    q.close()
