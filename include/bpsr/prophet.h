@@ -188,8 +188,14 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  * a synchronous copy) between begin and its last push: the consumer waits
  * for releases only that thread would issue, until its timeout.  The
  * scheduler and block queue must outlive the loop and must not be driven
- * directly while it runs. */
-enum { BYTEPS_PROPHET_LOOP_INLINE = 1 };
+ * directly while it runs.
+ * With flags & BYTEPS_PROPHET_LOOP_HOST_RELEASE the complete blocks are
+ * released from the host (byteps_reduce_blockq_release_host, no stream work;
+ * create enables host releases on the block queue): for pushes whose bytes are
+ * already visible to the device when byteps_prophet_loop_push is called
+ * (RDMA into HBM, or copies the caller has waited for); release_stream is then
+ * unused. */
+enum { BYTEPS_PROPHET_LOOP_INLINE = 1, BYTEPS_PROPHET_LOOP_HOST_RELEASE = 2 };
 typedef struct byteps_prophet_loop byteps_prophet_loop;
 int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,
                                const int32_t* block_of, int32_t nhandles, int32_t nblocks,

@@ -8,8 +8,9 @@
 // arrive, counts released partitions per block and, at the end of each
 // release group, releases every block that became complete — one
 // byteps_reduce_blockq_release_range per run of consecutive blocks, on the
-// release stream, behind the copies that landed the pushes — then reports the
-// group's partitions finished (credit back to the scheduler).
+// release stream, behind the copies that landed the pushes, or from the host
+// with BYTEPS_PROPHET_LOOP_HOST_RELEASE when the pushes are already in HBM —
+// then reports the group's partitions finished (credit back to the scheduler).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -47,6 +48,7 @@ struct byteps_prophet_loop {
   std::vector<char> got;            // task handle pushed this iteration
   int err = 0;
   bool inline_drain = false;   // BYTEPS_PROPHET_LOOP_INLINE: pushers drain
+  bool host_release = false;   // BYTEPS_PROPHET_LOOP_HOST_RELEASE: release_host, no stream
   std::atomic<bool> waiting{false};  // the loop thread sleeps on cv
   std::mutex drain_mu;
   std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
@@ -68,7 +70,8 @@ struct byteps_prophet_loop {
       }
       int e = b;
       while (e < nb && !released[e] && left[e] == 0) released[e++] = 1;
-      const int rc = byteps_reduce_blockq_release_range(bq, b, e - b, rel_stream);
+      const int rc = host_release ? byteps_reduce_blockq_release_host(bq, b, e - b)
+                                  : byteps_reduce_blockq_release_range(bq, b, e - b, rel_stream);
       if (rc) return rc;
       blocks_released += e - b;
       b = e;
@@ -169,6 +172,14 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
     return bpsr::hip_fail(e, "hipGetDevice");
   }
   l->inline_drain = (flags & BYTEPS_PROPHET_LOOP_INLINE) != 0;
+  l->host_release = (flags & BYTEPS_PROPHET_LOOP_HOST_RELEASE) != 0;
+  if (l->host_release) {
+    const int rc = byteps_reduce_blockq_host_releases(bq, 1);
+    if (rc) {
+      delete l;
+      return rc;
+    }
+  }
   if (!l->inline_drain) l->th = std::thread([l] { l->run(); });
   *out = l;
   return 0;

@@ -205,14 +205,18 @@ class PushLoop:
     issue, until its timeout."""
 
     def __init__(self, queue: ProphetPushQueue, blockq, block_of, release_stream=None,
-                 inline: bool = False):
+                 inline: bool = False, host_release: bool = False):
+        """``host_release=True``: complete blocks are released from the host
+        (``BlockQueue.release_host``, no stream work) — for pushes whose bytes
+        are already visible to the device when ``push`` is called."""
         self._L = _lib()
         self.queue, self.blockq = queue, blockq
         bo = (ctypes.c_int32 * max(len(block_of), 1))(*block_of)
         h = ctypes.c_void_p()
+        flags = (1 if inline else 0) | (2 if host_release else 0)
         _ck(self._L.byteps_prophet_loop_create(queue._h, blockq.handle, bo, len(block_of),
                                                blockq.nblocks, _stream_ptr(release_stream),
-                                               1 if inline else 0, ctypes.byref(h)))
+                                               flags, ctypes.byref(h)))
         self._h = h
 
     def begin(self, consumer_stream=None) -> None:

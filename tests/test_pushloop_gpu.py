@@ -76,15 +76,19 @@ def _feed(loop, tasks, seed, skip=None):
         loop.push(t, i)
 
 
+@pytest.mark.parametrize("host", [False, True], ids=["stream_release", "host_release"])
 @pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
 @pytest.mark.parametrize("net_b", [10**6, 1000], ids=["whole_blocks", "budget_cuts_blocks"])
-def test_push_loop_iterations_exact(net_b, inline):
+def test_push_loop_iterations_exact(net_b, inline, host):
+    """host: the loop releases complete blocks from the host (the pushes are
+    resident before the iteration begins, BYTEPS_PROPHET_LOOP_HOST_RELEASE)."""
     from prophet_amd.prophet import PushLoop
     S = _setup(net_b=net_b)
     cons = S["bq"].stream()              # the library's consumer stream
     rel = torch.cuda.Stream()
     torch.cuda.synchronize()
-    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline)
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline,
+                    host_release=host)
     import gc
     gc.collect()      # inline: no GC-triggered hipFree may run inside an iteration
     for it in range(3):

@@ -183,7 +183,10 @@ int main(int argc, char** argv) {
   // the library's PUSH loop (byteps_prophet_loop_*): one scheduler + loop per
   // input set (each set has its own block queue)
   std::vector<byteps_prophet_queue*> lq(kSets, nullptr);
-  std::vector<byteps_prophet_loop*> loops(kSets, nullptr), iloops(kSets, nullptr);
+  std::vector<byteps_prophet_loop*> loops(kSets, nullptr), iloops(kSets, nullptr),
+      hloops(kSets, nullptr);
+  std::vector<byteps_prophet_queue*> hq(kSets, nullptr);  // host-release loops' schedulers
+  std::vector<byteps_reduce_blockq*> hbq(kSets, nullptr);   // and block queues
   std::vector<int> left(nb);
   double sched_us = 0;
   long sched_iters = 0, groups_seen = 0, release_calls = 0;
@@ -316,6 +319,15 @@ int main(int argc, char** argv) {
     sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     ++sched_iters;
   };
+  const Fn push_loop_host = [&](int i) {
+    const int k = i % kSets;
+    const auto t0 = std::chrono::steady_clock::now();
+    CKR(byteps_prophet_loop_begin(hloops[k], cons));
+    for (const auto& t : tasks.arrivals) CKR(byteps_prophet_loop_push(hloops[k], &t));
+    CKR(byteps_prophet_loop_end(hloops[k], 5.0));
+    sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ++sched_iters;
+  };
   const Fn push_loop = [&](int i) {
     const int k = i % kSets;
     const auto t0 = std::chrono::steady_clock::now();
@@ -358,6 +370,19 @@ int main(int argc, char** argv) {
     }
     variants.push_back({"blockq_prophet_push_loop", &push_loop});
     variants.push_back({"blockq_prophet_push_loop_inline", &push_loop_inline});
+    // host releases (data resident): separate block queues, since enabling
+    // host releases adds the forwarding workgroup to every later launch
+    for (int k = 0; k < kSets; ++k) {
+      CKR(byteps_prophet_create(&pc, &hq[k]));
+      auto hd = descs(t, sets[k], sets[k].out);
+      CKR(byteps_reduce_blockq_create(hd.data(), (int)hd.size(), t.block_end.data(), nb,
+                                      BYTEPS_REDUCE_FLOAT16, BYTEPS_REDUCE_MODE_REFERENCE,
+                                      &hbq[k]));
+      CKR(byteps_reduce_blockq_config(hbq[k], 0, 5.0));
+      CKR(byteps_prophet_loop_create(hq[k], hbq[k], block_of.data(), (int32_t)block_of.size(),
+                                     nb, nullptr, BYTEPS_PROPHET_LOOP_HOST_RELEASE, &hloops[k]));
+    }
+    variants.push_back({"blockq_prophet_push_loop_host_release", &push_loop_host});
   }
   const double alg = (double)(N + 1) * (double)t.total;
   hipEvent_t e0, e1;
@@ -417,7 +442,10 @@ int main(int argc, char** argv) {
   for (int k = 0; k < kSets; ++k) {
     if (loops[k]) byteps_prophet_loop_destroy(loops[k]);
     if (iloops[k]) byteps_prophet_loop_destroy(iloops[k]);
+    if (hloops[k]) byteps_prophet_loop_destroy(hloops[k]);
     if (lq[k]) byteps_prophet_destroy(lq[k]);
+    if (hq[k]) byteps_prophet_destroy(hq[k]);
+    if (hbq[k]) byteps_reduce_blockq_destroy(hbq[k]);
   }
   if (sched) byteps_prophet_destroy(sched);
   for (auto& s : sets) {
