@@ -1036,7 +1036,11 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 5)},
+                     "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 5),
+                     # also the read stream alone (N * B of the
+                     # (N + 1) * B), against the same peak
+                     "read_only_GBps": round(N * B / (kern_ms * 1e-3) / 1e9, 1),
+                     "read_only_frac": round(N * B / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "check_vs_torch_fold": ok,
     }
     if not cuda:
