@@ -39,7 +39,7 @@ for s in $STEPS; do
                         "f32 reference 2"; do
               set -- $spec
               run dt_$1_$2_$3 200 python bench.py --dtype $1 --mode $2 --workers $3 --steps 50 \
-                  --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 || exit 1
+                  --no-cpu-baseline --no-scaling --no-cfg3 --no-fp16 --no-e2e || exit 1
             done ;;
     configs) run configs 900 python tools/bench_configs.py --only cfg1,sweep,cfg4,cfg5,cfg2e2e ;;
     pmc3)  run pmc_cfg3 400 python tools/pmc_cfg3.py "$OUT/pmc_cfg3" ;;
