@@ -234,6 +234,8 @@ inline int fold_vpt(uint64_t nvec, int vpt) {
 // (DESIGN.md §4.1); long sweeps stream faster with nt stores.
 constexpr int kPolPlain = 0, kPolNt = 1, kPolWt = 2;
 constexpr uint64_t kWtMaxBytes = 96ull << 20;  // per source (Tuning default)
+// write-through folds from this size per source run 4-KiB tiles, 2 per CU
+constexpr uint64_t kHalfTileMinBytes = 64ull << 20;
 inline int cache_pol(const Tuning& tu, uint64_t bytes_per_src) {
   if (!tu.nt) return kPolPlain;
   return bytes_per_src < tu.wt_max_bytes ? kPolWt : kPolNt;

@@ -286,6 +286,23 @@ def test_store_policy_threshold_equals_torch(red, dev, mib, batched):
         assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
 
 
+@pytest.mark.parametrize("nbytes", [69_178_772, (80 << 20) + 6, 95 << 20])
+def test_half_tile_band_equals_torch(red, dev, nbytes):
+    """8-way folds of 64-96 MiB per source run 4-KiB tiles at 2 workgroups
+    per CU (bpsr_kernels_impl.h launch_fold_op); config 4's G = 8 shard and
+    ragged sizes, against torch's left fold."""
+    g = torch.Generator(device=dev).manual_seed(nbytes % 1000)
+    ne = nbytes // 4
+    srcs = [torch.randn(ne, device=dev, generator=g) for _ in range(8)]
+    dst = torch.empty_like(srcs[0])
+    red.sum_n(dst, srcs, nbytes, DType.FLOAT32)
+    want = srcs[0].clone()
+    for x in srcs[1:]:
+        want.add_(x)
+    torch.cuda.synchronize()
+    assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
+
+
 @pytest.mark.parametrize("dt", [DType.FLOAT16, DType.BFLOAT16], ids=lambda d: DType(d).name)
 def test_accum_f32_mode_within_one_ulp(red, dev, dt):
     from prophet_amd.reducer import MODE_ACCUM_F32
