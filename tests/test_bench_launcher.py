@@ -103,3 +103,30 @@ def test_traffic_quoted_only_for_same_kernel_sources(tmp_path, monkeypatch):
     assert t is None and "changed" in src["status"]
     t, src = bench.pmc_traffic("other workload")
     assert t is None
+
+
+def test_pmc_tool_counts_the_headline_kernel_only(tmp_path):
+    """tools/pmc_traffic.py sums each dispatch's counter over the headline
+    kernel only: other fold instantiations in the same pass (the bench line's
+    fp16, config-3/4/5 objects) must not enter the median."""
+    import csv
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic
+    d = tmp_path / "write_size"
+    d.mkdir()
+    rows = []
+    for i in range(5):   # headline dispatches, counter split over two rows each
+        for part in (100.0, 28.0):
+            rows.append({"Dispatch_Id": str(i), "Kernel_Name":
+                         "void bpsr::fold_kernel<bpsr::OpF32, 2, 1, 8>(bpsr::FoldArgs)",
+                         "Counter_Name": "WRITE_SIZE", "Counter_Value": str(part)})
+    for i in range(5, 30):   # another fold in the same pass
+        rows.append({"Dispatch_Id": str(i), "Kernel_Name":
+                     "void bpsr::fold_kernel<bpsr::OpBF16, 4, 2, 16>(bpsr::FoldArgs)",
+                     "Counter_Name": "WRITE_SIZE", "Counter_Value": "7"})
+    with open(d / "x_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    vals = pmc_traffic.collect("WRITE_SIZE", str(d))
+    assert sorted(vals) == [128.0] * 5
