@@ -28,6 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # bench line's fp16, config-3/4/5 objects, when not disabled) must not enter
 # the median
 KERNEL_KEY = "fold_kernel<bpsr::OpF32, 2, 1, 8>"
+KERNEL = None   # --kernel
 
 
 def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[float], dict]:
@@ -45,11 +46,13 @@ def run_pass(counter: str, outdir: str, bench_args: list[str]) -> tuple[list[flo
         raise SystemExit(f"rocprofv3 pass {counter} failed rc={r.returncode}\n{r.stderr[-3000:]}")
     with open(os.path.join(d, "bench_line.json"), "w") as fh:
         json.dump(bench_line, fh)
-    return collect(counter, d), bench_line
+    return collect(counter, d, KERNEL), bench_line
 
 
-def collect(counter: str, d: str) -> list[float]:
-    """Per-dispatch counter sums of the headline kernel from a pass's CSVs."""
+def collect(counter: str, d: str, kernel: str | None = None) -> list[float]:
+    """Per-dispatch counter sums of the headline kernel (or ``kernel``) from a
+    pass's CSVs."""
+    kname = kernel or KERNEL_KEY
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -57,7 +60,7 @@ def collect(counter: str, d: str) -> list[float]:
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if KERNEL_KEY not in row.get("Kernel_Name", ""):
+                if kname not in row.get("Kernel_Name", ""):
                     continue
                 if row.get("Counter_Name") != counter:
                     continue
@@ -72,16 +75,20 @@ def main():
     p.add_argument("--commit", action="store_true")
     p.add_argument("--session", default=os.environ.get("BPSR_SESSION", ""),
                    help="session tag recorded with the numbers (bench line traffic_source)")
+    p.add_argument("--kernel", default=None,
+                   help="kernel-name substring to count (default: the headline kernel)")
     p.add_argument("--reaggregate", action="store_true",
                    help="re-read the passes already under --out (no profiling run)")
     p.add_argument("bench_args", nargs="*",
                    default=["--steps", "12", "--warmup", "2", "--no-cpu-baseline",
                             "--no-scaling", "--no-cfg3", "--no-fp16", "--no-e2e"])
     a = p.parse_args()
+    global KERNEL
+    KERNEL = a.kernel
     os.makedirs(a.out, exist_ok=True)
     if a.reaggregate:
-        fetch = collect("FETCH_SIZE", os.path.join(a.out, "fetch_size"))
-        write = collect("WRITE_SIZE", os.path.join(a.out, "write_size"))
+        fetch = collect("FETCH_SIZE", os.path.join(a.out, "fetch_size"), KERNEL)
+        write = collect("WRITE_SIZE", os.path.join(a.out, "write_size"), KERNEL)
         bl = {}
         blf = os.path.join(a.out, "fetch_size", "bench_line.json")
         if os.path.exists(blf):
@@ -97,7 +104,7 @@ def main():
         "workload": cfg.get("workload"),
         "session": a.session or None,
         "kernel_build": bench.kernel_build_id(),
-        "kernel": KERNEL_KEY,
+        "kernel": KERNEL or KERNEL_KEY,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_median": statistics.median(fetch) if fetch else None,
         "WRITE_SIZE_KiB_median": statistics.median(write) if write else None,
