@@ -708,9 +708,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     path issues them behind each block's pushes); ``pre_released``: every block
     released before the launch; ``live_host_releases``: the launch, then the 12
     releases from the host (byteps_reduce_blockq_release_host — the pushes are
-    resident, as after an RDMA write into HBM), no stream work per release;
-    ``live_release_after``: stream-ordered releases like ``live`` through an
-    event and the host words (byteps_reduce_blockq_release_after), no kernel.  Device time per iteration from HIP events on
+    resident, as after an RDMA write into HBM), no stream work per release.  Device time per iteration from HIP events on
     the consumer's stream (median of ``reps`` runs of ``iters`` back-to-back
     iterations over ``sets`` rotated input sets), host time of the issuing
     loop, exactness against torch's own left fold."""
@@ -770,12 +768,6 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
         for b in range(nb):
             q.release_host(b)
 
-    def live_after(i):  # stream-ordered like `live`, but event + host word, no kernel
-        q = hqueues[i % sets]
-        q.launch(live_s)
-        for b in range(nb):
-            q.release_after(b, 1, rel_s)
-
     # probe: one live iteration must complete before anything is timed (a
     # profiler that serialises dispatches would strand the consumer; it then
     # gives up after its 1-s timeout and status() raises, ending this leg)
@@ -789,7 +781,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                         "(one consumer launch per iteration)"),
            "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
     for name, fn in (("live", live), ("pre_released", pre_released),
-                     ("live_host_releases", live_host), ("live_release_after", live_after)):
+                     ("live_host_releases", live_host)):
         for i in range(30):
             fn(i)
         torch.cuda.synchronize()
@@ -813,7 +805,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     for q in queues + hqueues:
         q.status(live_s)
     ok = True
-    for fn in (live, live_host, live_after):
+    for fn in (live, live_host):
         for i, (w, out) in enumerate(data):
             out.zero_()
             torch.cuda.synchronize()

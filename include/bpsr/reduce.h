@@ -224,14 +224,6 @@ int byteps_reduce_blockq_destroy(byteps_reduce_blockq* q);
  * launches. */
 int byteps_reduce_blockq_host_releases(byteps_reduce_blockq* q, int on);
 int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int count);
-/* Stream-ordered, without a kernel: blocks [f, f + c) are released once the
- * work queued on `stream` so far has completed — an event recorded there, a
- * library thread waiting for it, then the host release words (host releases
- * must be enabled).  Same ordering guarantee as release_range, no kernel
- * dispatched beside the consumer; the release lands a few microseconds after
- * the stream reaches it. */
-int byteps_reduce_blockq_release_after(byteps_reduce_blockq* q, int first, int count,
-                                       void* stream);
 /* The device's consumer stream (see above); owned by the library. */
 int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream);
 /* Debug (synchronises the device): out = launch epoch, nblocks, the sticky

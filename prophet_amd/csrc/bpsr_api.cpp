@@ -11,12 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <condition_variable>
-#include <deque>
-#include <memory>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "bpsr_internal.h"
@@ -571,60 +567,6 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* p) {
 }
 
 // ------------------------------------------------------------ block queue --
-// Stream-ordered releases without a kernel (byteps_reduce_blockq_release_after):
-// an event recorded on the caller's stream; this thread waits for each event
-// in call order and then stores the blocks' epochs into the host release
-// words, which the launch's helper workgroup forwards.
-struct BlockqEventReleaser {
-  struct Item {
-    hipEvent_t ev;
-    int first;
-    std::vector<uint32_t> eps;  // epoch of each block first, first + 1, ...
-  };
-  uint32_t* words = nullptr;  // the queue's host release words
-  int device = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<Item> items;
-  std::vector<hipEvent_t> pool;  // completed events, reused
-  bool stop = false;
-  std::thread th;
-
-  static void raise(uint32_t* w, uint32_t ep) {
-    uint32_t cur = __atomic_load_n(w, __ATOMIC_ACQUIRE);
-    while ((int32_t)(ep - cur) > 0 &&
-           !__atomic_compare_exchange_n(w, &cur, ep, false, __ATOMIC_RELEASE, __ATOMIC_ACQUIRE)) {
-    }
-  }
-  void run() {
-    (void)hipSetDevice(device);
-    for (;;) {
-      Item it;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return stop || !items.empty(); });
-        if (items.empty()) return;  // stopping and drained
-        it = std::move(items.front());
-        items.pop_front();
-      }
-      (void)hipEventSynchronize(it.ev);  // a failed wait still releases: the launch's
-      for (size_t k = 0; k < it.eps.size(); ++k)  // status reports device errors
-        raise(words + it.first + k, it.eps[k]);
-      std::lock_guard<std::mutex> g(mu);
-      pool.push_back(it.ev);
-    }
-  }
-  ~BlockqEventReleaser() {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      stop = true;
-    }
-    cv.notify_all();
-    if (th.joinable()) th.join();
-    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
-  }
-};
-
 struct byteps_reduce_blockq {
   int device = 0;
   int dtype = 0;
@@ -668,7 +610,6 @@ struct byteps_reduce_blockq {
   uint32_t* hflags = nullptr;
   uint32_t* hflags_dev = nullptr;
   bool host_rel = false;
-  std::unique_ptr<BlockqEventReleaser> er;  // release_after, created on first use
 };
 
 // One consumer stream per device, created on first use, never destroyed:
@@ -705,7 +646,6 @@ static hipError_t blockq_events(byteps_reduce_blockq* q) {
 }
 
 static void blockq_free(byteps_reduce_blockq* q) {
-  q->er.reset();  // waits for the pending stream-ordered host releases
   if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
   if (q->join_ev) (void)hipEventDestroy(q->join_ev);
   if (q->dev_table) (void)hipFree(q->dev_table);
@@ -955,54 +895,6 @@ int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int co
     q->rel_epoch[b] = ep;
     __atomic_store_n(q->hflags + b, ep, __ATOMIC_RELEASE);
   }
-  return BYTEPS_REDUCE_OK;
-}
-
-int byteps_reduce_blockq_release_after(byteps_reduce_blockq* q, int first, int count,
-                                       void* stream) {
-  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
-  if (first < 0 || count < 0 || first > q->nblocks || count > q->nblocks - first)
-    return fail(BYTEPS_REDUCE_EARGS, "blocks [%d, %d+%d) outside [0, %d)", first, first, count,
-                q->nblocks);
-  hipStream_t s = to_stream(stream);
-  std::lock_guard<std::mutex> g(q->mu);
-  if (!q->host_rel)
-    return fail(BYTEPS_REDUCE_EARGS, "host releases not enabled (byteps_reduce_blockq_host_releases)");
-  if (!q->er) {
-    auto er = std::make_unique<BlockqEventReleaser>();
-    er->words = q->hflags;
-    er->device = q->device;
-    try {
-      er->th = std::thread([p = er.get()] { p->run(); });
-    } catch (...) {
-      return fail(BYTEPS_REDUCE_EARGS, "cannot start the release thread");
-    }
-    q->er = std::move(er);
-  }
-  BlockqEventReleaser& er = *q->er;
-  hipEvent_t ev = nullptr;
-  {
-    std::lock_guard<std::mutex> eg(er.mu);
-    if (!er.pool.empty()) {
-      ev = er.pool.back();
-      er.pool.pop_back();
-    }
-  }
-  hipError_t e = ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventRecord(ev, s);
-  if (e != hipSuccess) {
-    if (ev) (void)hipEventDestroy(ev);
-    return hip_fail(e, "release event");
-  }
-  BlockqEventReleaser::Item it;
-  it.ev = ev;
-  it.first = first;
-  for (int b = first; b < first + count; ++b) it.eps.push_back(++q->rel_epoch[b]);
-  {
-    std::lock_guard<std::mutex> eg(er.mu);
-    er.items.push_back(std::move(it));
-  }
-  er.cv.notify_one();
   return BYTEPS_REDUCE_OK;
 }
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
     "byteps_reduce_blockq_debug", "byteps_reduce_blockq_stream",
     "byteps_reduce_blockq_release_range", "byteps_reduce_blockq_host_releases",
-    "byteps_reduce_blockq_release_host", "byteps_reduce_blockq_release_after",
+    "byteps_reduce_blockq_release_host",
 )
 
 
@@ -107,7 +107,6 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_status.argtypes = [_vp, _vp]
     L.byteps_reduce_blockq_host_releases.argtypes = [_vp, _int]
     L.byteps_reduce_blockq_release_host.argtypes = [_vp, _int, _int]
-    L.byteps_reduce_blockq_release_after.argtypes = [_vp, _int, _int, _vp]
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     L.byteps_reduce_blockq_debug.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint32), _int]
     L.byteps_reduce_blockq_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
@@ -310,13 +309,6 @@ class BlockQueue:
         """Release blocks [first, first + count) from the host: no stream, no
         kernel.  Their data must already be complete and visible to the device."""
         _check(self.lib.byteps_reduce_blockq_release_host(self.handle, int(first), int(count)))
-
-    def release_after(self, first: int, count: int = 1, stream=None) -> None:
-        """Release blocks [first, first + count) once the work queued on
-        ``stream`` so far has completed, without a kernel (event + library
-        thread + host release words; host releases must be enabled)."""
-        _check(self.lib.byteps_reduce_blockq_release_after(self.handle, int(first), int(count),
-                                                           _stream_of(self.first, stream)))
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))

@@ -491,36 +491,3 @@ def test_host_releases_rules(red, dev):
     q.host_releases(False)
     q.config(wg_per_cu=1)
     q.close()
-
-
-def test_release_after_dma_is_stream_ordered(red, dev):
-    """byteps_reduce_blockq_release_after: each block's pushes land by H2D DMA
-    on a side stream after the launch, and the block is released behind them
-    through an event and the host words (no kernel); exact over 3 epochs,
-    mixed with a kernel release and a host release in the last one."""
-    dt = DType.FLOAT16
-    tab = Table(dev, dt, MIXED)
-    q = red.make_blockq(tab.blocks, dt)
-    q.host_releases(True)
-    s = torch.cuda.Stream()
-    flat = 0
-    for it in range(3):
-        pushes, wants = tab.host_inputs(700 + it)
-        torch.cuda.synchronize()
-        q.launch()
-        flat = 0
-        for b, blk in enumerate(tab.blocks):
-            with torch.cuda.stream(s):
-                for (dst, srcs, L) in blk:
-                    for s_, p in zip(srcs, pushes[flat]):
-                        if L:
-                            s_.copy_(p, non_blocking=True)
-                    flat += 1
-            if it == 2 and b == 1:
-                q.release_range(b, 1, s)          # a kernel release in between
-            else:
-                q.release_after(b, 1, s)
-        q.status()
-        torch.cuda.synchronize()
-        tab.check(wants)
-    q.close()
