@@ -598,12 +598,6 @@ struct byteps_reduce_blockq {
   // pooled high- and normal-priority streams shared one for some pool
   // indices, tools/pushloop_diag.py).
   bool own_queue = true;
-  // BPSR_BQ_RELEASE=copy (measurement only): releases as 4-byte H2D copies of
-  // the epoch from a pinned ring (copy engine, no kernel) instead of the
-  // one-wave release kernel.  Plain stores: epochs must arrive in order.
-  bool release_by_copy = false;
-  uint32_t* rel_src = nullptr;  // pinned [kRelRing][nblocks]
-  static constexpr int kRelRing = 16;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   // Host releases (byteps_reduce_blockq_host_releases): pinned, coherent
   // words the host writes and the launch's helper workgroup forwards.
@@ -652,7 +646,6 @@ static void blockq_free(byteps_reduce_blockq* q) {
   if (q->flags) (void)hipFree(q->flags);
   if (q->ctl) (void)hipFree(q->ctl);
   if (q->host_err) (void)hipHostFree(q->host_err);
-  if (q->rel_src) (void)hipHostFree(q->rel_src);
   if (q->hflags) (void)hipHostFree(q->hflags);
   delete q;
 }
@@ -721,10 +714,6 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
   if (e == hipSuccess) e = hipDeviceSynchronize();  // words zeroed before any stream uses them
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&q->host_err), sizeof(uint32_t));
-  if (const char* v = getenv("BPSR_BQ_RELEASE")) q->release_by_copy = std::string(v) == "copy";
-  if (e == hipSuccess && q->release_by_copy)
-    e = hipHostMalloc(reinterpret_cast<void**>(&q->rel_src),
-                      sizeof(uint32_t) * (size_t)nblocks * byteps_reduce_blockq::kRelRing);
   if (e != hipSuccess) {
     blockq_free(q);
     return hip_fail(e, "block queue setup");
@@ -826,22 +815,15 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
   // at different epochs (a block released ahead) goes out as one kernel per
   // run of equal epochs.  A one-wave kernel raises the words at system scope:
   // a hipMemset node was not seen by the consumer's polls under graph replay,
-  // and hipStreamWriteValue32 measured slower for per-block releases.
+  // and hipStreamWriteValue32, copy-engine copies, host functions and events
+  // measured no better for per-block releases.
   int b = first;
   const int end = first + count;
   while (b < end) {
     const uint32_t ep = q->rel_epoch[b] + 1;
     int run = b + 1;
     while (run < end && q->rel_epoch[run] + 1 == ep) ++run;
-    hipError_t e;
-    if (q->release_by_copy) {
-      uint32_t* src = q->rel_src + (size_t)(ep % byteps_reduce_blockq::kRelRing) * q->nblocks;
-      for (int k = b; k < run; ++k) src[k] = ep;
-      e = hipMemcpyAsync(q->flags + b, src + b, sizeof(uint32_t) * (size_t)(run - b),
-                         hipMemcpyHostToDevice, s);
-    } else {
-      e = launch_blockq_release(q->flags, (uint32_t)b, (uint32_t)(run - b), ep, s);
-    }
+    const hipError_t e = launch_blockq_release(q->flags, (uint32_t)b, (uint32_t)(run - b), ep, s);
     if (e != hipSuccess) return hip_fail(e, "block release");
     for (int k = b; k < run; ++k) q->rel_epoch[k] = ep;
     b = run;

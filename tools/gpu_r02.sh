@@ -65,10 +65,6 @@ for s in $STEPS; do
     bqsweep) for v in 1 2 4; do for o in 1 2 3; do
                run bq_v${v}_o${o} 200 env BPSR_BQ_VPT=$v BPSR_BQ_GATE_OCC=$o ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 || exit 1
              done; done ;;
-    bqcopy) run bq_kernel 200 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
-            run bq_copy 200 env BPSR_BQ_RELEASE=copy ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
-            run bq_kernel2 200 ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 &&
-            run bq_copy2 200 env BPSR_BQ_RELEASE=copy ./tools/cfg3_native tools/cfg3_resnet50_table.txt 200 5 ;;
     native) run native 400 python -u -m pytest tests/test_native_gpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     cfg1n) run cfg1_native 300 ./tools/cfg1_native 4 20 ;;
     cfg1memcpy) run cfg1_native_memcpy 300 env BPSR_SERVER_PULL_COPY=memcpy ./tools/cfg1_native 4 20 ;;
