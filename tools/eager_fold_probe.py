@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Measurement tool: the same 8-way fp32 fold timed eagerly (HIP events around
-back-to-back launches on one stream, a spin kernel first) and replayed from a
-hipGraph of the same launches."""
+"""Measurement tool: an 8-way fp32 fold of the given sizes timed eagerly (HIP
+events around 20 back-to-back launches on one stream, a spin kernel first,
+median of 5), from skewed arenas as the bench uses."""
 import json, os, statistics, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -38,21 +38,7 @@ for nbytes in [int(x) for x in sys.argv[1].split(",")]:
         e1.record(st)
         torch.cuda.synchronize()
         eager.append(e0.elapsed_time(e1) * 1e3 / reps)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
-        for i in range(reps):
-            launch(i)
-    graph = []
-    for _ in range(5):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(st):
-            torch.cuda._sleep(2_000_000)
-        e0.record(st)
-        g.replay()
-        e1.record(st)
-        torch.cuda.synchronize()
-        graph.append(e0.elapsed_time(e1) * 1e3 / reps)
-    print(json.dumps({"bytes": nbytes, "eager_us": round(statistics.median(eager), 2),
-                      "graph_us": round(statistics.median(graph), 2)}), flush=True)
-    del g, data
+    print(json.dumps({"bytes": nbytes, "eager_us": round(statistics.median(eager), 2)}),
+          flush=True)
+    del data
     torch.cuda.empty_cache()
