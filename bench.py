@@ -59,6 +59,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 LEAD_CYCLES = 2_000_000  # spin ahead of a timed block (~1 ms of GPU clock)
 GIB = float(1 << 30)
+WATCHDOG_EXIT = 3  # every rank's status when the N > 1 watchdog fires
 METRIC = "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs"
 # --dtype name -> (byteps DataType id, torch dtype name); ids: common.h:52-65 (+ bf16 = 11)
 DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
@@ -153,9 +154,12 @@ def launch_ranks(n: int, argv: list[str], timeout_s: float = 1500.0) -> int:
     rc = 0
     while True:
         codes = [p.poll() for p in procs]
+        # the first rank to fail decides the status (others may then be
+        # terminated by this loop, which must not mask it)
         bad = [c for c in codes if c not in (None, 0)]
         if bad or time.monotonic() > t_end:
             rc = bad[0] if bad else 124
+            print(f"bench launcher: rank status {codes}; exiting {rc}", file=sys.stderr)
             for p in procs:
                 if p.poll() is None:
                     p.terminate()
@@ -467,6 +471,8 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
     import torch.distributed as dist
     from prophet_amd.buckets import vgg16_param_sizes
     from prophet_amd.shard import ShardedReducer
+    if os.environ.get("BPSR_BENCH_TEST_STALL") == "scatter":
+        time.sleep(3600)                # test hook: a collective that never returns
     E = n_elems or sum(vgg16_param_sizes())
     sr = ShardedReducer(E, fold=fold)   # fold=None: the HIP fold (tests inject a CPU one)
     root = 0
@@ -1049,7 +1055,11 @@ def main(argv=None):
         line["device"] = (f"rehearsal: {world} ranks sharing cuda:0 over gloo (HIP fold, "
                           "no RCCL, no scatter leg): NOT a measurement")
 
-    def extra_legs():
+    def extra_legs(state=None):
+        def leg(name):
+            if state is not None:
+                state["leg"] = name
+        leg("scaling_cfg4")
         if not args.no_scaling:
             try:
                 line["scaling_cfg4"] = scaling_leg(dev, world, rank, N, fold_f32,
@@ -1057,6 +1067,7 @@ def main(argv=None):
             except Exception as e:  # report, never hide
                 line["scaling_cfg4"] = {"error": repr(e)}
             if world > 1 and not args.no_scatter:
+                leg("scatter")
                 try:
                     line["scaling_cfg4"]["scatter"] = scatter_leg(
                         dev, world, rank, N, n_elems=args.scaling_elems or None,
@@ -1064,6 +1075,7 @@ def main(argv=None):
                 except Exception as e:  # report, never hide
                     line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
         if world > 1 and not args.no_scatter:
+            leg("local_reduce")
             try:
                 line["local_reduce"] = local_reduce_leg(
                     dev, world, rank, n_elems=args.scaling_elems or None,
@@ -1071,6 +1083,7 @@ def main(argv=None):
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}
         if cuda and not args.no_e2e:
+            leg("e2e_cfg5")
             try:
                 line["e2e_cfg5"] = e2e_leg(dev, world, rank,
                                            bucket_bytes=args.e2e_bucket_mib << 20)
@@ -1078,7 +1091,7 @@ def main(argv=None):
                 line["e2e_cfg5"] = {"error": repr(e)}
 
     if world == 1:
-        extra_legs()
+        extra_legs(None)
         if cuda and args.dtype == "f32" and mode == 0 and not args.no_fp16:
             try:
                 line["fp16"] = fp16_leg(dev, red, N, B, args.steps)
@@ -1097,28 +1110,37 @@ def main(argv=None):
         emit(line)
         return
     # N > 1: the headline line is complete; the config-4 legs run after it
-    # under a watchdog, so a stuck or failing collective can cost only those
-    # fields, never the line.
+    # under a watchdog.  A stuck or failing collective then costs only those
+    # fields, never the line — but the run FAILS: the line carries "error" and
+    # every rank exits non-zero, so a hang on first hardware contact cannot
+    # pass for success (launch_ranks / torch.distributed.run relay the status).
     import threading
     lock = threading.Lock()
-    state = {"printed": False}
+    state = {"printed": False, "leg": "start"}
+    limit_s = float(os.environ.get("BPSR_BENCH_WATCHDOG_S", "240"))
 
-    def emit_and_maybe_exit(exit_now: bool):
+    def emit_and_maybe_exit(exit_code):
         with lock:
             if rank == 0 and not state["printed"]:
                 emit(line)
                 state["printed"] = True
-        if exit_now:
-            os._exit(0)
+        if exit_code is not None:
+            sys.stderr.flush()
+            os._exit(exit_code)
 
-    watchdog = threading.Timer(240.0, lambda: (line.setdefault(
-        "scaling_cfg4", {}).setdefault("error", "timed out after 240 s"),
-        emit_and_maybe_exit(True)))
+    def on_timeout():
+        msg = f"watchdog: leg {state['leg']!r} still running after {limit_s:.0f} s"
+        line["error"] = msg
+        line.setdefault("scaling_cfg4", {}).setdefault("error", msg)
+        print(f"bench rank {rank}: {msg}", file=sys.stderr)
+        emit_and_maybe_exit(WATCHDOG_EXIT)
+
+    watchdog = threading.Timer(limit_s, on_timeout)
     watchdog.daemon = True
     watchdog.start()
-    extra_legs()
-    emit_and_maybe_exit(False)
+    extra_legs(state)
     watchdog.cancel()
+    emit_and_maybe_exit(None)
     dist.destroy_process_group()
 
 

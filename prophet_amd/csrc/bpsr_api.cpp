@@ -392,6 +392,28 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
   return BYTEPS_REDUCE_OK;
 }
 
+int fold_any_alias(void* dst, const void* const* srcs, int n, size_t len, int dtype, int mode,
+                   hipStream_t s) {
+  int alias = -1;
+  for (int k = 0; k < n && srcs; ++k)
+    if (srcs[k] == dst) alias = k;
+  if (alias <= 0) return byteps_reduce_sum_n(dst, srcs, n, len, dtype, mode, s);
+  int rc = check_common(dtype, mode);
+  if (rc) return rc;
+  if (n > kMaxSrcs)
+    return fail(BYTEPS_REDUCE_EARGS, "dst aliases srcs[%d] of a %d-way fold (> %d)", alias, n,
+                kMaxSrcs);
+  if (len == 0) return BYTEPS_REDUCE_OK;
+  for (int k = 0; k < n; ++k) {
+    if (!srcs[k]) return fail(BYTEPS_REDUCE_EARGS, "null srcs[%d]", k);
+    if (overlaps_partially(dst, srcs[k], len))
+      return fail(BYTEPS_REDUCE_EARGS, "dst partially overlaps srcs[%d]", k);
+    if (k != alias && srcs[k] == dst)
+      return fail(BYTEPS_REDUCE_EARGS, "dst aliases two sources");
+  }
+  return fold_once(dst, srcs, n, len, dtype, mode, /*copy_trailing=*/true, s);
+}
+
 }  // namespace bpsr
 
 using namespace bpsr;

@@ -240,6 +240,12 @@ inline int cache_pol(const Tuning& tu, uint64_t bytes_per_src) {
   if (!tu.nt) return kPolPlain;
   return bytes_per_src < tu.wt_max_bytes ? kPolWt : kPolNt;
 }
+// byteps_reduce_sum_n, except that dst may also alias one srcs[k] with k > 0
+// exactly (n <= kMaxSrcs: one launch, every element read before it is
+// written by the same thread) — the in-place owner fold of the shard calls.
+int fold_any_alias(void* dst, const void* const* srcs, int n, size_t len, int dtype, int mode,
+                   hipStream_t s);
+
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s);
 

@@ -1,5 +1,5 @@
 """The C-ABI library loads here (no GPU) and exports exactly what
-include/bpsr/{reduce,server,prophet}.h declare; host-only argument checks run without a GPU."""
+include/bpsr/{reduce,server,prophet,shard}.h declare; host-only argument checks run without a GPU."""
 import ctypes
 import os
 import re
@@ -11,7 +11,8 @@ from prophet_amd import reducer
 from prophet_amd.dtypes import ALL_DTYPES, elem_size
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "bpsr", h) for h in ("reduce.h", "server.h", "prophet.h")]
+HEADERS = [os.path.join(ROOT, "include", "bpsr", h)
+           for h in ("reduce.h", "server.h", "prophet.h", "shard.h")]
 
 
 def header_functions(headers=HEADERS):
@@ -27,7 +28,9 @@ def test_header_declares_expected_api():
     assert header_functions(HEADERS[:1]) == sorted(reducer.EXPORTS)
     assert header_functions(HEADERS[1:2]) == sorted(SERVER_EXPORTS)
     from prophet_amd.prophet import PROPHET_EXPORTS
-    assert header_functions(HEADERS[2:]) == sorted(PROPHET_EXPORTS)
+    assert header_functions(HEADERS[2:3]) == sorted(PROPHET_EXPORTS)
+    from prophet_amd.shard import SHARD_EXPORTS
+    assert header_functions(HEADERS[3:]) == sorted(SHARD_EXPORTS)
 
 
 def test_library_exports_every_header_symbol():
@@ -93,8 +96,9 @@ def test_bucket_desc_layout_matches_header():
 
 
 def test_cpp_wrapper_compiles_with_reference_flags(tmp_path):
-    """include/bpsr/gpu_reducer.hpp + reduce.h under the reference's own
-    compiler settings (g++ -std=c++11 -Wall, setup.py:171), linked to libbpsr.so."""
+    """include/bpsr/gpu_reducer.hpp, gpu_shard.hpp, reduce.h and shard.h under
+    the reference's own compiler settings (g++ -std=c++11 -Wall, setup.py:171),
+    linked to libbpsr.so."""
     exe = tmp_path / "header_check"
     src = os.path.join(ROOT, "tests", "cpp", "header_check.cpp")
     libdir = os.path.dirname(reducer.LIB_PATH)

@@ -78,6 +78,37 @@ def test_torchrun_launch_one_line():
     assert line["scaling_cfg4"]["scatter"]["exact_vs_torch_fold"] is True
 
 
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_stalled_collective_fails_loudly(launcher):
+    """A leg that never returns (test hook: the scatter leg sleeps, as a stuck
+    RCCL call would) trips the watchdog: the headline line still comes out,
+    carrying ``error``, and the run exits NON-zero (every rank exits 3; the
+    self-launcher and torch.distributed.run relay it)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(BPSR_BENCH_TEST_STALL="scatter", BPSR_BENCH_WATCHDOG_S="8")
+    args = [os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2", "--steps", "2",
+            "--warmup", "1", "--workers", "3", "--bucket-mib", "0.0625", "--sets", "2",
+            "--no-cpu-baseline", "--scaling-elems", "10007"]
+    if launcher == "self":
+        cmd = [sys.executable] + args
+    else:
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+               "2", "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert "scatter" in line["error"] and "still running" in line["error"]
+    assert line["n_gpus"] == 2 and line["value"] > 0
+
+
 def test_launcher_failing_rank_fails_the_run():
     env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
