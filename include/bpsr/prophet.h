@@ -194,7 +194,10 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  * create enables host releases on the block queue): for pushes whose bytes are
  * already visible to the device when byteps_prophet_loop_push is called
  * (RDMA into HBM, or copies the caller has waited for); release_stream is then
- * unused. */
+ * unused.  Otherwise, with the loop thread, release_stream must not be NULL
+ * (EARGS): NULL would mean the LOOP thread's per-thread stream, which no copy
+ * the caller queued on its own stream is ordered before.  Inline, NULL is the
+ * pushing thread's per-thread stream. */
 enum { BYTEPS_PROPHET_LOOP_INLINE = 1, BYTEPS_PROPHET_LOOP_HOST_RELEASE = 2 };
 typedef struct byteps_prophet_loop byteps_prophet_loop;
 int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* bq,

@@ -49,7 +49,8 @@
 extern "C" {
 #endif
 
-#define BYTEPS_REDUCE_ABI_VERSION 2
+/* 3: byteps_server_config.engine_blocking; bpsr/shard.h */
+#define BYTEPS_REDUCE_ABI_VERSION 3
 
 /* Data type ids: byteps/common/common.h:52-65 (mshadow order), plus bf16 as a
  * build extension (the reference has none). */

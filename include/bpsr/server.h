@@ -54,6 +54,13 @@ typedef struct byteps_server_config {
                           by (fewest counted pushes on the key, oldest) —
                           queue.h:68-97 — one at a time; 0 = FIFO, issued at
                           arrival (the reference default)                    */
+  int engine_blocking; /* BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:324): every
+                          push returns only once the work it issued (copy,
+                          sum, fold) has completed, and every pull is answered
+                          at once from the store as it stands — no round gating,
+                          no pull counting (server.cc:284-285); a pull issued
+                          before the round's last push sees the previous
+                          round, as in the reference.  0 = the default engine */
 } byteps_server_config;
 
 typedef struct byteps_server byteps_server;
@@ -62,7 +69,7 @@ typedef struct byteps_server byteps_server;
  * them: DMLC_NUM_WORKER, BYTEPS_SERVER_ENGINE_THREAD, BYTEPS_ENABLE_ASYNC
  * (here "1" means asynchronous; the reference reads the flag inverted,
  * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
- * BYTEPS_SERVER_ENABLE_SCHEDULE, device 0. */
+ * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
@@ -179,6 +186,85 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
  * go to log_keys (up to max_log) and their count to *n_log. */
 int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* log_keys,
                              int max_log, int* n_log);
+
+/* ------------------------------------------------------------------------
+ * Key space sharded over several server instances (one per GPU of a node):
+ * the counterpart of the reference's key -> server assignment
+ * (BytePSGlobal::EncodeDefaultKey, global.cc:530-567) inside ONE process
+ * that owns the node's GPUs.  Each instance is a byteps_server (its own
+ * lanes, slots and store on its own device); the group routes every call.
+ *
+ * Split policies:
+ *   BYTEPS_SERVER_SPLIT_HASH   whole keys, instance = hash(key) % instances
+ *       with the reference's BYTEPS_KEY_HASH_FN (djb2 default; naive, sdbm,
+ *       built_in x BYTEPS_BUILT_IN_HASH_COEF) — the reference's own rule, the
+ *       same arithmetic (each key's round is one left fold in arrival order);
+ *   BYTEPS_SERVER_SPLIT_RANGE  every key of at least split_min_bytes is cut
+ *       into one contiguous piece per instance — the owner ranges of the
+ *       reduce-scatter split (core_loops.cc:210-211) in 128-byte units, the
+ *       tail to the last instance — so each GPU owns a contiguous slice of
+ *       every large partition; smaller keys go whole by hash.  Piece starts
+ *       are multiples of 128 B (of 8 elements for every dtype), so the fp16
+ *       body/tail rule of cpu_reducer.cc:103,118 holds piece by piece.  Each
+ *       piece is a strict left fold in the arrival order ITS instance saw; when
+ *       workers race, a key's pieces may fold in different orders (the
+ *       reference has one order per key, since one server holds it).
+ * Pushes scatter the pieces (each instance copies its piece into its own
+ * HBM); pulls gather them back into the caller's buffer.  All calls are
+ * thread-safe like the single-instance ones and block like them. */
+enum byteps_server_split { BYTEPS_SERVER_SPLIT_HASH = 0, BYTEPS_SERVER_SPLIT_RANGE = 1 };
+/* BYTEPS_KEY_HASH_FN values (global.cc:541-554). */
+enum byteps_key_hash { BYTEPS_KEY_HASH_DJB2 = 0, BYTEPS_KEY_HASH_NAIVE = 1,
+                       BYTEPS_KEY_HASH_SDBM = 2, BYTEPS_KEY_HASH_BUILT_IN = 3 };
+
+typedef struct byteps_server_group_config {
+  byteps_server_config server; /* every instance's config (.device is ignored)  */
+  int num_servers;             /* instances (>= 1)                              */
+  int devices[16];             /* device of instance i (may repeat)             */
+  int split;                   /* byteps_server_split                           */
+  int hash_fn;                 /* byteps_key_hash                               */
+  uint32_t hash_coef;          /* built_in multiplier (BYTEPS_BUILT_IN_HASH_COEF) */
+  size_t split_min_bytes;      /* RANGE: smaller keys go whole (0 = 128 * n)    */
+} byteps_server_group_config;
+
+#define BYTEPS_SERVER_GROUP_MAX 16
+
+/* The reference's key hash (global.cc:491-523) of `key` under `fn`. */
+uint64_t byteps_server_key_hash(uint64_t key, int fn, uint32_t coef);
+
+/* Defaults from the environment: the server config (byteps_server_config_from_env),
+ * num_servers and devices 0..n-1 from BPSR_SERVER_GPUS (default 1), split from
+ * BPSR_SERVER_SPLIT (hash|range), BYTEPS_KEY_HASH_FN, BYTEPS_BUILT_IN_HASH_COEF,
+ * BPSR_SERVER_SPLIT_MIN_BYTES.  An unknown hash name is EARGS (the reference
+ * aborts, global.cc:555-557). */
+int byteps_server_group_config_from_env(byteps_server_group_config* cfg);
+
+typedef struct byteps_server_group byteps_server_group;
+int byteps_server_group_create(const byteps_server_group_config* cfg, byteps_server_group** out);
+int byteps_server_group_destroy(byteps_server_group* g);
+/* Pieces of a key of `len` bytes: for i < *npieces (<= cap), piece i of bytes
+ * [offset[i], offset[i] + plen[i]) lives on instance server[i].  The rule is a
+ * pure function of the config (byteps_server_route: what a worker-side
+ * transport needs to address the instances, like EncodeDefaultKey). */
+int byteps_server_route(const byteps_server_group_config* cfg, uint64_t key, size_t len,
+                        int* npieces, int* server, size_t* offset, size_t* plen, int cap);
+int byteps_server_group_route(byteps_server_group* g, uint64_t key, size_t len, int* npieces,
+                              int* server, size_t* offset, size_t* plen, int cap);
+/* Instance i (for its zero-copy / view calls on routed pieces). */
+int byteps_server_group_instance(byteps_server_group* g, int i, byteps_server** s);
+int byteps_server_group_init_key(byteps_server_group* g, uint64_t key, size_t len, int dtype);
+/* byteps_server_push / _pull over the pieces (the pieces' copies run
+ * concurrently; the call returns when all are done). */
+int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, const void* data,
+                             size_t len, int dtype, int location);
+int byteps_server_group_pull(byteps_server_group* g, uint64_t key, void* out, size_t len,
+                             int location);
+/* byteps_server_push_many / _pull_many: keys routed, one batched call per instance. */
+int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
+                                  const void* const* datas, const size_t* lens, int n, int worker,
+                                  int dtype, int location);
+int byteps_server_group_pull_many(byteps_server_group* g, const uint64_t* keys,
+                                  void* const* outs, const size_t* lens, int n, int location);
 
 #ifdef __cplusplus
 }

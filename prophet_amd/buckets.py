@@ -16,6 +16,7 @@ operations.cc:237-247 (``(declared_key << 16) + i``).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 DEFAULT_PARTITION_BYTES = 4_096_000           # global.cc:42
@@ -82,6 +83,29 @@ def partition_bound(partition_bytes: int = DEFAULT_PARTITION_BYTES, local_size: 
     """global.cc:128-135: AlignTo(bytes, 8*local_size) rounds down."""
     a = 8 * local_size
     return partition_bytes // a * a
+
+
+def _atoi(text: str) -> int:
+    """C atoi: leading whitespace, optional sign, digits; 0 if none."""
+    t = text.lstrip()
+    i = 1 if t[:1] in ("+", "-") else 0
+    j = i
+    while j < len(t) and t[j].isdigit():
+        j += 1
+    return int(t[:j]) if j > i else 0
+
+
+def partition_bytes_from_env(env=None) -> int:
+    """BYTEPS_PARTITION_BYTES as global.cc:128-130 reads it (atoi), else the
+    4,096,000 default (global.cc:42)."""
+    v = (os.environ if env is None else env).get("BYTEPS_PARTITION_BYTES")
+    return _atoi(v) if v is not None else DEFAULT_PARTITION_BYTES
+
+
+def local_size_from_env(env=None) -> int:
+    """BYTEPS_LOCAL_SIZE (communicator.cc:71-77, atoi), else 1."""
+    v = (os.environ if env is None else env).get("BYTEPS_LOCAL_SIZE")
+    return _atoi(v) if v is not None else 1
 
 
 @dataclass(frozen=True)

@@ -761,6 +761,12 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   const uint32_t epoch = q->launch_epoch + 1;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+    // Host releases write only the pinned words; the helper workgroup that
+    // forwards them is left out of a captured launch, so such a launch would
+    // wait for its timeout on every replay.
+    if (q->host_rel)
+      return fail(BYTEPS_REDUCE_EARGS, "captured block-queue launch with host releases on "
+                                       "(byteps_reduce_blockq_host_releases(q, 0) first)");
     // A captured launch keeps this epoch in every replay: only iterations
     // whose releases are captured before it (same graph, stream order) replay
     // correctly, so that is what a capture must hold.

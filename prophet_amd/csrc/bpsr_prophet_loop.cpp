@@ -151,6 +151,11 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
   if (!pq || !bq || !block_of || !out || nhandles < 0 || nblocks < 1)
     return bpsr::fail(BYTEPS_REDUCE_EARGS, "null argument, nhandles < 0 or nblocks < 1");
   *out = nullptr;
+  if (!release_stream && !(flags & BYTEPS_PROPHET_LOOP_INLINE) &&
+      !(flags & BYTEPS_PROPHET_LOOP_HOST_RELEASE))
+    return bpsr::fail(BYTEPS_REDUCE_EARGS,
+                      "loop thread with stream releases needs a release_stream (NULL would be "
+                      "the loop thread's own per-thread stream, unordered with the pushes' copies)");
   auto* l = new (std::nothrow) byteps_prophet_loop;
   if (!l) return bpsr::fail(BYTEPS_REDUCE_EARGS, "out of memory");
   l->pq = pq;

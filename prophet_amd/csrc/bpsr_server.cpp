@@ -141,6 +141,7 @@ struct KeyState {
 struct byteps_server {
   byteps_server_config cfg;
   bool schedule = false;
+  bool blocking = false;  // BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:324)
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
@@ -152,6 +153,11 @@ struct byteps_server {
   std::deque<bpsr::Response> rq;
   bool rq_stop = false;
   std::thread responder;
+  // Fault injection for tests (BPSR_SERVER_FAIL_AFTER=n): the (n+1)-th fold
+  // issue (init copy or engine job) and every later one fail as a failed
+  // kernel launch would.  -1 = off.
+  long fail_after = -1;
+  std::atomic<long> issued{0};
 };
 
 namespace bpsr {
@@ -325,10 +331,18 @@ void respond_later(byteps_server* s, KeyState* ks, byteps_server_pull_cb cb, voi
   enqueue_response(s, r);
 }
 
+// May a pull of the key be answered now?  Sync mode: once the round's push
+// is finished (server.cc:293-304).  Engine blocking mode answers every pull at
+// once from the store as it stands (server.cc:284-285 SendPullResponse with
+// no gating), as does async mode.
+bool pull_ready(const byteps_server* s, const KeyState* ks) {
+  return s->blocking || ks->push_finished || ks->error;
+}
+
 // Count one answered pull; after NumWorkers the key re-arms (server.cc:105-113).
 // Caller holds ks->mu.
 void count_pull(byteps_server* s, KeyState* ks) {
-  if (s->cfg.async_mode) return;
+  if (s->cfg.async_mode || s->blocking) return;  // nothing gates on the count
   if (++ks->pull_cnt == s->cfg.num_workers) {
     ks->push_finished = false;
     ks->pull_cnt = 0;
@@ -421,10 +435,17 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
   return 0;
 }
 
+int injected_failure(byteps_server* s) {
+  if (s->fail_after < 0 || s->issued.fetch_add(1) < s->fail_after) return 0;
+  return fail(BYTEPS_REDUCE_EHIP, "injected fold failure (BPSR_SERVER_FAIL_AFTER=%ld)",
+              s->fail_after);
+}
+
 // Issue a job's kernels on the lane's fold stream and apply its state
 // changes — the body of the engine thread (server.cc:70-145).  Caller holds
 // ks->mu.
 int execute(byteps_server* s, const FoldJob& j) {
+  if (int rc = injected_failure(s)) return rc;
   KeyState* ks = j.ks;
   Lane& L = *s->lanes[ks->lane];
   void* fs = reinterpret_cast<void*>(L.fold);
@@ -470,7 +491,14 @@ int execute(byteps_server* s, const FoldJob& j) {
 // build issues them to the lane's stream in arrival order), or queue it for
 // the lane's dispatcher (scheduling on).  Caller holds ks->mu.
 int submit(byteps_server* s, KeyState* ks, FoldJob&& j) {
-  if (!s->schedule) return execute(s, j);
+  if (!s->schedule) {
+    // The arrival is already recorded: a fold that cannot be issued must
+    // fail the key, or every other worker's push / pull of it waits forever
+    // (the dispatcher and flush_folds do the same for their jobs).
+    const int rc = execute(s, j);
+    if (rc) fail_key(s, ks, rc);
+    return rc;
+  }
   ks->pending++;
   s->lanes[ks->lane]->q->push(ks->key, std::move(j));
   return 0;
@@ -520,13 +548,22 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d sent two init pushes", w);
     ks->got[w] = 1;
     if (++ks->init_count < N) return 0;
-    hipError_t we = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
-    if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
-    int rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, reinterpret_cast<void*>(L.fold));
-    if (rc) return rc;
-    hipError_t e = hipEventRecord(ks->done, L.fold);
-    if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
-    if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+    // every init push is counted: a failure from here on fails the key (the
+    // other workers' init pushes wait for `inited || error`)
+    int rc = injected_failure(s);
+    hipError_t we = rc ? hipSuccess : hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+    if (!rc && we != hipSuccess) rc = hip_fail(we, "hipStreamWaitEvent");
+    if (!rc)
+      rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, reinterpret_cast<void*>(L.fold));
+    if (!rc) {
+      hipError_t e = hipEventRecord(ks->done, L.fold);
+      if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
+      if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+    }
+    if (rc) {
+      fail_key(s, ks, rc);
+      return rc;
+    }
     ks->fold_ev = ks->done;
     ks->has_done = true;
     ks->inited = true;
@@ -636,6 +673,16 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
   return first_rc;
 }
 
+// Engine blocking mode (server.cc:205-262): the handler did the copy / sum
+// itself before answering the push, so the push returns once the work it
+// issued on the key's lane has completed.
+int finish_blocking(byteps_server* s, KeyState* ks, std::unique_lock<std::mutex>& lk) {
+  hipStream_t fs = s->lanes[ks->lane]->fold;
+  lk.unlock();
+  hipError_t e = hipStreamSynchronize(fs);
+  return e == hipSuccess ? 0 : hip_fail(e, "engine blocking: fold sync");
+}
+
 // Init pushes block until every worker's init push has arrived and the store
 // is initialised: the reference answers them only then (server.cc:184-198).
 int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock<std::mutex>& lk) {
@@ -703,6 +750,8 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   cfg->device = 0;
   const char* sc = getenv("BYTEPS_SERVER_ENABLE_SCHEDULE");  // server.cc:335
   cfg->enable_schedule = (sc && atoi(sc) != 0) ? 1 : 0;
+  const char* eb = getenv("BYTEPS_SERVER_ENGINE_BLOCKING");  // server.cc:324
+  cfg->engine_blocking = (eb && atoi(eb) != 0) ? 1 : 0;
   return BYTEPS_REDUCE_OK;
 }
 
@@ -717,6 +766,8 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   auto s = std::make_unique<byteps_server>();
   s->cfg = *cfg;
   s->schedule = cfg->enable_schedule != 0;
+  s->blocking = cfg->engine_blocking != 0;
+  if (const char* fa = getenv("BPSR_SERVER_FAIL_AFTER")) s->fail_after = atol(fa);
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
@@ -844,7 +895,8 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
-  return arrive_and_wait_init(s, ks, worker, lk);
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk))) return rc;
+  return s->blocking ? finish_blocking(s, ks, lk) : 0;
 }
 
 int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
@@ -912,7 +964,8 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
   std::unique_lock<std::mutex> lk(ks->mu);
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-  return arrive_and_wait_init(s, ks, worker, lk);
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk))) return rc;
+  return s->blocking ? finish_blocking(s, ks, lk) : 0;
 }
 
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location) {
@@ -923,7 +976,7 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (!ks) return BYTEPS_REDUCE_EARGS;
   std::unique_lock<std::mutex> lk(ks->mu);
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
-  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
   // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
@@ -947,13 +1000,14 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   // this copy, so none lands mid-copy.  (Sync mode: the store cannot change
   // while the pull is outstanding — the next round needs this worker's next
   // push, which follows the pull.)
-  if (e == hipSuccess && s->cfg.async_mode) e = hipStreamWaitEvent(L.fold, ks->pulled, 0);
+  if (e == hipSuccess && (s->cfg.async_mode || s->blocking))
+    e = hipStreamWaitEvent(L.fold, ks->pulled, 0);
   if (e != hipSuccess) return hip_fail(e, "pull copy");
   hipEvent_t ev = ks->pulled;  // a later pull may re-record it: it then covers this copy too
   lk.unlock();
   e = hipEventSynchronize(ev);
   if (e != hipSuccess) return hip_fail(e, "pull copy");
-  if (s->cfg.async_mode) return BYTEPS_REDUCE_OK;
+  if (s->cfg.async_mode || s->blocking) return BYTEPS_REDUCE_OK;
   lk.lock();
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   return BYTEPS_REDUCE_OK;
@@ -969,7 +1023,7 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   KeyState* ks = key_for_pull(s, key);
   if (!ks) return BYTEPS_REDUCE_EARGS;
   std::unique_lock<std::mutex> lk(ks->mu);
-  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
   if ((rc = ensure_mirror(s, ks, !s->cfg.async_mode))) return rc;
   size_t idx = ks->rounds & 1;
@@ -1003,7 +1057,7 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   KeyState* ks = key_for_pull(s, key);
   if (!ks) return BYTEPS_REDUCE_EARGS;
   std::unique_lock<std::mutex> lk(ks->mu);
-  ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+  ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
   // The round is published only after its fold (or the lane's batch mark
   // behind it) was recorded, so this event covers the store's last write.
@@ -1038,8 +1092,9 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
     respond_later(s, ks, cb, ctx, ks->mirror[idx], 0);
     return BYTEPS_REDUCE_OK;
   }
-  if ((rc = ensure_mirror(s, ks, ks->push_finished))) return rc;
-  if (ks->push_finished)  // server.cc:293-301: push already finished
+  const bool now = s->blocking || ks->push_finished;
+  if ((rc = ensure_mirror(s, ks, now))) return rc;
+  if (now)  // server.cc:293-301: push already finished (blocking mode: always)
     respond_later(s, ks, cb, ctx, ks->mirror[ks->rounds & 1], 0);
   else                    // server.cc:303-304: queued until the round finishes
     ks->waiting.push_back({cb, ctx});
@@ -1178,6 +1233,12 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     }
   }
   if ((rc = flush_folds(s, defer))) return rc;
+  if (s->blocking)  // engine blocking mode: the folds issued above have completed
+    for (size_t l = 0; l < by_lane.size(); ++l)
+      if (!by_lane[l].empty()) {
+        hipError_t e = hipStreamSynchronize(s->lanes[l]->fold);
+        if (e != hipSuccess) return hip_fail(e, "engine blocking: fold sync");
+      }
   // 3. blocking contract: every source may be reused once the call returns
   //    (a lane's copy mark, re-recorded since, covers this call's copies too)
   for (size_t l = 0; l < by_lane.size(); ++l) {
@@ -1256,7 +1317,7 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
       return fail(BYTEPS_REDUCE_EARGS, "pull %d: bad buffer or %zu bytes > key len %zu", i,
                   lens[i], ks->len);
     }
-    if (!(ks->push_finished || ks->error)) {
+    if (!pull_ready(s, ks)) {
       lk.unlock();
       // let enough ready bytes go while this round finishes; fewer, larger
       // batched copies otherwise (rounds often complete together)
@@ -1265,7 +1326,7 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
         ready_bytes = 0;
       }
       lk.lock();
-      ks->cv.wait(lk, [&] { return ks->push_finished || ks->error; });
+      ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
     }
     if (ks->error) {
       lk.unlock();

@@ -208,7 +208,13 @@ class PushLoop:
                  inline: bool = False, host_release: bool = False):
         """``host_release=True``: complete blocks are released from the host
         (``BlockQueue.release_host``, no stream work) — for pushes whose bytes
-        are already visible to the device when ``push`` is called."""
+        are already visible to the device when ``push`` is called.  Otherwise
+        the loop thread (``inline=False``) needs ``release_stream``: the stream
+        the pushes' copies are queued on (None is refused — the library would
+        read it as the loop thread's own per-thread stream)."""
+        if release_stream is None and not inline and not host_release:
+            raise ValueError("PushLoop: release_stream is required with the loop thread and "
+                             "stream releases (the stream the pushes' copies are queued on)")
         self._L = _lib()
         self.queue, self.blockq = queue, blockq
         bo = (ctypes.c_int32 * max(len(block_of), 1))(*block_of)
@@ -332,13 +338,23 @@ def release_groups(queue: ProphetPushQueue, arrivals, finish_immediately: bool =
     rel = (_Task * max(n, 1))()
     starts = (ctypes.c_int32 * (n + 1))()
     phases = (ctypes.c_int32 * max(n, 1))()
+    unset = (1 << 64) - 1
+    for i in range(n):
+        rel[i].handle = unset
     ng = queue._L.byteps_prophet_release_groups(
         queue._h, arr, n, int(finish_immediately), int(with_phase), int(max_idle),
         rel, starts, phases)
     if ng < 0:
+        # The native queue keeps what it accepted and did not release (e.g.
+        # "no progress"): those handles stay live for later get_task() polls.
+        # Released ones (written to rel) and — when the queue holds nothing,
+        # as after a refused arrival — every handle of this call are dropped.
+        held = queue.pending() > 0
         with queue._lock:
+            released = {rel[i].handle for i in range(n) if rel[i].handle != unset}
             for c in arr[:n]:
-                queue._live.pop(c.handle, None)
+                if c.handle in released or not held:
+                    queue._live.pop(c.handle, None)
         _ck(ng)
     groups = []
     with queue._lock:

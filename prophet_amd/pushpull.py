@@ -31,7 +31,8 @@ from __future__ import annotations
 import threading
 from dataclasses import dataclass, field
 
-from .buckets import DEFAULT_PARTITION_BYTES, cantor_command, depair_command, partition_bound
+from .buckets import (DEFAULT_PARTITION_BYTES, cantor_command, depair_command,
+                      local_size_from_env, partition_bound, partition_bytes_from_env)
 from .dtypes import DType, elem_size
 
 K_DEFAULT_PUSH_PULL = 0     # RequestType::kDefaultPushPull (common.h:68-71)
@@ -73,12 +74,23 @@ class Worker:
     """One BytePS worker (its root device) talking to the server front end."""
 
     def __init__(self, rank: int, frontend: ServerFrontend,
-                 partition_bytes: int = DEFAULT_PARTITION_BYTES, local_size: int = 1):
+                 partition_bytes: int | None = None, local_size: int | None = None):
+        """``partition_bytes`` / ``local_size`` default to the reference's
+        environment: BYTEPS_PARTITION_BYTES (global.cc:128-130, else 4,096,000)
+        and BYTEPS_LOCAL_SIZE (communicator.cc:71-77, else 1); the bound is
+        AlignTo(partition_bytes, 8 * local_size), rounded down (global.cc:135)."""
         self.rank = rank
         self.frontend = frontend
+        if partition_bytes is None:
+            partition_bytes = partition_bytes_from_env()
+        if local_size is None:
+            local_size = local_size_from_env()
+        if local_size < 1:
+            raise ValueError("local_size must be >= 1")
         self.bound = partition_bound(partition_bytes, local_size)
         if self.bound <= 0:
-            raise ValueError("partition bound must be positive")
+            raise ValueError(f"partition bound must be positive (BYTEPS_PARTITION_BYTES="
+                             f"{partition_bytes}, local_size={local_size})")
         self.contexts: dict[str, Context] = {}
         self._declared: list[str] = []
         self._pool = None

@@ -24,7 +24,14 @@ SERVER_EXPORTS = (
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
     "byteps_server_debug_lane", "byteps_server_push_ready_many", "byteps_server_push_many",
     "byteps_server_pull_many", "byteps_server_pull_device_view",
+    "byteps_server_key_hash", "byteps_server_group_config_from_env", "byteps_server_route",
+    "byteps_server_group_create", "byteps_server_group_destroy", "byteps_server_group_route",
+    "byteps_server_group_instance", "byteps_server_group_init_key", "byteps_server_group_push",
+    "byteps_server_group_pull", "byteps_server_group_push_many", "byteps_server_group_pull_many",
 )
+SPLIT_HASH, SPLIT_RANGE = 0, 1
+HASH_FNS = {"djb2": 0, "naive": 1, "sdbm": 2, "built_in": 3}
+GROUP_MAX = 16
 
 _vp, _sz, _int, _u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
 # void cb(void* ctx, uint64_t key, const void* data, size_t len, int status)
@@ -35,12 +42,36 @@ PUSH_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _int, _int)
 
 class ServerConfig(ctypes.Structure):
     _fields_ = [("num_workers", _int), ("engine_lanes", _int), ("policy", _int),
-                ("async_mode", _int), ("device", _int), ("enable_schedule", _int)]
+                ("async_mode", _int), ("device", _int), ("enable_schedule", _int),
+                ("engine_blocking", _int)]
+
+
+class GroupConfig(ctypes.Structure):
+    _fields_ = [("server", ServerConfig), ("num_servers", _int), ("devices", _int * 16),
+                ("split", _int), ("hash_fn", _int), ("hash_coef", ctypes.c_uint32),
+                ("split_min_bytes", _sz)]
 
 
 def _lib():
     L = load_library()
     if not getattr(L, "_server_bound", False):
+        P = ctypes.POINTER
+        L.byteps_server_key_hash.argtypes = [_u64, _int, ctypes.c_uint32]
+        L.byteps_server_key_hash.restype = _u64
+        L.byteps_server_group_config_from_env.argtypes = [P(GroupConfig)]
+        L.byteps_server_group_create.argtypes = [P(GroupConfig), P(_vp)]
+        L.byteps_server_group_destroy.argtypes = [_vp]
+        L.byteps_server_group_route.argtypes = [_vp, _u64, _sz, P(_int), P(_int), P(_sz), P(_sz),
+                                                _int]
+        L.byteps_server_route.argtypes = [P(GroupConfig), _u64, _sz, P(_int), P(_int), P(_sz),
+                                          P(_sz), _int]
+        L.byteps_server_group_instance.argtypes = [_vp, _int, P(_vp)]
+        L.byteps_server_group_init_key.argtypes = [_vp, _u64, _sz, _int]
+        L.byteps_server_group_push.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int]
+        L.byteps_server_group_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
+        L.byteps_server_group_push_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int, _int,
+                                                    _int]
+        L.byteps_server_group_pull_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int]
         L.byteps_server_config_from_env.argtypes = [ctypes.POINTER(ServerConfig)]
         L.byteps_server_create.argtypes = [ctypes.POINTER(ServerConfig), ctypes.POINTER(_vp)]
         L.byteps_server_destroy.argtypes = [_vp]
@@ -69,23 +100,77 @@ def _lib():
     return L
 
 
-def _buf(x):
+def _buf(x, sync: bool = True):
     """(pointer, nbytes, location) of a numpy array or torch tensor."""
     if isinstance(x, np.ndarray):
         assert x.flags["C_CONTIGUOUS"]
         return x.ctypes.data, x.nbytes, HOST
     if hasattr(x, "data_ptr"):
         loc = DEVICE if x.device.type == "cuda" else HOST
-        if loc == DEVICE:
-            # The server copies on streams of its own: whatever torch queued
-            # for this tensor on the calling thread's current stream (the
-            # kernel that produced a push, a fill of a pull's destination)
-            # must be done first.  Work on other torch streams is the
-            # caller's to order.
-            import torch
-            torch.cuda.current_stream(x.device).synchronize()
+        if loc == DEVICE and sync:
+            _sync_producers([x])
         return int(x.data_ptr()), x.numel() * x.element_size(), loc
     raise TypeError(f"unsupported buffer {type(x)!r}")
+
+
+def _sync_producers(xs) -> None:
+    """The server copies on streams of its own: whatever torch queued for
+    these device tensors on the calling thread's current stream (the kernel
+    that produced a push, a fill of a pull's destination) must be done first.
+    One wait per device per call (batched calls: not one per buffer); a
+    stream with nothing pending costs a query.  Work on other torch streams is
+    the caller's to order."""
+    import torch
+    seen = set()
+    for x in xs:
+        if not hasattr(x, "device") or x.device.type != "cuda" or x.device in seen:
+            continue
+        seen.add(x.device)
+        st = torch.cuda.current_stream(x.device)
+        if not st.query():
+            st.synchronize()
+
+
+def key_hash(key: int, fn: str = "djb2", coef: int = 1) -> int:
+    """The reference's key hash (global.cc:491-523) through the C ABI."""
+    return int(_lib().byteps_server_key_hash(key, HASH_FNS[fn], coef))
+
+
+def make_group_config(num_workers: int, devices, engine_lanes: int = 4, policy: int = FUSED,
+                      async_mode: bool = False, enable_schedule: bool = False,
+                      engine_blocking: bool = False, split: str = "hash", hash_fn: str = "djb2",
+                      hash_coef: int = 1, split_min_bytes: int = 0) -> GroupConfig:
+    devices = list(devices)
+    c = GroupConfig()
+    c.server = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), 0,
+                            int(enable_schedule), int(engine_blocking))
+    c.num_servers = len(devices)
+    for i, d in enumerate(devices[:GROUP_MAX]):
+        c.devices[i] = d
+    c.split = {"hash": SPLIT_HASH, "range": SPLIT_RANGE}[split]
+    c.hash_fn = HASH_FNS[hash_fn]
+    c.hash_coef = hash_coef
+    c.split_min_bytes = split_min_bytes
+    return c
+
+
+def _pieces(fn, *args) -> list[tuple[int, int, int]]:
+    n = _int()
+    cap = GROUP_MAX
+    srv, off, ln = (_int * cap)(), (_sz * cap)(), (_sz * cap)()
+    _check(fn(*args, ctypes.byref(n), srv, off, ln, cap))
+    return [(srv[i], int(off[i]), int(ln[i])) for i in range(n.value)]
+
+
+def route(cfg: GroupConfig, key: int, nbytes: int) -> list[tuple[int, int, int]]:
+    """byteps_server_route: [(instance, offset, length)] of a key's pieces."""
+    return _pieces(_lib().byteps_server_route, ctypes.byref(cfg), key, nbytes)
+
+
+def group_config_from_env() -> GroupConfig:
+    c = GroupConfig()
+    _check(_lib().byteps_server_group_config_from_env(ctypes.byref(c)))
+    return c
 
 
 def config_from_env() -> ServerConfig:
@@ -96,10 +181,11 @@ def config_from_env() -> ServerConfig:
 
 class PSServer:
     def __init__(self, num_workers: int, engine_lanes: int = 4, policy: int = FUSED,
-                 async_mode: bool = False, device: int = 0, enable_schedule: bool = False):
+                 async_mode: bool = False, device: int = 0, enable_schedule: bool = False,
+                 engine_blocking: bool = False):
         self.lib = _lib()
         self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device,
-                                int(enable_schedule))
+                                int(enable_schedule), int(engine_blocking))
         self.handle = _vp()
         self._pending = {}
         _check(self.lib.byteps_server_create(ctypes.byref(self.cfg), ctypes.byref(self.handle)))
@@ -207,7 +293,8 @@ class PSServer:
         _check(self.lib.byteps_server_push_ready_many(self.handle, arr, len(keys), worker))
 
     def push_many(self, keys, worker: int, datas, dtype: int) -> None:
-        bufs = [_buf(d) for d in datas]
+        _sync_producers(datas)
+        bufs = [_buf(d, sync=False) for d in datas]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("push_many: all sources host, or all device")
@@ -217,7 +304,8 @@ class PSServer:
             (_sz * n)(*[b for _, b, _ in bufs]), n, worker, int(dtype), locs.pop() if n else 0))
 
     def pull_many(self, keys, outs) -> None:
-        bufs = [_buf(o) for o in outs]
+        _sync_producers(outs)
+        bufs = [_buf(o, sync=False) for o in outs]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("pull_many: all destinations host, or all device")
@@ -236,8 +324,92 @@ class PSServer:
         return [int(keys[i]) for i in range(min(n.value, max_log))]
 
     def close(self) -> None:
-        if self.handle:
+        if self.handle and getattr(self, "_owned", True):
             self.lib.byteps_server_destroy(self.handle)
+        self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class PSServerGroup:
+    """The key space over several server instances (byteps_server_group_*,
+    include/bpsr/server.h): whole keys by the reference's key hash
+    (``split="hash"``), or large keys cut into per-instance owner ranges
+    (``split="range"``).  Same push / pull / batched calls as PSServer."""
+
+    def __init__(self, num_workers: int, devices, engine_lanes: int = 4, policy: int = FUSED,
+                 async_mode: bool = False, enable_schedule: bool = False,
+                 engine_blocking: bool = False, split: str = "hash", hash_fn: str = "djb2",
+                 hash_coef: int = 1, split_min_bytes: int = 0):
+        self.lib = _lib()
+        c = make_group_config(num_workers, devices, engine_lanes, policy, async_mode,
+                              enable_schedule, engine_blocking, split, hash_fn, hash_coef,
+                              split_min_bytes)
+        self.cfg = c
+        self.handle = _vp()
+        _check(self.lib.byteps_server_group_create(ctypes.byref(c), ctypes.byref(self.handle)))
+
+    def route(self, key: int, nbytes: int) -> list[tuple[int, int, int]]:
+        """[(instance, offset, length)] of the key's pieces."""
+        return _pieces(self.lib.byteps_server_group_route, self.handle, key, nbytes)
+
+    def instance(self, i: int) -> "PSServer":
+        """Instance i as a non-owning PSServer (views, key_info of pieces)."""
+        h = _vp()
+        _check(self.lib.byteps_server_group_instance(self.handle, i, ctypes.byref(h)))
+        srv = PSServer.__new__(PSServer)
+        srv.lib, srv.cfg, srv.handle, srv._pending = self.lib, self.cfg.server, h, {}
+        srv._owned = False
+        return srv
+
+    def init_key(self, key: int, nbytes: int, dtype: int) -> None:
+        _check(self.lib.byteps_server_group_init_key(self.handle, key, nbytes, int(dtype)))
+
+    def push(self, key: int, worker: int, data, dtype: int, nbytes: int | None = None) -> None:
+        p, n, loc = _buf(data)
+        _check(self.lib.byteps_server_group_push(self.handle, key, worker, p,
+                                                 n if nbytes is None else nbytes, int(dtype), loc))
+
+    def pull(self, key: int, out, nbytes: int | None = None) -> None:
+        p, n, loc = _buf(out)
+        _check(self.lib.byteps_server_group_pull(self.handle, key, p,
+                                                 n if nbytes is None else nbytes, loc))
+
+    def push_many(self, keys, worker: int, datas, dtype: int) -> None:
+        _sync_producers(datas)
+        bufs = [_buf(d, sync=False) for d in datas]
+        locs = {loc for _, _, loc in bufs}
+        if len(locs) > 1:
+            raise ValueError("push_many: all sources host, or all device")
+        n = len(keys)
+        _check(self.lib.byteps_server_group_push_many(
+            self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
+            (_sz * n)(*[b for _, b, _ in bufs]), n, worker, int(dtype), locs.pop() if n else 0))
+
+    def pull_many(self, keys, outs) -> None:
+        _sync_producers(outs)
+        bufs = [_buf(o, sync=False) for o in outs]
+        locs = {loc for _, _, loc in bufs}
+        if len(locs) > 1:
+            raise ValueError("pull_many: all destinations host, or all device")
+        n = len(keys)
+        _check(self.lib.byteps_server_group_pull_many(
+            self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
+            (_sz * n)(*[b for _, b, _ in bufs]), n, locs.pop() if n else 0))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.byteps_server_group_destroy(self.handle)
             self.handle = _vp()
 
     def __del__(self):
@@ -253,5 +425,6 @@ class PSServer:
         self.close()
 
 
-__all__ = ["PSServer", "ServerConfig", "config_from_env", "FUSED", "INCREMENTAL", "HOST",
+__all__ = ["PSServer", "PSServerGroup", "GroupConfig", "key_hash", "group_config_from_env",
+           "make_group_config", "route", "ServerConfig", "config_from_env", "FUSED", "INCREMENTAL", "HOST",
            "DEVICE", "ReduceError", "SERVER_EXPORTS"]

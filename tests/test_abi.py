@@ -47,7 +47,7 @@ def test_library_exports_every_header_symbol():
 
 def test_version_and_dtype_sizes():
     lib = reducer.load_library()
-    assert lib.byteps_reduce_version() == 2
+    assert lib.byteps_reduce_version() == 3
     for dt in ALL_DTYPES:
         assert lib.byteps_reduce_dtype_size(int(dt)) == elem_size(dt)
     assert lib.byteps_reduce_dtype_size(7) == reducer.EDTYPE
@@ -116,8 +116,12 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     monkeypatch.setenv("BYTEPS_SERVER_ENGINE_THREAD", "3")
     monkeypatch.setenv("BYTEPS_ENABLE_ASYNC", "0")
     monkeypatch.setenv("BPSR_SERVER_POLICY", "incremental")
+    monkeypatch.setenv("BYTEPS_SERVER_ENGINE_BLOCKING", "1")
     c = server.config_from_env()
     assert (c.num_workers, c.engine_lanes, c.async_mode, c.policy) == (8, 3, 0, server.INCREMENTAL)
+    assert c.engine_blocking == 1
+    monkeypatch.setenv("BYTEPS_SERVER_ENGINE_BLOCKING", "0")
+    assert server.config_from_env().engine_blocking == 0
     lib = server._lib()
     bad = server.ServerConfig(0, 4, 0, 0, 0)
     h = ctypes.c_void_p()

@@ -488,6 +488,16 @@ def test_host_releases_rules(red, dev):
         q.config(wg_per_cu=2)
     with pytest.raises(ReduceError):
         q.release_host(1, 2)
+    # a captured launch cannot carry the host-release helper: refused, even
+    # with every block pre-released from the host
+    q.release_host(0, 2)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with pytest.raises(ReduceError) as ei:
+        with torch.cuda.graph(g, stream=s):
+            q.launch(s)
+    assert ei.value.code == EARGS and "host releases" in str(ei.value)
+    torch.cuda.synchronize()
     q.host_releases(False)
     q.config(wg_per_cu=1)
     q.close()

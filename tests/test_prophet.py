@@ -272,6 +272,19 @@ def test_native_errors():
     q2 = ProphetPushQueue(64, 1, 50, checkpoints=(-1, 1, 3), backward_exec=(0, 0, 0))
     with pytest.raises(ReduceError, match="no progress"):
         release_groups(q2, _arrivals(), finish_immediately=False, max_idle=1000)
+    # the tasks the queue still holds stay pollable after the
+    # failure (no KeyError): give credit and drain them
+    held = q2.pending()
+    assert held > 0
+    got = []
+    for _ in range(10_000):
+        q2.report_finish(1 << 20)
+        t = q2.get_task()
+        if t is not None:
+            got.append(t)
+        if q2.pending() == 0:
+            break
+    assert len(got) == held and all(isinstance(t, PushTask) for t in got)
 
 
 def test_native_defaults_are_the_reference_model():

@@ -210,3 +210,50 @@ def test_push_pull_async_handles():
         want = sum(np.arange(30, dtype=np.int32) * (r + 1) + i for r in range(N))
         for r in range(N):
             assert np.array_equal(vals[(r, n)], want)
+
+
+def test_partition_bytes_and_local_size_from_env(monkeypatch):
+    """BYTEPS_PARTITION_BYTES / BYTEPS_LOCAL_SIZE change the key lists exactly
+    as the reference's bound does: AlignTo(atoi(bytes), 8 * local_size)
+    rounded down (global.cc:128-135, communicator.cc:71-77)."""
+    monkeypatch.setenv("BYTEPS_PARTITION_BYTES", "1000063")
+    monkeypatch.setenv("BYTEPS_LOCAL_SIZE", "8")
+    srv = FakeServer(1)
+    w = Worker(0, ServerFrontend(srv))
+    assert w.bound == 1_000_063 // 64 * 64 == 1_000_000
+    x = np.arange(750_001, dtype=np.int32)               # 3,000,004 B
+    ctx = w.init_tensor("g", x, DType.INT32)
+    assert ctx.key_list == [0, 1, 2, 3]
+    assert [ln for _, _, ln in ctx.parts] == [1_000_000] * 3 + [4]
+    w.declare("h")
+    ctx2 = w.init_tensor("h", np.zeros(10, np.int32), DType.INT32)
+    assert ctx2.key_list == [1 << 16]
+    # the ResNet-50 fp16 set under this bound: partitions per tensor
+    from prophet_amd.buckets import partition_all
+    parts = partition_all([n * 2 for n in resnet50_param_sizes()], bound=w.bound)
+    want = sum(-(-n * 2 // 1_000_000) for n in resnet50_param_sizes())
+    assert len(parts) == want and want > 165           # more keys than the default's 165
+
+
+@pytest.mark.parametrize("env,bound", [
+    ({}, 4_096_000),                                          # defaults
+    ({"BYTEPS_LOCAL_SIZE": "8"}, 4_096_000),                  # 4096000 % 64 == 0
+    ({"BYTEPS_PARTITION_BYTES": "4096001", "BYTEPS_LOCAL_SIZE": "3"}, 4_095_984),
+    ({"BYTEPS_PARTITION_BYTES": " 2048000xyz"}, 2_048_000),   # atoi
+    ({"BYTEPS_PARTITION_BYTES": "100", "BYTEPS_LOCAL_SIZE": "8"}, 64),
+])
+def test_partition_bound_env_cases(monkeypatch, env, bound):
+    for k in ("BYTEPS_PARTITION_BYTES", "BYTEPS_LOCAL_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert Worker(0, ServerFrontend(FakeServer(1))).bound == bound
+
+
+def test_partition_bound_env_zero_is_refused(monkeypatch):
+    monkeypatch.setenv("BYTEPS_PARTITION_BYTES", "63")
+    monkeypatch.setenv("BYTEPS_LOCAL_SIZE", "8")      # AlignTo(63, 64) == 0
+    with pytest.raises(ValueError, match="positive"):
+        Worker(0, ServerFrontend(FakeServer(1)))
+    # explicit arguments still override the environment
+    assert Worker(0, ServerFrontend(FakeServer(1)), partition_bytes=1000, local_size=1).bound == 1000

@@ -886,3 +886,94 @@ def test_pull_device_view_held_until_own_push(port):
         _init_round(a, dt, 2, [16])
         with pytest.raises(ReduceError, match="sync mode"):
             a.pull_device_view(0)
+
+
+@pytest.mark.parametrize("fail_after", [0, 1], ids=["init_copy", "round_fold"])
+def test_fold_failure_fails_waiters_instead_of_hanging(monkeypatch, fail_after):
+    """with scheduling off a fold that cannot be issued must fail
+    the key (fail_key), else the other workers wait forever.  Fault injection
+    (BPSR_SERVER_FAIL_AFTER=n: the (n+1)-th fold issue fails): 0 = the init
+    copy fails while worker 0's init push waits for the barrier; 1 = round 1's
+    fused fold fails while worker 0 waits in a pull.  Every waiter returns the
+    error; later calls on the key return it too."""
+    from prophet_amd.reducer import EHIP, ReduceError
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_FAIL_AFTER", str(fail_after))
+    dt, n = DType.FLOAT32, 4096
+    srv = PSServer(2, engine_lanes=1)
+    out = {}
+
+    def waiter():
+        try:
+            if fail_after == 0:
+                srv.push(5, 0, data(dt, n, 0, 0, 5), dt)          # blocks: init barrier
+            else:
+                srv.pull(5, np.zeros(n * 4, np.uint8))           # blocks: round 1
+            out["w"] = 0
+        except ReduceError as e:
+            out["w"] = e.code
+    if fail_after == 1:
+        t0 = threading.Thread(target=srv.push, args=(5, 0, data(dt, n, 0, 0, 5), dt))
+        t0.start()
+        srv.push(5, 1, data(dt, n, 1, 0, 5), dt)                 # init round completes
+        t0.join(timeout=60)
+        srv.push(5, 0, data(dt, n, 0, 1, 5), dt)                 # round 1, first arrival
+    t = threading.Thread(target=waiter)
+    t.start()
+    time.sleep(0.2)                                              # the waiter is blocked
+    with pytest.raises(ReduceError) as ei:
+        srv.push(5, 1, data(dt, n, 1, 1, 5), dt)                 # completes -> fold fails
+    assert ei.value.code == EHIP and "injected" in str(ei.value)
+    t.join(timeout=30)
+    assert not t.is_alive(), "waiter hung after the failed fold"
+    assert out["w"] == EHIP
+    with pytest.raises(ReduceError) as ei:
+        srv.pull(5, np.zeros(n * 4, np.uint8))
+    assert ei.value.code == EHIP
+    srv.close()
+
+
+@pytest.mark.parametrize("policy", [0, 1], ids=["fused", "incremental"])
+def test_engine_blocking_mode(port, policy):
+    """BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:205-262, 284-285): a push
+    returns once its copy / sum / fold has completed, and a pull is answered
+    at once from the store as it stands — a pull before the round's last push
+    sees the previous round (the reference's ungated SendPullResponse), one
+    after it sees the new left fold; pulls are not counted, so any number of
+    them never blocks the next round."""
+    from prophet_amd.server import PSServer, config_from_env
+    dt, n, N = DType.FLOAT32, 70_001, 3
+    srv = PSServer(N, engine_lanes=2, policy=policy, engine_blocking=True)
+    init = [data(dt, n, w, 0, 9) for w in range(N)]
+    ts = [threading.Thread(target=srv.push, args=(9, w, init[w], dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    out = np.zeros(n * 4, np.uint8)
+    srv.pull(9, out)
+    assert any(np.array_equal(out, x) for x in init)    # init store = last init arrival
+    prev = out.copy()
+    for rnd in (1, 2, 3):
+        ins = [data(dt, n, w, rnd, 9) for w in range(N)]
+        order = [(rnd + k) % N for k in range(N)]
+        for i, w in enumerate(order):
+            srv.push(9, w, ins[w], dt)
+            if i < N - 1:
+                for _ in range(2):                       # ungated, uncounted pulls
+                    srv.pull(9, out)
+                    assert np.array_equal(out, prev), (rnd, i)
+        want = np.zeros(n * 4, np.uint8)
+        port.sum_n(want, [ins[w] for w in order], want.nbytes, dt)
+        srv.pull(9, out)
+        assert np.array_equal(out, want), rnd
+        view = np.frombuffer(srv.pull_view(9), np.uint8)
+        assert np.array_equal(view, want), rnd
+        prev = want
+    srv.close()
+    import os
+    os.environ["BYTEPS_SERVER_ENGINE_BLOCKING"] = "1"
+    try:
+        assert config_from_env().engine_blocking == 1
+    finally:
+        del os.environ["BYTEPS_SERVER_ENGINE_BLOCKING"]
