@@ -66,6 +66,13 @@ struct Lane {
   // (every push copy of the lane so far); batched calls wait for fold_mark /
   // d2h_mark once per lane instead of one event per key.
   hipEvent_t copy_mark = nullptr, fold_mark = nullptr, d2h_mark = nullptr;
+  // Completed rounds of single-key calls waiting to be issued (combining, no
+  // scheduling): the first caller to find no issuer active becomes it and
+  // issues everything queued — one batched launch for what piled up while it
+  // was launching — until the list is empty (issue_combined).
+  std::mutex comb_mu;
+  std::vector<FoldJob> comb;
+  bool comb_active = false;
 };
 
 // A pull ready to be answered, or a push to acknowledge, by the responder.
@@ -142,6 +149,7 @@ struct byteps_server {
   byteps_server_config cfg;
   bool schedule = false;
   bool blocking = false;  // BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:324)
+  bool combine = true;    // coalesce single-key calls' folds per lane (BPSR_SERVER_COMBINE)
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
@@ -683,11 +691,72 @@ int finish_blocking(byteps_server* s, KeyState* ks, std::unique_lock<std::mutex>
   return e == hipSuccess ? 0 : hip_fail(e, "engine blocking: fold sync");
 }
 
+// Issue one deferred round (no batching partner).
+int issue_one(byteps_server* s, FoldJob& j) {
+  KeyState* ks = j.ks;
+  std::lock_guard<std::mutex> g(ks->mu);
+  ks->pending--;
+  const int rc = ks->error ? 0 : execute(s, j);
+  if (rc) fail_key(s, ks, rc);
+  ks->cv.notify_all();
+  return rc;
+}
+
+// Combining issue of the rounds single-key calls completed (defer lists of
+// arrive; caller holds no key lock).  Each lane keeps one list: a caller
+// appends its rounds; if no issuer is active it becomes the issuer and issues
+// the list — one fold launch for a lone round, ONE batched launch for rounds
+// that piled up meanwhile (other workers' calls completing keys while it was
+// launching) — until the list is empty.  So an uncontended call issues its
+// fold at once, and concurrent calls share launches instead of queueing one
+// each (the reference engine's per-message sums, server.cc:70-145, paid per
+// key on the host too).  A fold that fails fails its key (fail_key).
+int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs) {
+  if (jobs.empty()) return 0;
+  int first_rc = 0;
+  std::stable_sort(jobs.begin(), jobs.end(),
+                   [](const FoldJob& a, const FoldJob& b) { return a.ks->lane < b.ks->lane; });
+  size_t i = 0;
+  while (i < jobs.size()) {
+    const int lane = jobs[i].ks->lane;
+    Lane& L = *s->lanes[lane];
+    bool issuer = false;
+    {
+      std::lock_guard<std::mutex> g(L.comb_mu);
+      for (; i < jobs.size() && jobs[i].ks->lane == lane; ++i) L.comb.push_back(std::move(jobs[i]));
+      if (!L.comb_active) issuer = L.comb_active = true;
+    }
+    while (issuer) {
+      std::vector<FoldJob> take;
+      {
+        std::lock_guard<std::mutex> g(L.comb_mu);
+        if (L.comb.empty()) {
+          L.comb_active = false;
+          break;
+        }
+        take.swap(L.comb);
+      }
+      const int rc = take.size() == 1 ? issue_one(s, take[0]) : flush_folds(s, take);
+      if (rc && !first_rc) first_rc = rc;
+    }
+  }
+  jobs.clear();
+  return first_rc;
+}
+
+// After a single-key call issued (or queued) its round: the key's own error,
+// if its fold failed by the time the call returns.
+int own_key_status(KeyState* ks) {
+  std::lock_guard<std::mutex> g(ks->mu);
+  return ks->error ? key_error(ks) : 0;
+}
+
 // Init pushes block until every worker's init push has arrived and the store
 // is initialised: the reference answers them only then (server.cc:184-198).
-int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock<std::mutex>& lk) {
+int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock<std::mutex>& lk,
+                         std::vector<FoldJob>* defer = nullptr) {
   const bool init_round = !ks->inited;
-  int rc = arrive(s, ks, w);
+  int rc = arrive(s, ks, w, defer);
   if (rc || !init_round) return rc;
   ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
   return ks->error ? key_error(ks) : 0;
@@ -768,6 +837,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   s->schedule = cfg->enable_schedule != 0;
   s->blocking = cfg->engine_blocking != 0;
   if (const char* fa = getenv("BPSR_SERVER_FAIL_AFTER")) s->fail_after = atol(fa);
+  if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
@@ -895,7 +965,13 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
-  if ((rc = arrive_and_wait_init(s, ks, worker, lk))) return rc;
+  std::vector<FoldJob> defer;
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return rc;
+  if (!defer.empty()) {
+    lk.unlock();
+    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return rc;
+    lk.lock();
+  }
   return s->blocking ? finish_blocking(s, ks, lk) : 0;
 }
 
@@ -914,7 +990,8 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
   if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
   const bool init_push = !ks->inited;
-  if ((rc = arrive(s, ks, worker))) {  // arrival order = call order
+  std::vector<FoldJob> defer;
+  if ((rc = arrive(s, ks, worker, s->combine ? &defer : nullptr))) {  // arrival order = call order
     // the caller gets its buffer back on error: let the queued copy finish first
     (void)hipEventSynchronize(ks->copied);
     return rc;
@@ -932,6 +1009,10 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
     return BYTEPS_REDUCE_OK;
   }
   enqueue_response(s, r);
+  if (!defer.empty()) {
+    lk.unlock();
+    if (issue_combined(s, defer)) return own_key_status(ks);
+  }
   return BYTEPS_REDUCE_OK;
 }
 
@@ -964,7 +1045,13 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
   std::unique_lock<std::mutex> lk(ks->mu);
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-  if ((rc = arrive_and_wait_init(s, ks, worker, lk))) return rc;
+  std::vector<FoldJob> defer;
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return rc;
+  if (!defer.empty()) {
+    lk.unlock();
+    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return rc;
+    lk.lock();
+  }
   return s->blocking ? finish_blocking(s, ks, lk) : 0;
 }
 

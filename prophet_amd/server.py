@@ -123,7 +123,7 @@ def _sync_producers(xs) -> None:
     import torch
     seen = set()
     for x in xs:
-        if not hasattr(x, "device") or x.device.type != "cuda" or x.device in seen:
+        if not hasattr(x, "data_ptr") or x.device.type != "cuda" or x.device in seen:
             continue
         seen.add(x.device)
         st = torch.cuda.current_stream(x.device)

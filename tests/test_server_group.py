@@ -128,3 +128,12 @@ def test_group_config_from_env(monkeypatch):
     monkeypatch.setenv("BPSR_SERVER_GPUS", "17")
     with pytest.raises(reducer.ReduceError):
         server.group_config_from_env()
+
+
+def test_producer_sync_accepts_host_buffers():
+    """numpy 2 arrays carry a ``.device`` attribute too: the one-wait-per-call
+    producer sync of the batched calls must skip host buffers (numpy and CPU
+    tensors) without touching a GPU."""
+    import numpy as np
+    import torch
+    server._sync_producers([np.zeros(4, np.uint8), torch.zeros(4), np.ones(2)])
