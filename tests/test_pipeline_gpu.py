@@ -50,16 +50,33 @@ def test_streaming_zero_copy_rejects_pageable(red):
         sr.reduce(host, torch.zeros(64, dtype=torch.uint8).pin_memory(), 64, DType.UINT8)
 
 
-def test_sharded_reduce_from_host_single_rank(red):
+@pytest.fixture
+def gloo_world1():
+    """A world-1 gloo default group for the test, destroyed after it (a group
+    left behind would make a later init_process_group fail)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    made = False
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        made = True
+    yield
+    if made and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_sharded_reduce_from_host_single_rank(red, gloo_world1):
     """reduce_from_host: the owner's slice of pinned host pushes straight to its
     HBM slots, HIP fold; equal to torch's left fold."""
     import torch.distributed as dist
     from prophet_amd.shard import ShardedReducer
-    if not dist.is_initialized():
-        import os
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("gloo", rank=0, world_size=1)
     n = 200_003
     sr = ShardedReducer(n)
     dev = torch.device("cuda:0")
@@ -74,14 +91,9 @@ def test_sharded_reduce_from_host_single_rank(red):
     assert torch.equal(owned.cpu(), ref)
 
 
-def test_sharded_reducer_single_rank(red):
+def test_sharded_reducer_single_rank(red, gloo_world1):
     import torch.distributed as dist
     from prophet_amd.shard import ShardedReducer
-    if not dist.is_initialized():
-        import os
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("gloo", rank=0, world_size=1)
     n = 100_003
     sr = ShardedReducer(n)            # default fold = HIP via the C ABI
     dev = torch.device("cuda:0")

@@ -347,6 +347,8 @@ def test_rccl_wrap_torch_process_group_comm():
     from prophet_amd.shard import ShardComm
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     dev = torch.device("cuda", 0)
+    if dist.is_initialized():       # a group another test left behind
+        dist.destroy_process_group()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
         t = torch.ones(4, device=dev)

@@ -35,11 +35,14 @@ for s in $STEPS; do
     srv) for v in 0 1 4; do run srv_v$v 300 $SRV 20 4 $v || exit 1; done ;;
     srvall) run srvall 400 $SRV 20 4 ;;
     srvprof) for v in 0 4; do
-               run srvprof_v$v 300 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/srvprof_v$v -o run -- $SRV 10 4 $v || exit 1
+               run srvprof_v$v 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/srvprof_v$v -o run -- $SRV 10 4 $v || exit 1
              done ;;
     cfg3) run cfg3 300 tools/cfg3_native tools/cfg3_resnet50_table.txt 200 7 tools/cfg3_resnet50_tasks.txt ;;
-    cfg3prof) run cfg3prof 300 rocprofv3 --kernel-trace --stats -d $OUT/cfg3prof -o run -- tools/cfg3_native tools/cfg3_resnet50_table.txt 200 3 "" blockq_live_release ;;
-    benchprof) run benchprof 600 rocprofv3 --kernel-trace --stats -d $OUT/benchprof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    cfg3prof) run cfg3prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/cfg3prof -o run -- tools/cfg3_native tools/cfg3_resnet50_table.txt 200 3 "" blockq_live_release ;;
+    benchprof) run benchprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/benchprof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
+  # keep what comes back small: traces compressed, databases dropped
+  find "$OUT" -name '*.db' -delete
+  find "$OUT" -name '*_trace.csv' -size +1M -exec gzip -f {} \;
 done
