@@ -710,17 +710,25 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     (scheduled_queue.h:78-79, last checkpoint extended to 160), folded by the
     block queue: ONE consumer launch per iteration that starts each block once
     it is released (byteps_reduce_blockq_*).  ``live``: the
-    launch, then the 12 per-block releases from a second stream (as the push
-    path issues them behind each block's pushes); ``pre_released``: every block
-    released before the launch; ``live_host_releases``: the launch, then the 12
-    releases from the host (byteps_reduce_blockq_release_host — the pushes are
-    resident, as after an RDMA write into HBM), no stream work per release.  Device time per iteration from HIP events on
+    product push path — the native PUSH loop (byteps_prophet_loop_*, inline)
+    launches the consumer, the 165 partitions are pushed in backward order as
+    one batch (they have all landed), Prophet's scheduler (scheduled_queue.cc
+    getTask) releases them group by group and the loop releases the blocks
+    those groups complete with stream-ordered release kernels on a second
+    stream, the groups ready together as one kernel (``release_kernels_per_iter``);
+    ``live_per_block``: the launch, then one release kernel per block from
+    the second stream (the round-2 ``live``: every block as its own release
+    group); ``pre_released``: every block released before the launch;
+    ``live_host_releases``: the launch, then the 12 releases from the host
+    (byteps_reduce_blockq_release_host — the pushes are resident, as after an
+    RDMA write into HBM), no stream work per release.  Device time per iteration from HIP events on
     the consumer's stream (median of ``reps`` runs of ``iters`` back-to-back
     iterations over ``sets`` rotated input sets), host time of the issuing
     loop, exactness against torch's own left fold."""
     import torch
     from prophet_amd.buckets import partition_all, prophet_blocks, resnet50_param_sizes
     from prophet_amd.dtypes import DType
+    from prophet_amd.prophet import ProphetPushQueue, PushLoop, PushTask, model_checkpoints
     sizes = [n * 2 for n in resnet50_param_sizes()]
     parts = partition_all(sizes)
     toff = [0]
@@ -731,6 +739,13 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     for blk in prophet_blocks(len(sizes)):
         tset = set(blk)
         by_block.append([p for p in parts if p.tensor in tset])
+    # the PUSH loop's table: partition handle = position in block order
+    table = [p for bp in by_block for p in bp]
+    block_of = [b for b, bp in enumerate(by_block) for _ in bp]
+    nparts = {}
+    for p in parts:
+        nparts[p.tensor] = nparts.get(p.tensor, 0) + 1
+    arrivals = sorted(range(len(table)), key=lambda i: (-table[i].tensor, table[i].part))
     gen = torch.Generator(device=dev)
     data, queues, hqueues = [], [], []
     for i in range(sets):
@@ -756,8 +771,28 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     live_s = queues[0].stream()
     rel_s = torch.cuda.Stream(device=dev)
     nb = len(by_block)
+    # one scheduler + inline PUSH loop per input set (a loop drives one queue);
+    # Z_BATCH_SIZE 64, Z_NET_B 10000, Z_CREDIT 16 MiB, the reference's block
+    # budgets (as tools/cfg3_native.cpp and tests/test_pushloop_gpu.py)
+    loops, batches = [], []
+    for q in queues:
+        pq = ProphetPushQueue(batch_size=64, net_b=10000, credit=16 << 20,
+                              checkpoints=model_checkpoints(len(sizes)))
+        lp = PushLoop(pq, q, block_of, release_stream=rel_s, inline=True)
+        loops.append(lp)
+        batches.append(lp.make_batch(
+            [PushTask(table[i].tensor, table[i].part, table[i].len, nparts[table[i].tensor],
+                      (table[i].tensor << 16) + table[i].part) for i in arrivals], arrivals))
+    import gc
+    gc.collect()      # inline loop: no GC-triggered hipFree inside an iteration
 
-    def live(i):
+    def live(i):      # the PUSH loop: launch, one batch of landed pushes, releases
+        lp = loops[i % sets]
+        lp.begin(live_s)
+        lp.push_many(batches[i % sets])
+        lp.end(timeout_s=5.0)
+
+    def live_per_block(i):
         q = queues[i % sets]
         q.launch(live_s)
         for b in range(nb):
@@ -786,11 +821,13 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                         f"{len(parts)} partitions in {nb} Prophet blocks, block queue "
                         "(one consumer launch per iteration)"),
            "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
-    for name, fn in (("live", live), ("pre_released", pre_released),
-                     ("live_host_releases", live_host)):
+    rel_kernels = {"live_per_block": nb, "pre_released": 1, "live_host_releases": 0}
+    for name, fn in (("live", live), ("live_per_block", live_per_block),
+                     ("pre_released", pre_released), ("live_host_releases", live_host)):
         for i in range(30):
             fn(i)
         torch.cuda.synchronize()
+        c0 = sum(lp.release_calls() for lp in loops)
         ts, hs = [], []
         for _ in range(reps):
             e0 = torch.cuda.Event(enable_timing=True)
@@ -808,10 +845,14 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                      "spread": round((max(ts) - min(ts)) / ms, 4),
                      "frac_of_roofline": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "host_us_per_iter": round(statistics.median(hs), 1)}
+        if name == "live":
+            rel_kernels[name] = round((sum(lp.release_calls() for lp in loops) - c0)
+                                      / (reps * iters), 2)
+        res[name]["release_kernels_per_iter"] = rel_kernels[name]
     for q in queues + hqueues:
         q.status(live_s)
     ok = True
-    for fn in (live, live_host):
+    for fn in (live, live_per_block, live_host):
         for i, (w, out) in enumerate(data):
             out.zero_()
             torch.cuda.synchronize()
@@ -822,6 +863,8 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                 ref.add_(x.view(torch.float16))
             ok = ok and bool(torch.equal(ref.view(torch.uint8), out))
     res["exact_vs_torch_fold"] = ok
+    for lp in loops:
+        lp.close()
     for q in queues + hqueues:
         q.close()
     return res

@@ -170,10 +170,16 @@ int byteps_prophet_estimate_net_b(const int64_t* size, const int64_t* start_us,
  *       on the library's consumer stream, byteps_reduce_blockq_stream);
  *   byteps_prophet_loop_push(l, &task)  one per partition as its bytes land
  *       (their copies queued on release_stream, or finished), in any order —
- *       the loop thread polls getTask and, at the end of each release group,
- *       releases every block that became complete (one release_range per run
- *       of consecutive blocks, on release_stream), then reports the group's
- *       partitions finished;
+ *       the loop thread polls getTask, reports each release group's partitions
+ *       finished at the group's end (credit back, so the next group may go),
+ *       and when a poll makes no progress (the scheduler waits for pushes or
+ *       credit) releases every block that became complete meanwhile: ONE
+ *       release_range per run of consecutive blocks, on release_stream.  So
+ *       the release groups that are ready together — every group, when the
+ *       pushes have all landed — go out as one kernel, and a block is held
+ *       back at most by the host work of draining the groups ready with it;
+ *   byteps_prophet_loop_push_many(l, tasks, n)  the same for n partitions
+ *       that landed together (one drain for all of them), in array order;
  *   byteps_prophet_loop_end(l, timeout_s)  waits until every block has been
  *       released (timeout_s <= 0: no limit); with the loop thread, a task the
  *       scheduler refuses (e.g. a gradient outside the model) is reported
@@ -205,7 +211,12 @@ int byteps_prophet_loop_create(byteps_prophet_queue* pq, byteps_reduce_blockq* b
                                void* release_stream, int flags, byteps_prophet_loop** out);
 int byteps_prophet_loop_begin(byteps_prophet_loop* l, void* consumer_stream);
 int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* t);
+int byteps_prophet_loop_push_many(byteps_prophet_loop* l, const byteps_prophet_task* tasks,
+                                  int32_t n);
 int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s);
+/* Release calls (release_range kernels, or host releases) the loop has issued
+ * since create: telemetry for how many groups went out together. */
+int byteps_prophet_loop_release_calls(byteps_prophet_loop* l, uint64_t* calls);
 int byteps_prophet_loop_destroy(byteps_prophet_loop* l);
 
 #ifdef __cplusplus

@@ -80,7 +80,12 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
 
 /* A worker's push of `len` bytes for `key` (round 0 = init push).  The data is
  * copied into the worker's receive slot before the call returns (the caller may
- * reuse `data`); the fold is queued on the key's engine lane. */
+ * reuse `data`); the fold is queued on the key's engine lane.  Default engine
+ * (no scheduling, no engine blocking): the round a push completes is handed
+ * to the lane's issuer thread, which issues the rounds that piled up as ONE
+ * batched fold launch (BPSR_SERVER_COMBINE=0: the completing call issues its
+ * own fold).  A failed fold fails its key: every later call on it returns the
+ * error. */
 int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data,
                        size_t len, int dtype, int location);
 
@@ -112,7 +117,9 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
 int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 
 /* A worker's pull: blocks until the key's current round is finished (sync mode),
- * then copies the store (len bytes) to `out`. */
+ * then copies the store (len bytes) to `out`.  Device destinations in sync mode
+ * go through the lane's issuer thread: the pulls that piled up are copied by
+ * ONE batched copy launch. */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
 /* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
@@ -159,9 +166,15 @@ typedef void (*byteps_server_pull_cb)(void* ctx, uint64_t key, const void* data,
 int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_cb cb, void* ctx);
 
 /* Introspection for tests/debug (BYTEPS_SERVER_DEBUG analogue): completed
- * rounds, engine lane, and the arrival order of the last completed round. */
+ * rounds, engine lane, and the arrival order of the last completed round
+ * (waits until every round the key completed has been issued). */
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
                            int* last_order, int max_order);
+
+/* Telemetry since create: out[0] fold launches (single and batched), out[1]
+ * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
+ * views); the first n of them. */
+int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located
  * workers, an in-process transport; ps-lite sends one key per request,

@@ -4,8 +4,10 @@
 // (byteps/common/scheduled_queue.cc:217-296, scheduled_queue.h:77-95) with
 // containers that fit the access pattern: the priority multiset becomes one
 // FIFO of queued partitions per gradient (findTask is always an exact-priority
-// lookup, and equal priorities keep insertion order), the 160-entry arrays are
-// sized by the model's last checkpoint, the stack holds gradient indices.
+// lookup, and equal priorities keep insertion order) — a vector and a head
+// index that keep their capacity, so a steady-state iteration allocates
+// nothing — the 160-entry arrays are sized by the model's last checkpoint, the
+// stack holds gradient indices.
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -31,8 +33,21 @@ struct byteps_prophet_queue {
   std::vector<int32_t> checkpoints;
   std::vector<double> budget;           // per block, bytes (constructor, :26-33)
   int64_t credit0 = 0;
-  // queued tasks
-  std::vector<std::deque<byteps_prophet_task>> tasks;  // per gradient (_ms)
+  // queued tasks: per gradient (_ms) a FIFO = vector + head (emptied -> cleared)
+  struct Fifo {
+    std::vector<byteps_prophet_task> v;
+    size_t head = 0;
+    bool empty() const { return head == v.size(); }
+    const byteps_prophet_task& front() const { return v[head]; }
+    void push_back(const byteps_prophet_task& t) { v.push_back(t); }
+    void pop_front() {
+      if (++head == v.size()) {
+        v.clear();
+        head = 0;
+      }
+    }
+  };
+  std::vector<Fifo> tasks;
   std::vector<int32_t> tensor_part;                    // _tensor_part
   std::deque<byteps_prophet_task> fifo;                // _sq
   uint64_t nsched = 0;                                 // _ms.size()
@@ -362,5 +377,36 @@ int prophet_poll(byteps_prophet_queue* q, byteps_prophet_task* out, bool* progre
   std::lock_guard<std::mutex> g(q->mu);
   int32_t ph = 0;
   return q->poll(out, &ph, progressed) ? 1 : 0;
+}
+
+int prophet_add_many(byteps_prophet_queue* q, const byteps_prophet_task* t, size_t n) {
+  std::lock_guard<std::mutex> g(q->mu);
+  for (size_t i = 0; i < n; ++i)  // all or nothing
+    if (const int rc = q->validate(t[i])) return rc;
+  for (size_t i = 0; i < n; ++i) (void)q->add(t[i]);
+  return 0;
+}
+
+size_t prophet_drain(byteps_prophet_queue* q, std::vector<byteps_prophet_task>* released) {
+  std::lock_guard<std::mutex> g(q->mu);
+  const size_t first = released->size();
+  size_t group = first;  // first task of the open release group
+  for (;;) {
+    byteps_prophet_task t;
+    int32_t ph = 0;
+    bool prog = false;
+    if (q->poll(&t, &ph, &prog)) {
+      released->push_back(t);
+      continue;
+    }
+    if (group != released->size()) {  // a group ended: report_finish, :367-369
+      for (size_t i = group; i < released->size(); ++i)
+        if ((*released)[i].len > 0 && q->meetzero) q->credit += (*released)[i].len;
+      group = released->size();
+      continue;
+    }
+    if (!prog) break;
+  }
+  return released->size() - first;
 }
 }  // namespace bpsr

@@ -5,12 +5,15 @@
 // RunPushLoopOnce: getTask, send, FinishOrProceed -> reportFinish) over the
 // scheduled queue.  Here the "send" of a released partition is the device
 // fold of its block: the loop thread polls the scheduler whenever partitions
-// arrive, counts released partitions per block and, at the end of each
-// release group, releases every block that became complete — one
-// byteps_reduce_blockq_release_range per run of consecutive blocks, on the
+// arrive, counts released partitions per block, reports each release group's
+// partitions finished at the group's end (credit back to the scheduler) and,
+// once a poll makes no progress, releases every block that became complete —
+// one byteps_reduce_blockq_release_range per run of consecutive blocks, on the
 // release stream, behind the copies that landed the pushes, or from the host
-// with BYTEPS_PROPHET_LOOP_HOST_RELEASE when the pushes are already in HBM —
-// then reports the group's partitions finished (credit back to the scheduler).
+// with BYTEPS_PROPHET_LOOP_HOST_RELEASE when the pushes are already in HBM.
+// Groups that are ready together thus share one release kernel: every release
+// kernel that runs beside the consumer costs it ~0.4-0.6 us,
+// and a block waits at most for the host work of draining its companions.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -45,13 +48,14 @@ struct byteps_prophet_loop {
   std::vector<int32_t> left;        // partitions not yet released, per block
   std::vector<char> released;       // block released this iteration
   int32_t blocks_released = 0;
+  uint64_t release_calls = 0;       // release kernels / host releases issued, ever
   std::vector<char> got;            // task handle pushed this iteration
   int err = 0;
   bool inline_drain = false;   // BYTEPS_PROPHET_LOOP_INLINE: pushers drain
   bool host_release = false;   // BYTEPS_PROPHET_LOOP_HOST_RELEASE: release_host, no stream
   std::atomic<bool> waiting{false};  // the loop thread sleeps on cv
   std::mutex drain_mu;
-  std::vector<int64_t> group_lens;  // the open release group (under drain_mu)
+  std::vector<byteps_prophet_task> drained;  // one drain's releases (under drain_mu)
   // thread mode: pushes land in an inbox the loop thread empties into the
   // scheduler itself, so pushers and the drain never contend on its lock
   std::mutex inbox_mu;
@@ -73,6 +77,7 @@ struct byteps_prophet_loop {
       const int rc = host_release ? byteps_reduce_blockq_release_host(bq, b, e - b)
                                   : byteps_reduce_blockq_release_range(bq, b, e - b, rel_stream);
       if (rc) return rc;
+      ++release_calls;
       blocks_released += e - b;
       b = e;
     }
@@ -81,33 +86,18 @@ struct byteps_prophet_loop {
 
   // Drain the scheduler: poll until a zero poll made no progress (a zero poll
   // may still advance collection or end a block, and the next may release);
-  // at each release group's end, release the complete blocks, then report the
-  // group's partitions finished.  One drainer at a time (drain_mu).
+  // at each release group's end report the group's partitions finished
+  // (credit back: the next poll may release more); when the scheduler can go
+  // no further, release the complete blocks — the groups drained together in
+  // one kernel per run of blocks.  One drainer at a time (drain_mu).
   int drain() {
     std::lock_guard<std::mutex> dg(drain_mu);
-    int rc = 0;
-    for (;;) {
-      byteps_prophet_task t;
-      bool prog = false;
-      if (bpsr::prophet_poll(pq, &t, &prog) == 1) {
-        std::lock_guard<std::mutex> g(mu);
-        if (t.handle < block_of.size()) --left[block_of[t.handle]];
-        group_lens.push_back(t.len);
-        continue;
-      }
-      if (!group_lens.empty()) {  // a release group ended
-        {
-          std::lock_guard<std::mutex> g(mu);
-          rc = release_complete();
-        }
-        for (int64_t len : group_lens) byteps_prophet_report_finish(pq, len);
-        group_lens.clear();
-        if (rc) break;
-        continue;  // credit came back: the next poll may release more
-      }
-      if (!prog) break;
-    }
+    drained.clear();
+    bpsr::prophet_drain(pq, &drained);  // credit returned per group inside
     std::lock_guard<std::mutex> g(mu);
+    for (const auto& t : drained)
+      if (t.handle < block_of.size()) --left[block_of[t.handle]];
+    const int rc = release_complete();
     if (rc && !err) err = rc;
     if (err || blocks_released == nblocks()) done_cv.notify_all();
     return rc;
@@ -127,9 +117,7 @@ struct byteps_prophet_loop {
         std::lock_guard<std::mutex> g(inbox_mu);
         taken.swap(inbox);
       }
-      int rc = 0;
-      for (const auto& t : taken)
-        if (!rc) rc = byteps_prophet_add_task(pq, &t);
+      const int rc = bpsr::prophet_add_many(pq, taken.data(), taken.size());
       taken.clear();
       if (rc) {
         std::lock_guard<std::mutex> g(mu);
@@ -244,6 +232,49 @@ int byteps_prophet_loop_push(byteps_prophet_loop* l, const byteps_prophet_task* 
   return 0;
 }
 
+int byteps_prophet_loop_push_many(byteps_prophet_loop* l, const byteps_prophet_task* tasks,
+                                  int32_t n) {
+  if (!l || (!tasks && n > 0) || n < 0)
+    return bpsr::fail(BYTEPS_REDUCE_EARGS, "null loop or tasks, or n < 0");
+  {
+    std::lock_guard<std::mutex> g(l->mu);
+    if (!l->active) return bpsr::fail(BYTEPS_REDUCE_EARGS, "no iteration begun");
+    // all or nothing: a bad task leaves no partition of the call marked
+    for (int32_t i = 0; i < n; ++i) {
+      const uint64_t h = tasks[i].handle;
+      const bool out = h >= l->block_of.size();
+      if (out || l->got[h]) {
+        for (int32_t k = 0; k < i; ++k) l->got[tasks[k].handle] = 0;
+        if (out)
+          return bpsr::fail(BYTEPS_REDUCE_EARGS, "handle %llu outside the table (%zu partitions)",
+                            (unsigned long long)h, l->block_of.size());
+        return bpsr::fail(BYTEPS_REDUCE_EARGS, "partition %llu pushed twice in one iteration",
+                          (unsigned long long)h);
+      }
+      l->got[h] = 1;
+    }
+  }
+  if (n == 0) return 0;
+  if (l->inline_drain) {
+    if (const int rc = bpsr::prophet_add_many(l->pq, tasks, (size_t)n)) {
+      std::lock_guard<std::mutex> g(l->mu);  // refused whole: none counts as pushed
+      for (int32_t i = 0; i < n; ++i) l->got[tasks[i].handle] = 0;
+      return rc;
+    }
+    return l->drain();
+  }
+  {
+    std::lock_guard<std::mutex> g(l->inbox_mu);
+    l->inbox.insert(l->inbox.end(), tasks, tasks + n);
+  }
+  l->pushes.fetch_add(1);
+  if (l->waiting.load()) {
+    std::lock_guard<std::mutex> g(l->mu);
+    l->cv.notify_one();
+  }
+  return 0;
+}
+
 int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s) {
   if (!l) return bpsr::fail(BYTEPS_REDUCE_EARGS, "null loop");
   std::unique_lock<std::mutex> lk(l->mu);
@@ -269,6 +300,13 @@ int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s) {
     return bpsr::fail(BYTEPS_REDUCE_ETIMEOUT,
                       "iteration not complete after %.3f s: %d of %d blocks released", timeout_s,
                       l->blocks_released, l->nblocks());
+  return 0;
+}
+
+int byteps_prophet_loop_release_calls(byteps_prophet_loop* l, uint64_t* calls) {
+  if (!l || !calls) return bpsr::fail(BYTEPS_REDUCE_EARGS, "null argument");
+  std::lock_guard<std::mutex> g(l->mu);
+  *calls = l->release_calls;
   return 0;
 }
 

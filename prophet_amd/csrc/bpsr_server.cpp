@@ -47,6 +47,20 @@ struct FoldJob {
   std::vector<int> order;  // arrival order of the finished round
 };
 
+// A copying pull of device memory waiting for the lane's issuer (combining):
+// the issuer issues the pulls that piled up as ONE batched copy on the d2h
+// stream and hands each its batch's completion event.
+struct PullReq {
+  KeyState* ks = nullptr;
+  void* dst = nullptr;
+  size_t len = 0;
+  hipEvent_t ev = nullptr;  // set by the issuer with done
+  int rc = 0;
+  bool done = false;
+};
+
+constexpr int kBatchEvents = 32;  // per lane, reused round robin
+
 struct Lane {
   hipStream_t fold = nullptr;  // folds, in round order per key
   hipStream_t copy = nullptr;  // push copies
@@ -66,13 +80,21 @@ struct Lane {
   // (every push copy of the lane so far); batched calls wait for fold_mark /
   // d2h_mark once per lane instead of one event per key.
   hipEvent_t copy_mark = nullptr, fold_mark = nullptr, d2h_mark = nullptr;
-  // Completed rounds of single-key calls waiting to be issued (combining, no
-  // scheduling): the first caller to find no issuer active becomes it and
-  // issues everything queued — one batched launch for what piled up while it
-  // was launching — until the list is empty (issue_combined).
+  // Combining (no scheduling, no engine blocking): the rounds single-key
+  // calls complete and their device pulls go to the lane's issuer thread,
+  // which issues what piled up — ONE batched fold launch for the rounds, ONE
+  // batched copy for the pulls — while the callers go on (issuer_main).
   std::mutex comb_mu;
+  std::condition_variable comb_cv;   // work for the issuer
+  std::condition_variable pull_cv;   // issued pulls -> their callers
   std::vector<FoldJob> comb;
-  bool comb_active = false;
+  std::vector<PullReq*> pullq;
+  bool comb_stop = false;
+  std::thread issuer;
+  // per-batch completion events (a key of a batch waits on its batch's event,
+  // not on a lane mark that later batches re-record)
+  hipEvent_t batch_ev[kBatchEvents] = {};
+  uint64_t batch_seq = 0;
 };
 
 // A pull ready to be answered, or a push to acknowledge, by the responder.
@@ -149,7 +171,13 @@ struct byteps_server {
   byteps_server_config cfg;
   bool schedule = false;
   bool blocking = false;  // BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:324)
-  bool combine = true;    // coalesce single-key calls' folds per lane (BPSR_SERVER_COMBINE)
+  // lane issuer threads batch single-key calls' folds and device pulls
+  // (BPSR_SERVER_COMBINE=0: each call issues its own; off with scheduling or
+  // engine blocking, whose orders and completion rules are per call)
+  bool combine = true;
+  // telemetry (byteps_server_stats)
+  std::atomic<uint64_t> n_fold_launches{0}, n_rounds_folded{0}, n_pull_launches{0},
+      n_pulls{0};
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
@@ -418,15 +446,16 @@ void responder_main(byteps_server* s) {
 // A round's fold is issued: publish it (caller holds ks->mu).  `mark`: also
 // raise the lane's fold mark (a batched issue raises it once, before).
 int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
-                 bool mark = true) {
+                 bool mark = true, hipEvent_t batch = nullptr) {
   Lane& L = *s->lanes[ks->lane];
+  s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
   if (mark) {  // a single fold: its own event, and the lane's mark
     hipError_t e = hipEventRecord(ks->done, L.fold);
     if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
     ks->fold_ev = ks->done;
-  } else {     // batched: the mark raised behind the batch stands for it
-    ks->fold_ev = L.fold_mark;
+  } else {     // batched: the batch's own event (or the lane mark behind it)
+    ks->fold_ev = batch ? batch : L.fold_mark;
   }
   ks->has_done = true;
   int rc = 0;
@@ -464,6 +493,7 @@ int execute(byteps_server* s, const FoldJob& j) {
   hipError_t we = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
   if (we == hipSuccess && ks->mirrored) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
   if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+  s->n_fold_launches.fetch_add(1, std::memory_order_relaxed);
   int rc = 0;
   switch (j.kind) {
     case kSumRecv:  // SUM_RECV (server.cc:117-139): merged (= first arrival's slot) += push
@@ -471,6 +501,7 @@ int execute(byteps_server* s, const FoldJob& j) {
     case kAsyncSum: {  // server.cc:220-230: every push is summed straight into the store
       rc = byteps_reduce_sum(ks->store, ks->slot[j.w], ks->len, ks->dtype, fs);
       if (rc) return rc;
+      s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
       hipError_t e = hipEventRecord(ks->done, L.fold);
       if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
       if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -662,15 +693,19 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
     if (!rc)
       rc = batched_with_ring(d.data(), (int)d.size(), jobs[i].ks->dtype,
                              BYTEPS_REDUCE_MODE_REFERENCE, L.fold, L.ring);
+    hipEvent_t bev = nullptr;
     if (!rc) {  // raised before any round is published: a pull that sees one waits past it
-      hipError_t me = hipEventRecord(L.fold_mark, L.fold);
+      s->n_fold_launches.fetch_add(1, std::memory_order_relaxed);
+      bev = L.batch_ev[L.batch_seq++ % kBatchEvents];
+      hipError_t me = hipEventRecord(bev, L.fold);
+      if (me == hipSuccess) me = hipEventRecord(L.fold_mark, L.fold);
       if (me != hipSuccess) rc = hip_fail(me, "hipEventRecord");
     }
     for (size_t k = i; k < e; ++k) {
       KeyState* ks = jobs[k].ks;
       std::lock_guard<std::mutex> g(ks->mu);
       ks->pending--;
-      const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false);
+      const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false, bev);
       if (r2) fail_key(s, ks, r2);
       ks->cv.notify_all();
     }
@@ -702,46 +737,107 @@ int issue_one(byteps_server* s, FoldJob& j) {
   return rc;
 }
 
-// Combining issue of the rounds single-key calls completed (defer lists of
-// arrive; caller holds no key lock).  Each lane keeps one list: a caller
-// appends its rounds; if no issuer is active it becomes the issuer and issues
-// the list — one fold launch for a lone round, ONE batched launch for rounds
-// that piled up meanwhile (other workers' calls completing keys while it was
-// launching) — until the list is empty.  So an uncontended call issues its
-// fold at once, and concurrent calls share launches instead of queueing one
-// each (the reference engine's per-message sums, server.cc:70-145, paid per
-// key on the host too).  A fold that fails fails its key (fail_key).
+// Hand the rounds a single-key call completed (defer lists of arrive; caller
+// holds no key lock) to their lanes' issuer threads.  The call returns at
+// once: the round is published (pulls may go) when the issuer has issued its
+// fold.  Keys arriving together — the last worker of many keys, or several
+// workers' calls at once — thus share ONE batched launch per lane instead of
+// one launch each, and no caller issues other callers' folds.  The reference
+// engine pays a host sum per message (server.cc:70-145); here the host work
+// per round is an append and a wake-up.
 int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs) {
-  if (jobs.empty()) return 0;
-  int first_rc = 0;
-  std::stable_sort(jobs.begin(), jobs.end(),
-                   [](const FoldJob& a, const FoldJob& b) { return a.ks->lane < b.ks->lane; });
-  size_t i = 0;
-  while (i < jobs.size()) {
-    const int lane = jobs[i].ks->lane;
-    Lane& L = *s->lanes[lane];
-    bool issuer = false;
-    {
-      std::lock_guard<std::mutex> g(L.comb_mu);
-      for (; i < jobs.size() && jobs[i].ks->lane == lane; ++i) L.comb.push_back(std::move(jobs[i]));
-      if (!L.comb_active) issuer = L.comb_active = true;
-    }
-    while (issuer) {
-      std::vector<FoldJob> take;
-      {
-        std::lock_guard<std::mutex> g(L.comb_mu);
-        if (L.comb.empty()) {
-          L.comb_active = false;
-          break;
-        }
-        take.swap(L.comb);
-      }
-      const int rc = take.size() == 1 ? issue_one(s, take[0]) : flush_folds(s, take);
-      if (rc && !first_rc) first_rc = rc;
-    }
+  for (auto& j : jobs) {
+    Lane& L = *s->lanes[j.ks->lane];
+    std::lock_guard<std::mutex> g(L.comb_mu);
+    L.comb.push_back(std::move(j));
+    L.comb_cv.notify_one();
   }
   jobs.clear();
-  return first_rc;
+  return 0;
+}
+
+// Issue the device pulls that piled up on a lane: per lane ONE wait for the
+// lane's folds so far (every pulled round was published, so issued, before its
+// pull was queued), ONE batched copy, ONE event every request then waits for.
+void issue_pulls(byteps_server* s, Lane& L, std::vector<PullReq*>& reqs) {
+  int rc = 0;
+  hipEvent_t bev = nullptr;
+  {
+    std::lock_guard<std::mutex> bg(L.batch_mu);
+    hipError_t e = hipStreamWaitEvent(L.d2h, L.fold_mark, 0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    std::vector<byteps_bucket_desc> d(reqs.size());
+    for (size_t k = 0; k < reqs.size() && !rc; ++k) {
+      std::memset(&d[k], 0, sizeof(d[k]));
+      d[k].dst = reqs[k]->dst;
+      d[k].srcs[0] = reqs[k]->ks->store;
+      d[k].len = reqs[k]->len;
+      d[k].n = 1;
+    }
+    if (!rc)
+      rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
+                             BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring);
+    if (!rc) {
+      s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
+      bev = L.batch_ev[L.batch_seq++ % kBatchEvents];
+      e = hipEventRecord(bev, L.d2h);
+      if (e == hipSuccess) e = hipEventRecord(L.d2h_mark, L.d2h);
+      if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(L.comb_mu);
+    for (PullReq* r : reqs) {
+      r->rc = rc;
+      r->ev = bev;
+      r->done = true;
+    }
+  }
+  L.pull_cv.notify_all();
+  reqs.clear();
+}
+
+// The lane's issuer thread (combining): folds first, then pulls, each as one
+// batch of whatever piled up since the last issue.  Drains before it exits.
+void issuer_main(byteps_server* s, int lane) {
+  (void)hipSetDevice(s->cfg.device);
+  Lane& L = *s->lanes[lane];
+  std::vector<FoldJob> folds;
+  std::vector<PullReq*> pulls;
+  std::unique_lock<std::mutex> lk(L.comb_mu);
+  for (;;) {
+    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty() || !L.pullq.empty(); });
+    if (L.comb.empty() && L.pullq.empty()) return;  // stopping, drained
+    folds.swap(L.comb);
+    pulls.swap(L.pullq);
+    lk.unlock();
+    if (folds.size() == 1)
+      (void)issue_one(s, folds[0]);
+    else if (!folds.empty())
+      (void)flush_folds(s, folds);  // a failed fold fails its keys (fail_key)
+    folds.clear();
+    if (!pulls.empty()) issue_pulls(s, L, pulls);
+    lk.lock();
+  }
+}
+
+// A copying pull of device memory through the lane's issuer: queue it, wait
+// until it is issued, then for its batch's copy.  Caller holds no key lock.
+int pull_via_issuer(byteps_server* s, KeyState* ks, void* out, size_t len) {
+  Lane& L = *s->lanes[ks->lane];
+  PullReq r;
+  r.ks = ks;
+  r.dst = out;
+  r.len = len;
+  {
+    std::unique_lock<std::mutex> lk(L.comb_mu);
+    L.pullq.push_back(&r);
+    L.comb_cv.notify_one();
+    L.pull_cv.wait(lk, [&] { return r.done; });
+  }
+  if (r.rc) return r.rc;
+  hipError_t e = hipEventSynchronize(r.ev);
+  return e == hipSuccess ? 0 : hip_fail(e, "pull copy");
 }
 
 // After a single-key call issued (or queued) its round: the key's own error,
@@ -797,6 +893,14 @@ void destroy_lanes(byteps_server* s) {
     if (Lp && Lp->q) Lp->q->stop();
   for (auto& Lp : s->lanes)
     if (Lp && Lp->dispatcher.joinable()) Lp->dispatcher.join();
+  for (auto& Lp : s->lanes) {
+    if (!Lp) continue;
+    std::lock_guard<std::mutex> g(Lp->comb_mu);
+    Lp->comb_stop = true;
+    Lp->comb_cv.notify_all();
+  }
+  for (auto& Lp : s->lanes)  // the issuers issue what is queued, then exit
+    if (Lp && Lp->issuer.joinable()) Lp->issuer.join();
 }
 
 }  // namespace
@@ -838,6 +942,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   s->blocking = cfg->engine_blocking != 0;
   if (const char* fa = getenv("BPSR_SERVER_FAIL_AFTER")) s->fail_after = atol(fa);
   if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
+  if (s->schedule || s->blocking) s->combine = false;
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
@@ -867,6 +972,10 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
     L.ring = stage_ring_create();
     for (hipEvent_t* m : {&L.copy_mark, &L.fold_mark, &L.d2h_mark})
       if (e == hipSuccess) e = hipEventCreateWithFlags(m, hipEventDisableTiming);
+    for (hipEvent_t& b : L.batch_ev) {
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(b, L.fold);
+    }
     // recorded once on their (empty) streams: waiting on them is a no-op until
     // the lane issues work
     if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
@@ -881,6 +990,9 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
     if (s->schedule)
       for (int i = 0; i < cfg->engine_lanes; ++i)
         s->lanes[i]->dispatcher = std::thread(dispatcher_main, s.get(), i);
+    if (s->combine)
+      for (int i = 0; i < cfg->engine_lanes; ++i)
+        s->lanes[i]->issuer = std::thread(issuer_main, s.get(), i);
     s->responder = std::thread(responder_main, s.get());
   } catch (...) {
     byteps_server_destroy(s.release());
@@ -936,6 +1048,8 @@ int byteps_server_destroy(byteps_server* s) {
     if (Lp->ring) stage_ring_destroy(Lp->ring);
     for (hipEvent_t m : {Lp->copy_mark, Lp->fold_mark, Lp->d2h_mark})
       if (m) (void)hipEventDestroy(m);
+    for (hipEvent_t b : Lp->batch_ev)
+      if (b) (void)hipEventDestroy(b);
   }
   delete s;
   return BYTEPS_REDUCE_OK;
@@ -1065,6 +1179,18 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
+  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
+  if (s->combine && location == BYTEPS_SERVER_DEVICE && !s->cfg.async_mode) {
+    // sync mode: the store holds this round until every worker has pulled it
+    // (the next round needs this worker's next push), so the copy can wait
+    // for the lane's issuer and go out with the pulls that piled up
+    lk.unlock();
+    if ((rc = pull_via_issuer(s, ks, out, len))) return rc;
+    lk.lock();
+    count_pull(s, ks);  // server.cc:105-113
+    return BYTEPS_REDUCE_OK;
+  }
+  s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
   // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
   // pull_by_kernel).  No per-thread
@@ -1157,6 +1283,7 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
     if (e != hipSuccess) return hip_fail(e, "store fold sync");
   }
   lk.lock();
+  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   *data = view;
   if (len) *len = ks->len;
@@ -1193,7 +1320,8 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
   if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
   KeyState* ks = get_key(s, key, false);
   if (!ks) return fail(BYTEPS_REDUCE_EARGS, "unknown key");
-  std::lock_guard<std::mutex> g(ks->mu);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  ks->cv.wait(lk, [&] { return ks->pending == 0 || ks->error; });  // rounds handed to the issuer
   if (rounds) *rounds = ks->rounds;
   if (lane) *lane = ks->lane;
   if (last_order)
@@ -1383,6 +1511,7 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
                                   BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring);
         if (r) return r;
       }
+      s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
       if ((e = hipEventRecord(L.d2h_mark, L.d2h)) != hipSuccess)
         return hip_fail(e, "hipEventRecord");
       touched[l] = 1;
@@ -1433,6 +1562,15 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
     std::lock_guard<std::mutex> g(ks_of[i]->mu);
     count_pull(s, ks_of[i]);  // server.cc:105-113
   }
+  s->n_pulls.fetch_add((uint64_t)n, std::memory_order_relaxed);
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
+  if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  const uint64_t v[4] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+                         s->n_pull_launches.load(), s->n_pulls.load()};
+  for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

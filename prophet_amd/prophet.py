@@ -64,6 +64,7 @@ PROPHET_EXPORTS = (
     "byteps_prophet_get_state", "byteps_prophet_reset", "byteps_prophet_release_groups",
     "byteps_prophet_profile", "byteps_prophet_estimate_net_b",
     "byteps_prophet_loop_create", "byteps_prophet_loop_begin", "byteps_prophet_loop_push",
+    "byteps_prophet_loop_push_many", "byteps_prophet_loop_release_calls",
     "byteps_prophet_loop_end", "byteps_prophet_loop_destroy",
 )
 
@@ -92,6 +93,8 @@ def _lib():
                                                  ctypes.c_int32, vp, ctypes.c_int, P(vp)]
         L.byteps_prophet_loop_begin.argtypes = [vp, vp]
         L.byteps_prophet_loop_push.argtypes = [vp, P(_Task)]
+        L.byteps_prophet_loop_push_many.argtypes = [vp, P(_Task), ctypes.c_int32]
+        L.byteps_prophet_loop_release_calls.argtypes = [vp, P(ctypes.c_uint64)]
         L.byteps_prophet_loop_end.argtypes = [vp, ctypes.c_double]
         L.byteps_prophet_loop_destroy.argtypes = [vp]
         L.byteps_prophet_estimate_net_b.argtypes = [P(ctypes.c_int64)] * 3 + [
@@ -236,6 +239,31 @@ class PushLoop:
         c = _Task(task.grad, task.part, task.len, task.total_partnum, int(task.scheduled),
                   task.key, int(index))
         _ck(self._L.byteps_prophet_loop_push(self._h, ctypes.byref(c)))
+
+    def make_batch(self, tasks, indices):
+        """A reusable native array of (task, table index) pairs for
+        ``push_many`` (build it once per arrival set, push it every iteration)."""
+        arr = (_Task * max(len(tasks), 1))()
+        for i, (t, ix) in enumerate(zip(tasks, indices)):
+            arr[i] = _Task(t.grad, t.part, t.len, t.total_partnum, int(t.scheduled), t.key,
+                           int(ix))
+        return arr, len(tasks)
+
+    def push_many(self, batch) -> None:
+        """Push partitions that landed together (``make_batch``'s result, or a
+        list of (task, index) pairs): one scheduler drain, their release groups
+        released together."""
+        if not isinstance(batch, tuple):
+            pairs = list(batch)
+            batch = self.make_batch([t for t, _ in pairs], [i for _, i in pairs])
+        arr, n = batch
+        _ck(self._L.byteps_prophet_loop_push_many(self._h, arr, int(n)))
+
+    def release_calls(self) -> int:
+        """Release kernels (or host releases) issued since the loop was made."""
+        n = ctypes.c_uint64()
+        _ck(self._L.byteps_prophet_loop_release_calls(self._h, ctypes.byref(n)))
+        return n.value
 
     def end(self, timeout_s: float = 10.0) -> None:
         """Wait until every block has been released; with the consumer on the

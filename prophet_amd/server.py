@@ -23,7 +23,7 @@ SERVER_EXPORTS = (
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
     "byteps_server_debug_lane", "byteps_server_push_ready_many", "byteps_server_push_many",
-    "byteps_server_pull_many", "byteps_server_pull_device_view",
+    "byteps_server_pull_many", "byteps_server_pull_device_view", "byteps_server_stats",
     "byteps_server_key_hash", "byteps_server_group_config_from_env", "byteps_server_route",
     "byteps_server_group_create", "byteps_server_group_destroy", "byteps_server_group_route",
     "byteps_server_group_instance", "byteps_server_group_init_key", "byteps_server_group_push",
@@ -85,6 +85,7 @@ def _lib():
         L.byteps_server_pull_device_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
                                                      ctypes.POINTER(_sz)]
         L.byteps_server_pull_async.argtypes = [_vp, _u64, PULL_CB, _vp]
+        L.byteps_server_stats.argtypes = [_vp, ctypes.POINTER(_u64), _int]
         L.byteps_server_push_async.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int, PUSH_CB,
                                                _vp]
         L.byteps_server_key_info.argtypes = [_vp, _u64, ctypes.POINTER(_u64),
@@ -286,6 +287,13 @@ class PSServer:
         _check(self.lib.byteps_server_key_info(self.handle, key, ctypes.byref(rounds),
                                                ctypes.byref(lane), order, self.cfg.num_workers))
         return int(rounds.value), int(lane.value), list(order)
+
+    def stats(self) -> dict:
+        """Launch telemetry since create (byteps_server_stats)."""
+        out = (_u64 * 4)()
+        _check(self.lib.byteps_server_stats(self.handle, out, 4))
+        return {"fold_launches": out[0], "rounds_folded": out[1], "pull_launches": out[2],
+                "pulls": out[3]}
 
     # batched calls (server.h): one lane-wide launch for many keys
     def push_ready_many(self, keys, worker: int) -> None:

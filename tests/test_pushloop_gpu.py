@@ -115,6 +115,48 @@ def test_push_loop_iterations_exact(net_b, inline, host):
         assert np.array_equal(S["out"][a:a + ln].cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("inline", [False, True], ids=["thread", "inline"])
+def test_push_loop_push_many_exact(inline):
+    """push_many: partitions that landed together in one call (one drain, the
+    release groups ready together released as one kernel per run of blocks).
+    Config 3's partitions in three batches per iteration (the last holds the
+    rest), three iterations, bit-exact; a batch with a bad task is refused
+    whole — none of its partitions counts as pushed."""
+    from prophet_amd.prophet import PushLoop
+    from prophet_amd.reducer import ReduceError
+    S = _setup(seed=9)
+    cons = S["bq"].stream()
+    rel = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=inline)
+    tasks = S["tasks"]
+    cuts = [0, 40, 41, len(tasks)]
+    batches = [loop.make_batch([t for t, _ in tasks[a:b]], [i for _, i in tasks[a:b]])
+               for a, b in zip(cuts, cuts[1:])]
+    import gc
+    gc.collect()
+    for it in range(3):
+        S["out"].zero_()
+        torch.cuda.synchronize()
+        loop.begin(cons)
+        if it == 1:
+            t0, i0 = tasks[0]
+            with pytest.raises(ReduceError, match="twice"):
+                loop.push_many([(t0, i0), (t0, i0)])
+            with pytest.raises(ReduceError, match="outside the table"):
+                loop.push_many([(t0, i0), (t0, 10_000)])
+        c0 = loop.release_calls()
+        for b in batches:
+            loop.push_many(b)
+        loop.end(timeout_s=10.0)
+        # at most one release kernel per batch (per run of blocks it completed)
+        assert 1 <= loop.release_calls() - c0 <= S["nb"]
+        torch.cuda.synchronize()
+        S["bq"].status(cons)
+        assert torch.equal(S["out"], S["ref"].view(torch.uint8)), f"iteration {it}"
+    loop.close()
+
+
 def test_push_loop_errors_and_missing_partition():
     from prophet_amd.prophet import PushLoop
     from prophet_amd.reducer import ReduceError

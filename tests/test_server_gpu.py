@@ -768,6 +768,82 @@ def test_batched_calls_many_keys(port, policy, dt):
     srv.close()
 
 
+@pytest.mark.parametrize("combine", ["1", "0"], ids=["issuer", "per_call"])
+@pytest.mark.parametrize("dt", [DType.FLOAT16, DType.FLOAT32], ids=lambda d: DType(d).name)
+def test_single_key_calls_issuer_batches(port, dt, combine, monkeypatch):
+    """Single-key calls from 8 worker threads — push_ready into written slots
+    and copying pulls into device memory, 60 keys on 4 lanes, three rounds —
+    through the lanes' issuer threads (rounds and pulls that pile up go out as
+    one batched launch each) and with BPSR_SERVER_COMBINE=0 (every call issues
+    its own): every pulled byte equals the oracle's fold in the recorded
+    arrival order.  With the issuer, every round is folded once and every pull
+    answered once (telemetry), in no more launches than rounds."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_COMBINE", combine)
+    N, R = 8, 3
+    sizes = [1 + (j * 7919) % 50_000 for j in range(60)]
+    es = elem_size(dt)
+    keys = list(range(7, 7 + len(sizes)))
+    srv = PSServer(N, engine_lanes=4)
+    dev = torch.device("cuda:0")
+    host = {(w, r, j): data(dt, n, w, r, j) for w in range(N) for r in range(R + 1)
+            for j, n in enumerate(sizes)}
+    outs = {(w, r): [torch.empty(n * es, dtype=torch.uint8, device=dev) for n in sizes]
+            for w in range(N) for r in range(1, R + 1)}
+    bar = threading.Barrier(N + 1)
+    errors, orders = [], {}
+
+    def worker(w):
+        try:
+            for j, k in enumerate(keys):    # init pushes, device sources
+                srv.push(k, w, torch.from_numpy(host[(w, 0, j)]).to(dev), dt)
+            for r in range(1, R + 1):
+                for j, k in enumerate(keys):
+                    _copy_to_ptr(srv.recv_slot(k, w), torch.from_numpy(host[(w, r, j)]).to(dev))
+                bar.wait(timeout=120)       # every slot written: the round's pushes
+                for k in keys:
+                    srv.push_ready(k, w)
+                for j, k in enumerate(keys):
+                    srv.pull(k, outs[(w, r)][j])
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    st0 = None
+    for r in range(1, R + 1):
+        bar.wait(timeout=240)
+        if st0 is None:
+            st0 = srv.stats()
+        bar.wait(timeout=240)
+        for j, k in enumerate(keys):
+            rounds, _, order = srv.key_info(k)
+            assert rounds == r
+            orders[(r, j)] = order
+        bar.wait(timeout=120)
+    for t in ts:
+        t.join(timeout=60)
+    assert not errors, errors
+    st = srv.stats()
+    srv.close()
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [host[(w, r, j)] for w in orders[(r, j)]], n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, outs[(w, r)][j].cpu().numpy(), want,
+                                   nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
+    folded = st["rounds_folded"] - st0["rounds_folded"]
+    pulls = st["pulls"] - st0["pulls"]
+    assert folded == R * len(keys) and pulls == R * len(keys) * N
+    assert st["fold_launches"] - st0["fold_launches"] <= folded
+    assert st["pull_launches"] - st0["pull_launches"] <= pulls
+
+
 def _copy_to_ptr(ptr, src):
     """Device copy of tensor `src` to raw device pointer `ptr` (the transport
     writing into a receive slot)."""

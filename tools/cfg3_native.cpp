@@ -337,6 +337,18 @@ int main(int argc, char** argv) {
     sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     ++sched_iters;
   };
+  // the same with every partition in one push_many (they have all landed):
+  // one drain, the ready release groups released as one range
+  const Fn push_loop_inline_many = [&](int i) {
+    const int k = i % kSets;
+    const auto t0 = std::chrono::steady_clock::now();
+    CKR(byteps_prophet_loop_begin(iloops[k], cons));
+    CKR(byteps_prophet_loop_push_many(iloops[k], tasks.arrivals.data(),
+                                      (int32_t)tasks.arrivals.size()));
+    CKR(byteps_prophet_loop_end(iloops[k], 5.0));
+    sched_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    ++sched_iters;
+  };
   const Fn plan_no_blocks = [&](int i) {
     CKR(byteps_reduce_plan_launch(sets[i % kSets].plan_blocks, cons));
   };
@@ -370,6 +382,7 @@ int main(int argc, char** argv) {
     }
     variants.push_back({"blockq_prophet_push_loop", &push_loop});
     variants.push_back({"blockq_prophet_push_loop_inline", &push_loop_inline});
+    variants.push_back({"blockq_prophet_push_loop_inline_many", &push_loop_inline_many});
     // host releases (data resident): separate block queues, since enabling
     // host releases adds the forwarding workgroup to every later launch
     for (int k = 0; k < kSets; ++k) {

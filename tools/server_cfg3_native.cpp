@@ -132,6 +132,8 @@ int main(int argc, char** argv) {
                        hipMemcpyDeviceToDevice));
         }
     }
+    uint64_t st0[4] = {0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st0, 4));
     // persistent worker threads (a transport's receive threads), released per
     // round by the driver and joined by a countdown
     std::vector<double> ts;
@@ -139,12 +141,22 @@ int main(int argc, char** argv) {
     std::condition_variable cv;
     int go = -1, left = 0;
     const int total_rounds = rounds + 2 + (view ? 1 : 0);  // + a checking round
+    // when each worker's pushes of the round returned (ns since the epoch of
+    // steady_clock): the round splits into push phase (max) and pull phase
+    std::vector<std::atomic<int64_t>> push_done(N);
+    auto stamp = [&](int k) {
+      push_done[k].store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             std::chrono::steady_clock::now().time_since_epoch())
+                             .count());
+    };
+    std::vector<double> push_ts;
     auto one_round = [&](int k, int r) {
       if (view && r < rounds + 2) {  // zero-copy: every pull is a view of the store
         if (many)
           CKR(byteps_server_push_ready_many(srv, keys.data(), np, k));
         else
           for (int i = 0; i < np; ++i) CKR(byteps_server_push_ready(srv, (uint64_t)i, k));
+        stamp(k);
         for (int i = 0; i < np; ++i) {
           const void* v = nullptr;
           size_t vl = 0;
@@ -165,6 +177,7 @@ int main(int argc, char** argv) {
             else
               CKR(byteps_server_push_many(srv, keys.data(), srcs.data(), lens.data(), np, k,
                                           BYTEPS_REDUCE_FLOAT16, BYTEPS_SERVER_DEVICE));
+            stamp(k);
             CKR(byteps_server_pull_many(srv, keys.data(), dsts.data(), lens.data(), np,
                                         BYTEPS_SERVER_DEVICE));
             return;
@@ -177,6 +190,7 @@ int main(int argc, char** argv) {
                                            parts[i].second, BYTEPS_REDUCE_FLOAT16,
                                            BYTEPS_SERVER_DEVICE, on_push, nullptr));
           }
+          stamp(k);
           for (int i = 0; i < np; ++i)
             CKR(byteps_server_pull(srv, (uint64_t)i, out[k] + parts[i].first, parts[i].second,
                                    BYTEPS_SERVER_DEVICE));
@@ -210,7 +224,14 @@ int main(int argc, char** argv) {
       if (variant == 1)
         while (acks.load() < (long)N * np) std::this_thread::yield();
       const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      if (r >= 2 && r < rounds + 2) ts.push_back(s);
+      if (r >= 2 && r < rounds + 2) {
+        ts.push_back(s);
+        int64_t last = 0;
+        for (int k = 0; k < N; ++k) last = std::max(last, push_done[k].load());
+        const int64_t t0ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 t0.time_since_epoch()).count();
+        push_ts.push_back((double)(last - t0ns) * 1e-9);
+      }
     }
     for (auto& t : th) t.join();
     // exactness: every worker's pull equals worker 0's (one store per key)
@@ -223,13 +244,22 @@ int main(int argc, char** argv) {
     }
     std::sort(ts.begin(), ts.end());
     const double med = ts[ts.size() / 2];
+    std::sort(push_ts.begin(), push_ts.end());
+    const double push_med = push_ts[push_ts.size() / 2];
+    uint64_t st[4] = {0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st, 4));
+    for (int i = 0; i < 4; ++i) st[i] -= st0[i];
     printf("{\"config\": \"cfg3_via_server\", \"driver\": \"native C++ threads "
            "(tools/server_cfg3_native.cpp)\", \"variant\": \"%s\", \"n_workers\": %d, "
            "\"keys\": %d, \"lanes\": %d, \"bytes_per_worker\": %zu, \"round_ms\": %.4f, "
            "\"min_ms\": %.4f, \"us_per_key\": %.2f, \"hbm_frac_of_round\": %.4f, "
+           "\"push_phase_ms\": %.4f, \"fold_launches_per_round\": %.1f, "
+           "\"rounds_folded_per_round\": %.1f, \"pull_launches_per_round\": %.1f, "
            "\"pulls_agree\": %s}\n",
            names[variant], N, np, lanes, total, med * 1e3,
-           ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, same ? "true" : "false");
+           ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, push_med * 1e3,
+           (double)st[0] / total_rounds, (double)st[1] / total_rounds,
+           (double)st[2] / total_rounds, same ? "true" : "false");
     fflush(stdout);
     CKR(byteps_server_destroy(srv));
   }
