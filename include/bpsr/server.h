@@ -117,9 +117,7 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
 int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 
 /* A worker's pull: blocks until the key's current round is finished (sync mode),
- * then copies the store (len bytes) to `out`.  Device destinations in sync mode
- * go through the lane's issuer thread: the pulls that piled up are copied by
- * ONE batched copy launch. */
+ * then copies the store (len bytes) to `out`. */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
 /* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
@@ -173,7 +171,7 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
 
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
- * views); the first n of them. */
+ * views), out[4] ns the lane issuer threads spent issuing; the first n. */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

@@ -165,8 +165,11 @@ int elem_size(int dtype);  // 0 if unsupported
 struct StageRing;
 StageRing* stage_ring_create();
 void stage_ring_destroy(StageRing* r);
+// *done (optional): the event recorded behind the launch (the staging slot's
+// guard; re-recorded only after a host wait for this launch, when the slot is
+// reused), so a caller can wait for the launch without recording its own.
 int batched_with_ring(const struct byteps_bucket_desc* buckets, int nbuckets, int dtype,
-                      int mode, hipStream_t s, StageRing* ring);
+                      int mode, hipStream_t s, StageRing* ring, hipEvent_t* done = nullptr);
 
 // Thread-local error reporting (byteps_reduce_last_error): fail() is in
 // bpsr_error.h; hip_fail formats a HIP error the same way.

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -47,20 +48,6 @@ struct FoldJob {
   std::vector<int> order;  // arrival order of the finished round
 };
 
-// A copying pull of device memory waiting for the lane's issuer (combining):
-// the issuer issues the pulls that piled up as ONE batched copy on the d2h
-// stream and hands each its batch's completion event.
-struct PullReq {
-  KeyState* ks = nullptr;
-  void* dst = nullptr;
-  size_t len = 0;
-  hipEvent_t ev = nullptr;  // set by the issuer with done
-  int rc = 0;
-  bool done = false;
-};
-
-constexpr int kBatchEvents = 32;  // per lane, reused round robin
-
 struct Lane {
   hipStream_t fold = nullptr;  // folds, in round order per key
   hipStream_t copy = nullptr;  // push copies
@@ -81,20 +68,28 @@ struct Lane {
   // d2h_mark once per lane instead of one event per key.
   hipEvent_t copy_mark = nullptr, fold_mark = nullptr, d2h_mark = nullptr;
   // Combining (no scheduling, no engine blocking): the rounds single-key
-  // calls complete and their device pulls go to the lane's issuer thread,
-  // which issues what piled up — ONE batched fold launch for the rounds, ONE
-  // batched copy for the pulls — while the callers go on (issuer_main).
+  // calls complete go to the lane's issuer thread, which issues what piled up
+  // as ONE batched fold launch while the callers go on (issuer_main).
   std::mutex comb_mu;
   std::condition_variable comb_cv;   // work for the issuer
-  std::condition_variable pull_cv;   // issued pulls -> their callers
   std::vector<FoldJob> comb;
-  std::vector<PullReq*> pullq;
   bool comb_stop = false;
   std::thread issuer;
-  // per-batch completion events (a key of a batch waits on its batch's event,
-  // not on a lane mark that later batches re-record)
-  hipEvent_t batch_ev[kBatchEvents] = {};
-  uint64_t batch_seq = 0;
+  // Completion of what the issuer issued, tracked on the host so waiters make
+  // no HIP call (HIP calls serialise across threads: 8 threads syncing events
+  // per key cost 3.5 us each, tools/launch_cost.cpp): the issuer appends
+  // (seq, event) per launch, the lane's completer thread waits for them in
+  // order and publishes done_seq; a key remembers the seq of its last round.
+  std::mutex done_mu;
+  std::condition_variable cq_cv;    // issuer -> completer
+  std::condition_variable done_cv;  // completer -> waiters (and the issuer)
+  std::deque<std::pair<uint64_t, hipEvent_t>> cq;
+  uint64_t issued_seq = 0, done_seq = 0;
+  bool cq_stop = false;
+  std::thread completer;
+  // copies recorded into copy_mark so far / seen by a fold's wait on it (a
+  // fold stream already waiting on the latest copy mark need not wait again)
+  std::atomic<uint64_t> copy_seq{0}, fold_copy_seen{0};
 };
 
 // A pull ready to be answered, or a push to acknowledge, by the responder.
@@ -144,6 +139,7 @@ struct KeyState {
   // after a batched issue (flush_folds), which records no per-key event — the
   // lane's fold mark (a later record of it covers this fold too).
   hipEvent_t fold_ev = nullptr;
+  uint64_t fold_seq = 0;      // lane completion seq of the last issued round (0: untracked)
   hipEvent_t copied = nullptr;
   hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
   bool has_done = false;
@@ -175,9 +171,10 @@ struct byteps_server {
   // (BPSR_SERVER_COMBINE=0: each call issues its own; off with scheduling or
   // engine blocking, whose orders and completion rules are per call)
   bool combine = true;
+  uint64_t inflight = 2;  // issuer: launches queued or running per lane (BPSR_SERVER_INFLIGHT)
   // telemetry (byteps_server_stats)
   std::atomic<uint64_t> n_fold_launches{0}, n_rounds_folded{0}, n_pull_launches{0},
-      n_pulls{0};
+      n_pulls{0}, issuer_ns{0};
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
@@ -202,6 +199,45 @@ namespace {
 int set_device(const byteps_server* s) {
   hipError_t e = hipSetDevice(s->cfg.device);
   return e == hipSuccess ? 0 : hip_fail(e, "hipSetDevice");
+}
+
+// Make the lane's fold stream wait for its copies, unless it already waits
+// for the latest copy mark (push_ready-only rounds have no copies to wait for).
+hipError_t wait_copies(Lane& L) {
+  const uint64_t c = L.copy_seq.load();
+  if (c == L.fold_copy_seen.load()) return hipSuccess;
+  const hipError_t e = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+  if (e == hipSuccess) L.fold_copy_seen.store(c);
+  return e;
+}
+
+// Hand a launch's completion event to the lane's completer (combining):
+// returns its seq; done_seq >= seq once it has completed.
+uint64_t track(Lane& L, hipEvent_t ev) {
+  std::lock_guard<std::mutex> g(L.done_mu);
+  const uint64_t seq = ++L.issued_seq;
+  L.cq.emplace_back(seq, ev);
+  L.cq_cv.notify_one();
+  return seq;
+}
+
+// The lane's completer thread: waits for tracked launches in issue order and
+// publishes how far they have completed.
+void completer_main(byteps_server* s, int lane) {
+  (void)hipSetDevice(s->cfg.device);
+  Lane& L = *s->lanes[lane];
+  std::unique_lock<std::mutex> lk(L.done_mu);
+  for (;;) {
+    L.cq_cv.wait(lk, [&] { return L.cq_stop || !L.cq.empty(); });
+    if (L.cq.empty()) return;  // stopping, drained
+    const auto [seq, ev] = L.cq.front();
+    lk.unlock();
+    (void)hipEventSynchronize(ev);  // a failed launch failed its keys already
+    lk.lock();
+    L.cq.pop_front();
+    L.done_seq = seq;
+    L.done_cv.notify_all();
+  }
 }
 
 // server.h:138-162 GetThreadID: least accumulated bytes, sticky per key.
@@ -298,6 +334,7 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
                        L.copy);
   if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
   if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
+  if (e == hipSuccess) L.copy_seq.fetch_add(1);
   if (e == hipSuccess && wait) e = hipEventSynchronize(ks->copied);
   return e == hipSuccess ? 0 : hip_fail(e, "push copy");
 }
@@ -446,7 +483,7 @@ void responder_main(byteps_server* s) {
 // A round's fold is issued: publish it (caller holds ks->mu).  `mark`: also
 // raise the lane's fold mark (a batched issue raises it once, before).
 int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
-                 bool mark = true, hipEvent_t batch = nullptr) {
+                 bool mark = true, hipEvent_t batch = nullptr, uint64_t batch_seq = 0) {
   Lane& L = *s->lanes[ks->lane];
   s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
   if (mark) {  // a single fold: its own event, and the lane's mark
@@ -454,8 +491,10 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
     if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
     if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
     ks->fold_ev = ks->done;
+    ks->fold_seq = s->combine ? track(L, ks->done) : 0;
   } else {     // batched: the batch's own event (or the lane mark behind it)
     ks->fold_ev = batch ? batch : L.fold_mark;
+    ks->fold_seq = batch_seq;
   }
   ks->has_done = true;
   int rc = 0;
@@ -490,7 +529,7 @@ int execute(byteps_server* s, const FoldJob& j) {
   // before they finish; the copy stream is in order, so the lane's copy mark
   // covers every copy issued so far, batched ones included) and behind the
   // last mirror D2H of the store.
-  hipError_t we = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+  hipError_t we = wait_copies(L);
   if (we == hipSuccess && ks->mirrored) we = hipStreamWaitEvent(L.fold, ks->mirrored, 0);
   if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
   s->n_fold_launches.fetch_add(1, std::memory_order_relaxed);
@@ -506,6 +545,7 @@ int execute(byteps_server* s, const FoldJob& j) {
       if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
       if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
       ks->fold_ev = ks->done;
+      ks->fold_seq = 0;
       ks->has_done = true;
       ks->rounds++;
       ks->cv.notify_all();
@@ -590,7 +630,7 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     // every init push is counted: a failure from here on fails the key (the
     // other workers' init pushes wait for `inited || error`)
     int rc = injected_failure(s);
-    hipError_t we = rc ? hipSuccess : hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+    hipError_t we = rc ? hipSuccess : wait_copies(L);
     if (!rc && we != hipSuccess) rc = hip_fail(we, "hipStreamWaitEvent");
     if (!rc)
       rc = byteps_reduce_copy(ks->store, ks->slot[w], ks->len, reinterpret_cast<void*>(L.fold));
@@ -604,6 +644,7 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
       return rc;
     }
     ks->fold_ev = ks->done;
+    ks->fold_seq = 0;
     ks->has_done = true;
     ks->inited = true;
     std::fill(ks->got.begin(), ks->got.end(), 0);
@@ -674,7 +715,7 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
     Lane& L = *s->lanes[jobs[i].ks->lane];
     std::lock_guard<std::mutex> bg(L.batch_mu);
     std::vector<byteps_bucket_desc> d(e - i);
-    hipError_t we0 = hipStreamWaitEvent(L.fold, L.copy_mark, 0);  // every copy of the lane
+    hipError_t we0 = wait_copies(L);  // every copy of the lane
     int rc = we0 == hipSuccess ? 0 : hip_fail(we0, "hipStreamWaitEvent");
     for (size_t k = i; k < e; ++k) {
       KeyState* ks = jobs[k].ks;
@@ -690,22 +731,22 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
       b.len = ks->len;
       b.n = (int)jobs[k].order.size();
     }
+    hipEvent_t bev = nullptr;  // the launch's own event (batched_with_ring records it)
     if (!rc)
       rc = batched_with_ring(d.data(), (int)d.size(), jobs[i].ks->dtype,
-                             BYTEPS_REDUCE_MODE_REFERENCE, L.fold, L.ring);
-    hipEvent_t bev = nullptr;
+                             BYTEPS_REDUCE_MODE_REFERENCE, L.fold, L.ring, &bev);
+    uint64_t bseq = 0;
     if (!rc) {  // raised before any round is published: a pull that sees one waits past it
       s->n_fold_launches.fetch_add(1, std::memory_order_relaxed);
-      bev = L.batch_ev[L.batch_seq++ % kBatchEvents];
-      hipError_t me = hipEventRecord(bev, L.fold);
-      if (me == hipSuccess) me = hipEventRecord(L.fold_mark, L.fold);
+      hipError_t me = hipEventRecord(L.fold_mark, L.fold);
       if (me != hipSuccess) rc = hip_fail(me, "hipEventRecord");
+      if (!rc && bev && s->combine) bseq = track(L, bev);
     }
     for (size_t k = i; k < e; ++k) {
       KeyState* ks = jobs[k].ks;
       std::lock_guard<std::mutex> g(ks->mu);
       ks->pending--;
-      const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false, bev);
+      const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false, bev, bseq);
       if (r2) fail_key(s, ks, r2);
       ks->cv.notify_all();
     }
@@ -756,88 +797,38 @@ int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs) {
   return 0;
 }
 
-// Issue the device pulls that piled up on a lane: per lane ONE wait for the
-// lane's folds so far (every pulled round was published, so issued, before its
-// pull was queued), ONE batched copy, ONE event every request then waits for.
-void issue_pulls(byteps_server* s, Lane& L, std::vector<PullReq*>& reqs) {
-  int rc = 0;
-  hipEvent_t bev = nullptr;
-  {
-    std::lock_guard<std::mutex> bg(L.batch_mu);
-    hipError_t e = hipStreamWaitEvent(L.d2h, L.fold_mark, 0);
-    if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
-    std::vector<byteps_bucket_desc> d(reqs.size());
-    for (size_t k = 0; k < reqs.size() && !rc; ++k) {
-      std::memset(&d[k], 0, sizeof(d[k]));
-      d[k].dst = reqs[k]->dst;
-      d[k].srcs[0] = reqs[k]->ks->store;
-      d[k].len = reqs[k]->len;
-      d[k].n = 1;
-    }
-    if (!rc)
-      rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
-                             BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring);
-    if (!rc) {
-      s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
-      bev = L.batch_ev[L.batch_seq++ % kBatchEvents];
-      e = hipEventRecord(bev, L.d2h);
-      if (e == hipSuccess) e = hipEventRecord(L.d2h_mark, L.d2h);
-      if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
-    }
-  }
-  {
-    std::lock_guard<std::mutex> g(L.comb_mu);
-    for (PullReq* r : reqs) {
-      r->rc = rc;
-      r->ev = bev;
-      r->done = true;
-    }
-  }
-  L.pull_cv.notify_all();
-  reqs.clear();
-}
-
-// The lane's issuer thread (combining): folds first, then pulls, each as one
-// batch of whatever piled up since the last issue.  Drains before it exits.
+// The lane's issuer thread (combining): one batch of whatever rounds piled
+// up since the last issue.  Drains before it exits.
 void issuer_main(byteps_server* s, int lane) {
   (void)hipSetDevice(s->cfg.device);
   Lane& L = *s->lanes[lane];
   std::vector<FoldJob> folds;
-  std::vector<PullReq*> pulls;
   std::unique_lock<std::mutex> lk(L.comb_mu);
   for (;;) {
-    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty() || !L.pullq.empty(); });
-    if (L.comb.empty() && L.pullq.empty()) return;  // stopping, drained
-    folds.swap(L.comb);
-    pulls.swap(L.pullq);
+    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty(); });
+    if (L.comb.empty()) return;  // stopping, drained
+    // at most `inflight` of the lane's launches queued or running: while the
+    // device works through them, the rounds completing meanwhile pile up and
+    // go out together in the next launch
     lk.unlock();
+    {
+      std::unique_lock<std::mutex> dl(L.done_mu);
+      L.done_cv.wait(dl, [&] { return L.issued_seq - L.done_seq < s->inflight; });
+    }
+    lk.lock();
+    folds.swap(L.comb);
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
     if (folds.size() == 1)
       (void)issue_one(s, folds[0]);
-    else if (!folds.empty())
+    else
       (void)flush_folds(s, folds);  // a failed fold fails its keys (fail_key)
+    s->issuer_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t0).count(),
+                           std::memory_order_relaxed);
     folds.clear();
-    if (!pulls.empty()) issue_pulls(s, L, pulls);
     lk.lock();
   }
-}
-
-// A copying pull of device memory through the lane's issuer: queue it, wait
-// until it is issued, then for its batch's copy.  Caller holds no key lock.
-int pull_via_issuer(byteps_server* s, KeyState* ks, void* out, size_t len) {
-  Lane& L = *s->lanes[ks->lane];
-  PullReq r;
-  r.ks = ks;
-  r.dst = out;
-  r.len = len;
-  {
-    std::unique_lock<std::mutex> lk(L.comb_mu);
-    L.pullq.push_back(&r);
-    L.comb_cv.notify_one();
-    L.pull_cv.wait(lk, [&] { return r.done; });
-  }
-  if (r.rc) return r.rc;
-  hipError_t e = hipEventSynchronize(r.ev);
-  return e == hipSuccess ? 0 : hip_fail(e, "pull copy");
 }
 
 // After a single-key call issued (or queued) its round: the key's own error,
@@ -901,6 +892,14 @@ void destroy_lanes(byteps_server* s) {
   }
   for (auto& Lp : s->lanes)  // the issuers issue what is queued, then exit
     if (Lp && Lp->issuer.joinable()) Lp->issuer.join();
+  for (auto& Lp : s->lanes) {
+    if (!Lp) continue;
+    std::lock_guard<std::mutex> g(Lp->done_mu);
+    Lp->cq_stop = true;
+    Lp->cq_cv.notify_all();
+  }
+  for (auto& Lp : s->lanes)  // the completers see every tracked launch finish
+    if (Lp && Lp->completer.joinable()) Lp->completer.join();
 }
 
 }  // namespace
@@ -943,6 +942,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (const char* fa = getenv("BPSR_SERVER_FAIL_AFTER")) s->fail_after = atol(fa);
   if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
   if (s->schedule || s->blocking) s->combine = false;
+  if (const char* fl = getenv("BPSR_SERVER_INFLIGHT")) s->inflight = std::max(1L, atol(fl));
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
@@ -972,10 +972,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
     L.ring = stage_ring_create();
     for (hipEvent_t* m : {&L.copy_mark, &L.fold_mark, &L.d2h_mark})
       if (e == hipSuccess) e = hipEventCreateWithFlags(m, hipEventDisableTiming);
-    for (hipEvent_t& b : L.batch_ev) {
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventRecord(b, L.fold);
-    }
+
     // recorded once on their (empty) streams: waiting on them is a no-op until
     // the lane issues work
     if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
@@ -991,8 +988,10 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
       for (int i = 0; i < cfg->engine_lanes; ++i)
         s->lanes[i]->dispatcher = std::thread(dispatcher_main, s.get(), i);
     if (s->combine)
-      for (int i = 0; i < cfg->engine_lanes; ++i)
+      for (int i = 0; i < cfg->engine_lanes; ++i) {
+        s->lanes[i]->completer = std::thread(completer_main, s.get(), i);
         s->lanes[i]->issuer = std::thread(issuer_main, s.get(), i);
+      }
     s->responder = std::thread(responder_main, s.get());
   } catch (...) {
     byteps_server_destroy(s.release());
@@ -1048,8 +1047,7 @@ int byteps_server_destroy(byteps_server* s) {
     if (Lp->ring) stage_ring_destroy(Lp->ring);
     for (hipEvent_t m : {Lp->copy_mark, Lp->fold_mark, Lp->d2h_mark})
       if (m) (void)hipEventDestroy(m);
-    for (hipEvent_t b : Lp->batch_ev)
-      if (b) (void)hipEventDestroy(b);
+
   }
   delete s;
   return BYTEPS_REDUCE_OK;
@@ -1180,16 +1178,6 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
   s->n_pulls.fetch_add(1, std::memory_order_relaxed);
-  if (s->combine && location == BYTEPS_SERVER_DEVICE && !s->cfg.async_mode) {
-    // sync mode: the store holds this round until every worker has pulled it
-    // (the next round needs this worker's next push), so the copy can wait
-    // for the lane's issuer and go out with the pulls that piled up
-    lk.unlock();
-    if ((rc = pull_via_issuer(s, ks, out, len))) return rc;
-    lk.lock();
-    count_pull(s, ks);  // server.cc:105-113
-    return BYTEPS_REDUCE_OK;
-  }
   s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
   // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
@@ -1276,9 +1264,14 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   // behind it) was recorded, so this event covers the store's last write.
   const bool has = ks->has_done;
   hipEvent_t ev = ks->fold_ev;
+  const uint64_t need = ks->fold_seq;
   const void* view = ks->store;
   lk.unlock();
-  if (has) {
+  if (need) {  // tracked by the lane's completer: no HIP call here
+    Lane& L = *s->lanes[ks->lane];
+    std::unique_lock<std::mutex> dl(L.done_mu);
+    L.done_cv.wait(dl, [&] { return L.done_seq >= need; });
+  } else if (has) {
     hipError_t e = hipEventSynchronize(ev);
     if (e != hipSuccess) return hip_fail(e, "store fold sync");
   }
@@ -1427,6 +1420,7 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     }
     if ((e = hipEventRecord(L.copy_mark, L.copy)) != hipSuccess)
       return hip_fail(e, "hipEventRecord");
+    L.copy_seq.fetch_add(1);
   }
   // 2. arrivals, with the rounds they complete folded per lane in one launch
   std::vector<FoldJob> defer;
@@ -1568,9 +1562,9 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
 
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
   if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  const uint64_t v[4] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
-                         s->n_pull_launches.load(), s->n_pulls.load()};
-  for (int i = 0; i < n && i < 4; ++i) out[i] = v[i];
+  const uint64_t v[5] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+                         s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load()};
+  for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

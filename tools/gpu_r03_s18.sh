@@ -1,0 +1,6 @@
+export TMPDIR=/tmp; mkdir -p gpurun_out/r03s18
+timeout -k 10 300 tools/launch_cost 2000 > gpurun_out/r03s18/launch_cost.log 2>&1 || exit $?
+for v in 4 0 1 2 5; do
+  timeout -k 10 200 tools/server_cfg3_native tools/cfg3_resnet50_table.txt 20 4 $v >> gpurun_out/r03s18/srv.log 2>&1 || exit $?
+done
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/r03s18/tests.log 2>&1; rc=$?; tail -3 gpurun_out/r03s18/tests.log; exit $rc
