@@ -92,8 +92,8 @@ int main(int argc, char** argv) {
   const double alg = (double)(N + 1) * (double)total;
   const char* names[] = {"push_ready", "push_d2d", "push_ready_many+pull_many",
                          "push_many_d2d+pull_many", "push_ready+device_view",
-                         "push_ready_many+device_view"};
-  constexpr int kVariants = 6;
+                         "push_ready_many+device_view", "one_receive_thread:push_ready+device_view"};
+  constexpr int kVariants = 7;
   std::vector<uint64_t> keys(np);
   std::vector<size_t> lens(np);
   for (int i = 0; i < np; ++i) {
@@ -151,6 +151,28 @@ int main(int argc, char** argv) {
     };
     std::vector<double> push_ts;
     auto one_round = [&](int k, int r) {
+      if (variant == 6) {  // ps-lite's shape: ONE receive thread makes every call
+        if (k != 0) {
+          stamp(k);
+          return;
+        }
+        for (int i = 0; i < np; ++i)
+          for (int w = 0; w < N; ++w) CKR(byteps_server_push_ready(srv, (uint64_t)i, w));
+        stamp(0);
+        for (int i = 0; i < np; ++i)
+          for (int w = 0; w < N; ++w) {
+            if (r < rounds + 2) {
+              const void* v = nullptr;
+              size_t vl = 0;
+              CKR(byteps_server_pull_device_view(srv, (uint64_t)i, &v, &vl));
+              if (!v || vl != parts[i].second) exit(6);
+            } else {  // the checking round: copies into every worker's output
+              CKR(byteps_server_pull(srv, (uint64_t)i, out[w] + parts[i].first, parts[i].second,
+                                     BYTEPS_SERVER_DEVICE));
+            }
+          }
+        return;
+      }
       if (view && r < rounds + 2) {  // zero-copy: every pull is a view of the store
         if (many)
           CKR(byteps_server_push_ready_many(srv, keys.data(), np, k));
