@@ -99,7 +99,10 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
  * does (server.cc:184-198; workers use that answer as a barrier,
  * operations.cc:301-302).  Like byteps_server_push, a worker's push issued
  * while its previous push of the key (init push included) is not folded yet
- * waits inside the call until it is. */
+ * waits inside the call until it is.  Default engine, fused policy, sync mode,
+ * device data after the init round: the copy itself is the lane issuer's,
+ * batched with the other such pushes that piled up (one copy launch), and
+ * `data` must stay valid until cb. */
 typedef void (*byteps_server_push_cb)(void* ctx, uint64_t key, int worker, int status);
 int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
                              size_t len, int dtype, int location, byteps_server_push_cb cb,
@@ -171,7 +174,8 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
 
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
- * views), out[4] ns the lane issuer threads spent issuing; the first n. */
+ * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
+ * push-copy launches; the first n. */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

@@ -182,11 +182,12 @@ constexpr int kRing = 8;
 // of being copied to HBM first: a small hipMemcpyAsync H2D waits for the
 // stream's earlier work on the host (130-380 us per call behind queued folds,
 // rocprofv3 HIP trace of the server's issuer threads).
-constexpr size_t kZeroCopyTable = 256 * 1024;
+constexpr size_t kZeroCopyTable = 256 * 1024;  // default; a ring may read larger ones in place
 
 struct StageRing {
   StageSlot slots[kRing];
   int next = 0;
+  size_t zero_copy_max = kZeroCopyTable;
   std::vector<char> table;  // host copy of the table being built
   ~StageRing() {
     for (auto& s : slots) {
@@ -199,7 +200,11 @@ struct StageRing {
 };
 static thread_local StageRing g_ring;
 
-StageRing* stage_ring_create() { return new StageRing(); }
+StageRing* stage_ring_create(size_t zero_copy_max) {
+  auto* r = new StageRing();
+  if (zero_copy_max) r->zero_copy_max = zero_copy_max;
+  return r;
+}
 void stage_ring_destroy(StageRing* r) { delete r; }
 
 static int stage_acquire(StageRing& ring, size_t bytes, StageSlot** out) {
@@ -397,7 +402,7 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
   std::memcpy(slot->host, ring->table.data(), ti.bytes);
   hipError_t e = hipSuccess;
   const void* table = slot->host_dev;
-  if (ti.bytes > kZeroCopyTable) {  // large: one H2D copy, the kernel reads HBM
+  if (ti.bytes > ring->zero_copy_max) {  // large: one H2D copy, the kernel reads HBM
     e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
     table = slot->dev;

@@ -163,7 +163,9 @@ int elem_size(int dtype);  // 0 if unsupported
 // one per engine lane (transport threads come and go).  Not thread-safe: one
 // user at a time.
 struct StageRing;
-StageRing* stage_ring_create();
+// zero_copy_max: tables up to this many bytes are read by the kernel from the
+// pinned staging slot itself (0 = the library default, 256 KiB).
+StageRing* stage_ring_create(size_t zero_copy_max = 0);
 void stage_ring_destroy(StageRing* r);
 // *done (optional): the event recorded behind the launch (the staging slot's
 // guard; re-recorded only after a host wait for this launch, when the slot is

@@ -48,6 +48,33 @@ struct FoldJob {
   std::vector<int> order;  // arrival order of the finished round
 };
 
+struct Lane;
+// A pull ready to be answered, or a push to acknowledge, by the responder.
+struct Response {
+  uint64_t key = 0;
+  KeyState* ks = nullptr;
+  byteps_server_pull_cb cb = nullptr;
+  void* ctx = nullptr;
+  const char* view = nullptr;  // mirror holding the answered round
+  int status = 0;
+  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
+  int worker = -1;
+  // a push whose copy the lane's issuer batched: acknowledge once the lane's
+  // completer has seen launch wait_seq complete (else sync `copied`)
+  Lane* wait_lane = nullptr;
+  uint64_t wait_seq = 0;
+};
+
+// A non-blocking push of device data whose copy into its slot waits for the
+// lane's issuer (batched with the other copies that piled up).
+struct CopyJob {
+  KeyState* ks = nullptr;
+  int w = -1;
+  const void* src = nullptr;
+  size_t len = 0;
+  Response ack;
+};
+
 struct Lane {
   hipStream_t fold = nullptr;  // folds, in round order per key
   hipStream_t copy = nullptr;  // push copies
@@ -73,6 +100,7 @@ struct Lane {
   std::mutex comb_mu;
   std::condition_variable comb_cv;   // work for the issuer
   std::vector<FoldJob> comb;
+  std::vector<CopyJob> copies;       // non-blocking device pushes, before the folds
   bool comb_stop = false;
   std::thread issuer;
   // Completion of what the issuer issued, tracked on the host so waiters make
@@ -90,18 +118,6 @@ struct Lane {
   // copies recorded into copy_mark so far / seen by a fold's wait on it (a
   // fold stream already waiting on the latest copy mark need not wait again)
   std::atomic<uint64_t> copy_seq{0}, fold_copy_seen{0};
-};
-
-// A pull ready to be answered, or a push to acknowledge, by the responder.
-struct Response {
-  uint64_t key = 0;
-  KeyState* ks = nullptr;
-  byteps_server_pull_cb cb = nullptr;
-  void* ctx = nullptr;
-  const char* view = nullptr;  // mirror holding the answered round
-  int status = 0;
-  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
-  int worker = -1;
 };
 
 struct KeyState {
@@ -174,7 +190,7 @@ struct byteps_server {
   uint64_t inflight = 2;  // issuer: launches queued or running per lane (BPSR_SERVER_INFLIGHT)
   // telemetry (byteps_server_stats)
   std::atomic<uint64_t> n_fold_launches{0}, n_rounds_folded{0}, n_pull_launches{0},
-      n_pulls{0}, issuer_ns{0};
+      n_pulls{0}, issuer_ns{0}, n_copy_launches{0};
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   std::mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
@@ -453,7 +469,10 @@ void responder_main(byteps_server* s) {
     }
     if (r.push_cb) {  // the push's bytes are in HBM: the sender's buffer is free
       int status = r.status;
-      if (status == 0) {
+      if (status == 0 && r.wait_lane) {
+        std::unique_lock<std::mutex> dl(r.wait_lane->done_mu);
+        r.wait_lane->done_cv.wait(dl, [&] { return r.wait_lane->done_seq >= r.wait_seq; });
+      } else if (status == 0) {
         hipError_t e = hipEventSynchronize(r.ks->copied);
         if (e != hipSuccess) status = hip_fail(e, "push copy sync");
       }
@@ -797,16 +816,63 @@ int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs) {
   return 0;
 }
 
+// Issue the non-blocking device pushes that piled up on a lane: ONE wait for
+// the lane's folds so far (a slot is free once the fold that read it was
+// issued — the caller waited for that, can_push), ONE batched copy into the
+// slots, the lane's copy mark (later folds wait for it), then the pushes'
+// acknowledgements, which the responder sends once the copy has completed.
+void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
+  int rc = 0;
+  uint64_t seq = 0;
+  {
+    std::lock_guard<std::mutex> bg(L.batch_mu);
+    hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    std::vector<byteps_bucket_desc> d(jobs.size());
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      std::memset(&d[k], 0, sizeof(d[k]));
+      d[k].dst = jobs[k].ks->slot[jobs[k].w];
+      d[k].srcs[0] = jobs[k].src;
+      d[k].len = jobs[k].len;
+      d[k].n = 1;
+    }
+    hipEvent_t cev = nullptr;
+    if (!rc)
+      rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
+                             BYTEPS_REDUCE_MODE_REFERENCE, L.copy, L.ring, &cev);
+    if (!rc) {
+      s->n_copy_launches.fetch_add(1, std::memory_order_relaxed);
+      e = hipEventRecord(L.copy_mark, L.copy);
+      if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+      else L.copy_seq.fetch_add(1);
+      if (!rc && cev) seq = track(L, cev);
+    }
+  }
+  for (auto& j : jobs) {
+    if (rc) {  // the copy never ran: fail the key (its round cannot fold)
+      std::lock_guard<std::mutex> g(j.ks->mu);
+      fail_key(s, j.ks, rc);
+      j.ack.status = rc;
+    } else {
+      j.ack.wait_lane = &L;
+      j.ack.wait_seq = seq;
+    }
+    enqueue_response(s, j.ack);
+  }
+  jobs.clear();
+}
+
 // The lane's issuer thread (combining): one batch of whatever rounds piled
 // up since the last issue.  Drains before it exits.
 void issuer_main(byteps_server* s, int lane) {
   (void)hipSetDevice(s->cfg.device);
   Lane& L = *s->lanes[lane];
   std::vector<FoldJob> folds;
+  std::vector<CopyJob> copies;
   std::unique_lock<std::mutex> lk(L.comb_mu);
   for (;;) {
-    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty(); });
-    if (L.comb.empty()) return;  // stopping, drained
+    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty() || !L.copies.empty(); });
+    if (L.comb.empty() && L.copies.empty()) return;  // stopping, drained
     // at most `inflight` of the lane's launches queued or running: while the
     // device works through them, the rounds completing meanwhile pile up and
     // go out together in the next launch
@@ -817,11 +883,13 @@ void issuer_main(byteps_server* s, int lane) {
     }
     lk.lock();
     folds.swap(L.comb);
+    copies.swap(L.copies);
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
+    if (!copies.empty()) issue_copies(s, L, copies);  // before the folds that read them
     if (folds.size() == 1)
       (void)issue_one(s, folds[0]);
-    else
+    else if (!folds.empty())
       (void)flush_folds(s, folds);  // a failed fold fails its keys (fail_key)
     s->issuer_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - t0).count(),
@@ -969,7 +1037,9 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
       return hip_fail(e, "hipStreamCreate");
     }
     if (s->schedule) L.q = std::make_unique<EngineQueue<FoldJob>>(true);
-    L.ring = stage_ring_create();
+    // the lane's batches are read in place up to 4 MiB: a table copy would
+    // wait on the host behind the lane's queued work
+    L.ring = stage_ring_create(4u << 20);
     for (hipEvent_t* m : {&L.copy_mark, &L.fold_mark, &L.d2h_mark})
       if (e == hipSuccess) e = hipEventCreateWithFlags(m, hipEventDisableTiming);
 
@@ -1100,6 +1170,37 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
   if ((rc = allocate(s, ks, len, dtype))) return rc;
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
+  if (s->combine && location == BYTEPS_SERVER_DEVICE && ks->inited && !s->cfg.async_mode &&
+      s->cfg.policy == BYTEPS_SERVER_FUSED && s->cfg.num_workers <= kMaxSrcs) {
+    // the copy goes to the lane's issuer, batched with the other pushes that
+    // piled up, ahead of the fold this arrival may complete (also the
+    // issuer's, after the copies); acknowledged once the copy has completed
+    CopyJob cj;
+    cj.ks = ks;
+    cj.w = worker;
+    cj.src = data;
+    cj.len = len;
+    cj.ack.key = key;
+    cj.ack.ks = ks;
+    cj.ack.ctx = ctx;
+    cj.ack.push_cb = cb;
+    cj.ack.worker = worker;
+    {
+      Lane& L = *s->lanes[ks->lane];
+      std::lock_guard<std::mutex> g(L.comb_mu);
+      L.copies.push_back(cj);
+      L.comb_cv.notify_one();
+    }
+    std::vector<FoldJob> defer;
+    // cannot fail here: no error (checked under this lock), the slot is free
+    // (can_push), and the fused policy defers the round's fold
+    if ((rc = arrive(s, ks, worker, &defer))) return rc;
+    if (!defer.empty()) {
+      lk.unlock();
+      issue_combined(s, defer);
+    }
+    return BYTEPS_REDUCE_OK;
+  }
   if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
   const bool init_push = !ks->inited;
   std::vector<FoldJob> defer;
@@ -1562,9 +1663,10 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
 
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
   if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  const uint64_t v[5] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
-                         s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load()};
-  for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  const uint64_t v[6] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+                         s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
+                         s->n_copy_launches.load()};
+  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

@@ -842,6 +842,81 @@ def test_single_key_calls_issuer_batches(port, dt, combine, monkeypatch):
     assert st["pull_launches"] - st0["pull_launches"] <= pulls
 
 
+@pytest.mark.parametrize("combine", ["1", "0"], ids=["issuer", "per_call"])
+def test_push_async_device_copies_batched(port, combine, monkeypatch):
+    """Non-blocking pushes of device data (server.h: after the init round the
+    copies are the lane issuer's, batched): 6 worker threads x 50 keys x 3
+    rounds, fp16, every push acknowledged once, then device pulls — every
+    pulled byte equals the oracle's fold in arrival order; with the issuer
+    the copies went out in fewer launches than pushes."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_COMBINE", combine)
+    dt, N, R = DType.FLOAT16, 6, 3
+    sizes = [1 + (j * 6007) % 40_000 for j in range(50)]
+    keys = list(range(300, 300 + len(sizes)))
+    srv = PSServer(N, engine_lanes=3)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    outs = {(w, r): [torch.empty(n * 2, dtype=torch.uint8, device=dev) for n in sizes]
+            for w in range(N) for r in range(1, R + 1)}
+    torch.cuda.synchronize()
+    acks = threading.Semaphore(0)
+    bad = []
+
+    def ack(k, w, st):
+        if st:
+            bad.append((k, w, st))
+        acks.release()
+    bar = threading.Barrier(N + 1)
+    errors, orders = [], {}
+
+    def worker(w):
+        try:
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)          # init round: blocking
+            for r in range(1, R + 1):
+                for j, k in enumerate(keys):
+                    srv.push_async(k, w, src[(w, r, j)], dt, ack)
+                for j, k in enumerate(keys):
+                    srv.pull(k, outs[(w, r)][j])
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    st0 = srv.stats()
+    for r in range(1, R + 1):
+        bar.wait(timeout=240)
+        for j, k in enumerate(keys):
+            rounds, _, order = srv.key_info(k)
+            assert rounds == r
+            orders[(r, j)] = order
+        bar.wait(timeout=120)
+    for t in ts:
+        t.join(timeout=60)
+    assert not errors, errors
+    for _ in range(N * R * len(keys)):
+        assert acks.acquire(timeout=30)
+    assert not bad, bad[:5]
+    st = srv.stats()
+    srv.close()
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * 2, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, j) for w in orders[(r, j)]], n * 2, dt)
+            for w in range(N):
+                assert_bytes_match(dt, outs[(w, r)][j].cpu().numpy(), want,
+                                   nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
+    if combine == "1":
+        launches = st.get("push_copy_launches", 0) - st0.get("push_copy_launches", 0)
+        assert 1 <= launches <= N * R * len(keys)
+
+
 def _copy_to_ptr(ptr, src):
     """Device copy of tensor `src` to raw device pointer `ptr` (the transport
     writing into a receive slot)."""

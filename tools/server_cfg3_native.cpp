@@ -132,8 +132,8 @@ int main(int argc, char** argv) {
                        hipMemcpyDeviceToDevice));
         }
     }
-    uint64_t st0[5] = {0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st0, 5));
+    uint64_t st0[6] = {0, 0, 0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st0, 6));
     // persistent worker threads (a transport's receive threads), released per
     // round by the driver and joined by a countdown
     std::vector<double> ts;
@@ -268,21 +268,22 @@ int main(int argc, char** argv) {
     const double med = ts[ts.size() / 2];
     std::sort(push_ts.begin(), push_ts.end());
     const double push_med = push_ts[push_ts.size() / 2];
-    uint64_t st[5] = {0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st, 5));
-    for (int i = 0; i < 5; ++i) st[i] -= st0[i];
+    uint64_t st[6] = {0, 0, 0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st, 6));
+    for (int i = 0; i < 6; ++i) st[i] -= st0[i];
     printf("{\"config\": \"cfg3_via_server\", \"driver\": \"native C++ threads "
            "(tools/server_cfg3_native.cpp)\", \"variant\": \"%s\", \"n_workers\": %d, "
            "\"keys\": %d, \"lanes\": %d, \"bytes_per_worker\": %zu, \"round_ms\": %.4f, "
            "\"min_ms\": %.4f, \"us_per_key\": %.2f, \"hbm_frac_of_round\": %.4f, "
            "\"push_phase_ms\": %.4f, \"fold_launches_per_round\": %.1f, "
            "\"rounds_folded_per_round\": %.1f, \"pull_launches_per_round\": %.1f, "
-           "\"issuer_ms_per_round\": %.4f, "
+           "\"issuer_ms_per_round\": %.4f, \"push_copy_launches_per_round\": %.1f, "
            "\"pulls_agree\": %s}\n",
            names[variant], N, np, lanes, total, med * 1e3,
            ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, push_med * 1e3,
            (double)st[0] / total_rounds, (double)st[1] / total_rounds,
            (double)st[2] / total_rounds, (double)st[4] * 1e-6 / total_rounds,
+           (double)st[5] / total_rounds,
            same ? "true" : "false");
     fflush(stdout);
     CKR(byteps_server_destroy(srv));
