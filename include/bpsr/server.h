@@ -166,6 +166,19 @@ typedef void (*byteps_server_pull_cb)(void* ctx, uint64_t key, const void* data,
                                       int status);
 int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_cb cb, void* ctx);
 
+/* Non-blocking pull INTO a caller's device buffer (a worker GPU of the node,
+ * a registered device buffer of the transport): the reference's ZPull with a
+ * callback (the pull response lands in the worker's buffer).  Returns at once;
+ * once the key's round is finished the lane's issuer copies the store into
+ * `out` (len bytes), batched with the other pulls that piled up (one copy
+ * launch), and the responder thread calls cb(ctx, key, out, len, 0) when the
+ * copy has completed, counting the pull just before (as byteps_server_pull_async).
+ * Later folds of the key wait for the copy before rewriting the store.  Sync
+ * mode and the default engine only (EARGS otherwise); device memory only.
+ * Pulls still waiting at byteps_server_destroy get BYTEPS_REDUCE_ECANCELED. */
+int byteps_server_pull_into_async(byteps_server* s, uint64_t key, void* out, size_t len,
+                                  int location, byteps_server_pull_cb cb, void* ctx);
+
 /* Introspection for tests/debug (BYTEPS_SERVER_DEBUG analogue): completed
  * rounds, engine lane, and the arrival order of the last completed round
  * (waits until every round the key completed has been issued). */

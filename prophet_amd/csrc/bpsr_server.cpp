@@ -60,9 +60,20 @@ struct Response {
   byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
   int worker = -1;
   // a push whose copy the lane's issuer batched: acknowledge once the lane's
-  // completer has seen launch wait_seq complete (else sync `copied`)
+  // completer has seen launch wait_seq complete (else sync `copied`); the
+  // same for a pull copied into the caller's buffer (len: its length)
   Lane* wait_lane = nullptr;
   uint64_t wait_seq = 0;
+  size_t len = 0;
+};
+
+// A non-blocking pull into a caller's device buffer (byteps_server_pull_into_async)
+// whose copy waits for the lane's issuer.
+struct PullJob {
+  KeyState* ks = nullptr;
+  void* dst = nullptr;
+  size_t len = 0;
+  Response resp;
 };
 
 // A non-blocking push of device data whose copy into its slot waits for the
@@ -101,6 +112,7 @@ struct Lane {
   std::condition_variable comb_cv;   // work for the issuer
   std::vector<FoldJob> comb;
   std::vector<CopyJob> copies;       // non-blocking device pushes, before the folds
+  std::vector<PullJob> pulls;        // non-blocking pulls into device buffers
   bool comb_stop = false;
   std::thread issuer;
   // Completion of what the issuer issued, tracked on the host so waiters make
@@ -118,6 +130,9 @@ struct Lane {
   // copies recorded into copy_mark so far / seen by a fold's wait on it (a
   // fold stream already waiting on the latest copy mark need not wait again)
   std::atomic<uint64_t> copy_seq{0}, fold_copy_seen{0};
+  // pull copies recorded into d2h_mark / seen by a fold's wait on it (a
+  // fold rewrites the store those copies read)
+  std::atomic<uint64_t> pull_seq{0}, fold_pull_seen{0};
 };
 
 struct KeyState {
@@ -174,6 +189,14 @@ struct KeyState {
     void* ctx;
   };
   std::vector<Waiting> waiting;
+  // byteps_server_pull_into_async requests waiting for this round
+  struct WaitingCopy {
+    void* dst;
+    size_t len;
+    byteps_server_pull_cb cb;
+    void* ctx;
+  };
+  std::vector<WaitingCopy> waiting_copies;
 };
 
 }  // namespace
@@ -221,10 +244,19 @@ int set_device(const byteps_server* s) {
 // for the latest copy mark (push_ready-only rounds have no copies to wait for).
 hipError_t wait_copies(Lane& L) {
   const uint64_t c = L.copy_seq.load();
-  if (c == L.fold_copy_seen.load()) return hipSuccess;
-  const hipError_t e = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
-  if (e == hipSuccess) L.fold_copy_seen.store(c);
-  return e;
+  if (c != L.fold_copy_seen.load()) {
+    const hipError_t e = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+    if (e != hipSuccess) return e;
+    L.fold_copy_seen.store(c);
+  }
+  // and for the pull copies issued from the stores (a fold rewrites a store)
+  const uint64_t p = L.pull_seq.load();
+  if (p != L.fold_pull_seen.load()) {
+    const hipError_t e = hipStreamWaitEvent(L.fold, L.d2h_mark, 0);
+    if (e != hipSuccess) return e;
+    L.fold_pull_seen.store(p);
+  }
+  return hipSuccess;
 }
 
 // Hand a launch's completion event to the lane's completer (combining):
@@ -448,12 +480,34 @@ void fail_key(byteps_server* s, KeyState* ks, int rc) {
   }
   for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, nullptr, rc);
   ks->waiting.clear();
+  for (auto& wc : ks->waiting_copies) respond_later(s, ks, wc.cb, wc.ctx, nullptr, rc);
+  ks->waiting_copies.clear();
   for (auto& a : ks->init_acks) {
     a.status = rc;
     enqueue_response(s, a);
   }
   ks->init_acks.clear();
   ks->cv.notify_all();
+}
+
+// Queue a pull into a caller's device buffer for the lane's issuer (caller
+// holds ks->mu; the key's round is published, so its fold is issued).
+void queue_pull_copy(byteps_server* s, KeyState* ks, void* dst, size_t len,
+                     byteps_server_pull_cb cb, void* ctx) {
+  PullJob j;
+  j.ks = ks;
+  j.dst = dst;
+  j.len = len;
+  j.resp.key = ks->key;
+  j.resp.ks = ks;
+  j.resp.cb = cb;
+  j.resp.ctx = ctx;
+  j.resp.view = static_cast<const char*>(dst);
+  j.resp.len = len;
+  Lane& L = *s->lanes[ks->lane];
+  std::lock_guard<std::mutex> g(L.comb_mu);
+  L.pulls.push_back(j);
+  L.comb_cv.notify_one();
 }
 
 void responder_main(byteps_server* s) {
@@ -480,7 +534,10 @@ void responder_main(byteps_server* s) {
       continue;
     }
     int status = r.status;
-    if (status == 0) {
+    if (status == 0 && r.wait_lane) {  // a pull copied by the lane's issuer
+      std::unique_lock<std::mutex> dl(r.wait_lane->done_mu);
+      r.wait_lane->done_cv.wait(dl, [&] { return r.wait_lane->done_seq >= r.wait_seq; });
+    } else if (status == 0) {
       // The event still names the answered round's copy: the next round
       // cannot finish before this pull is counted (it needs this worker's
       // next push, which follows the answer).
@@ -495,7 +552,8 @@ void responder_main(byteps_server* s) {
       std::lock_guard<std::mutex> g(r.ks->mu);
       count_pull(s, r.ks);
     }
-    r.cb(r.ctx, r.key, status == 0 ? r.view : nullptr, status == 0 ? r.ks->len : 0, status);
+    r.cb(r.ctx, r.key, status == 0 ? r.view : nullptr,
+         status == 0 ? (r.len ? r.len : r.ks->len) : 0, status);
   }
 }
 
@@ -526,6 +584,8 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
   const char* view = ks->mirror.empty() ? nullptr : ks->mirror[ks->rounds & 1];
   for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, view, 0);
   ks->waiting.clear();
+  for (auto& wc : ks->waiting_copies) queue_pull_copy(s, ks, wc.dst, wc.len, wc.cb, wc.ctx);
+  ks->waiting_copies.clear();
   ks->cv.notify_all();
   return 0;
 }
@@ -862,6 +922,51 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
   jobs.clear();
 }
 
+// Issue the pulls into device buffers that piled up on a lane: ONE wait for
+// the lane's folds so far (every pulled round was issued before its pull was
+// queued), ONE batched copy from the stores on the d2h stream, the d2h mark
+// (later folds of the lane wait for it before rewriting a store), then the
+// answers, which the responder sends once the copy has completed.
+void issue_pull_copies(byteps_server* s, Lane& L, std::vector<PullJob>& jobs) {
+  int rc = 0;
+  uint64_t seq = 0;
+  {
+    std::lock_guard<std::mutex> bg(L.batch_mu);
+    hipError_t e = hipStreamWaitEvent(L.d2h, L.fold_mark, 0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    std::vector<byteps_bucket_desc> d(jobs.size());
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      std::memset(&d[k], 0, sizeof(d[k]));
+      d[k].dst = jobs[k].dst;
+      d[k].srcs[0] = jobs[k].ks->store;
+      d[k].len = jobs[k].len;
+      d[k].n = 1;
+    }
+    hipEvent_t cev = nullptr;
+    if (!rc)
+      rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
+                             BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring, &cev);
+    if (!rc) {
+      s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
+      e = hipEventRecord(L.d2h_mark, L.d2h);
+      if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+      else L.pull_seq.fetch_add(1);
+      if (!rc && cev) seq = track(L, cev);
+    }
+  }
+  s->n_pulls.fetch_add(jobs.size(), std::memory_order_relaxed);
+  for (auto& j : jobs) {
+    if (rc) {
+      j.resp.status = rc;
+    } else {
+      j.resp.wait_lane = &L;
+      j.resp.wait_seq = seq;
+    }
+    enqueue_response(s, j.resp);
+  }
+  jobs.clear();
+}
+
 // The lane's issuer thread (combining): one batch of whatever rounds piled
 // up since the last issue.  Drains before it exits.
 void issuer_main(byteps_server* s, int lane) {
@@ -869,10 +974,13 @@ void issuer_main(byteps_server* s, int lane) {
   Lane& L = *s->lanes[lane];
   std::vector<FoldJob> folds;
   std::vector<CopyJob> copies;
+  std::vector<PullJob> pulls;
   std::unique_lock<std::mutex> lk(L.comb_mu);
   for (;;) {
-    L.comb_cv.wait(lk, [&] { return L.comb_stop || !L.comb.empty() || !L.copies.empty(); });
-    if (L.comb.empty() && L.copies.empty()) return;  // stopping, drained
+    L.comb_cv.wait(lk, [&] {
+      return L.comb_stop || !L.comb.empty() || !L.copies.empty() || !L.pulls.empty();
+    });
+    if (L.comb.empty() && L.copies.empty() && L.pulls.empty()) return;  // stopping, drained
     // at most `inflight` of the lane's launches queued or running: while the
     // device works through them, the rounds completing meanwhile pile up and
     // go out together in the next launch
@@ -884,9 +992,11 @@ void issuer_main(byteps_server* s, int lane) {
     lk.lock();
     folds.swap(L.comb);
     copies.swap(L.copies);
+    pulls.swap(L.pulls);
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
     if (!copies.empty()) issue_copies(s, L, copies);  // before the folds that read them
+    if (!pulls.empty()) issue_pull_copies(s, L, pulls);  // before folds that rewrite stores
     if (folds.size() == 1)
       (void)issue_one(s, folds[0]);
     else if (!folds.empty())
@@ -1082,6 +1192,9 @@ int byteps_server_destroy(byteps_server* s) {
       for (auto& wp : ks->waiting)
         respond_later(s, ks, wp.cb, wp.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
       ks->waiting.clear();
+      for (auto& wc : ks->waiting_copies)
+        respond_later(s, ks, wc.cb, wc.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
+      ks->waiting_copies.clear();
       for (auto& a : ks->init_acks) {  // init pushes whose round never completed
         a.status = BYTEPS_REDUCE_ECANCELED;
         enqueue_response(s, a);
@@ -1406,6 +1519,29 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
     respond_later(s, ks, cb, ctx, ks->mirror[ks->rounds & 1], 0);
   else                    // server.cc:303-304: queued until the round finishes
     ks->waiting.push_back({cb, ctx});
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_pull_into_async(byteps_server* s, uint64_t key, void* out, size_t len,
+                                  int location, byteps_server_pull_cb cb, void* ctx) {
+  if (!s || !out || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (location != BYTEPS_SERVER_DEVICE)
+    return fail(BYTEPS_REDUCE_EARGS, "pull_into_async copies into device memory only "
+                                     "(host transports: byteps_server_pull_async views)");
+  if (s->cfg.async_mode || !s->combine)
+    return fail(BYTEPS_REDUCE_EARGS, "pull_into_async needs sync mode and the default engine "
+                                     "(no scheduling, no engine blocking, BPSR_SERVER_COMBINE!=0)");
+  int rc = set_device(s);
+  if (rc) return rc;
+  KeyState* ks = key_for_pull(s, key);
+  if (!ks) return BYTEPS_REDUCE_EARGS;
+  std::lock_guard<std::mutex> g(ks->mu);
+  if (ks->error) return key_error(ks);
+  if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
+  if (ks->push_finished)  // server.cc:293-301: the round is finished
+    queue_pull_copy(s, ks, out, len, cb, ctx);
+  else                    // server.cc:303-304: answered once it finishes
+    ks->waiting_copies.push_back({out, len, cb, ctx});
   return BYTEPS_REDUCE_OK;
 }
 

@@ -24,6 +24,7 @@ SERVER_EXPORTS = (
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",
     "byteps_server_debug_lane", "byteps_server_push_ready_many", "byteps_server_push_many",
     "byteps_server_pull_many", "byteps_server_pull_device_view", "byteps_server_stats",
+    "byteps_server_pull_into_async",
     "byteps_server_key_hash", "byteps_server_group_config_from_env", "byteps_server_route",
     "byteps_server_group_create", "byteps_server_group_destroy", "byteps_server_group_route",
     "byteps_server_group_instance", "byteps_server_group_init_key", "byteps_server_group_push",
@@ -85,6 +86,7 @@ def _lib():
         L.byteps_server_pull_device_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
                                                      ctypes.POINTER(_sz)]
         L.byteps_server_pull_async.argtypes = [_vp, _u64, PULL_CB, _vp]
+        L.byteps_server_pull_into_async.argtypes = [_vp, _u64, _vp, _sz, _int, PULL_CB, _vp]
         L.byteps_server_stats.argtypes = [_vp, ctypes.POINTER(_u64), _int]
         L.byteps_server_push_async.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int, PUSH_CB,
                                                _vp]
@@ -277,6 +279,30 @@ class PSServer:
         token = id(cfn)
         self._pending[token] = cfn          # keep the thunk alive until it ran
         rc = self.lib.byteps_server_pull_async(self.handle, key, cfn, None)
+        if rc != 0:
+            self._pending.pop(token, None)
+        _check(rc)
+
+    def pull_into_async(self, key: int, out, callback=None, nbytes: int | None = None) -> None:
+        """Non-blocking pull into a device tensor (byteps_server_pull_into_async):
+        the lane's issuer copies the finished round into ``out`` (batched with
+        the other pulls that piled up); ``callback(key, status)`` runs on the
+        responder thread once the bytes are there.  ``out`` is kept alive until
+        then."""
+        p, n, loc = _buf(out, sync=False)
+
+        def tramp(_ctx, k, _data, _n, status):
+            try:
+                if callback is not None:
+                    callback(int(k), int(status))
+            finally:
+                self._pending.pop(token, None)
+        cfn = PULL_CB(tramp)
+        token = id(cfn)
+        self._pending[token] = (cfn, out)
+        rc = self.lib.byteps_server_pull_into_async(self.handle, key, p,
+                                                    n if nbytes is None else nbytes, loc,
+                                                    cfn, None)
         if rc != 0:
             self._pending.pop(token, None)
         _check(rc)

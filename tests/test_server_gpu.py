@@ -842,13 +842,17 @@ def test_single_key_calls_issuer_batches(port, dt, combine, monkeypatch):
     assert st["pull_launches"] - st0["pull_launches"] <= pulls
 
 
-@pytest.mark.parametrize("combine", ["1", "0"], ids=["issuer", "per_call"])
-def test_push_async_device_copies_batched(port, combine, monkeypatch):
+@pytest.mark.parametrize("combine,pull_mode", [("1", "blocking"), ("0", "blocking"),
+                                               ("1", "into_async")],
+                         ids=["issuer", "per_call", "issuer_pull_into_async"])
+def test_push_async_device_copies_batched(port, combine, pull_mode, monkeypatch):
     """Non-blocking pushes of device data (server.h: after the init round the
     copies are the lane issuer's, batched): 6 worker threads x 50 keys x 3
-    rounds, fp16, every push acknowledged once, then device pulls — every
-    pulled byte equals the oracle's fold in arrival order; with the issuer
-    the copies went out in fewer launches than pushes."""
+    rounds, fp16, every push acknowledged once, then device pulls — blocking,
+    or all queued with pull_into_async (parked until the round finishes,
+    copied by the issuer) — every pulled byte equals the oracle's fold in
+    arrival order; with the issuer the copies went out in fewer launches than
+    pushes."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_COMBINE", combine)
     dt, N, R = DType.FLOAT16, 6, 3
@@ -878,8 +882,17 @@ def test_push_async_device_copies_batched(port, combine, monkeypatch):
             for r in range(1, R + 1):
                 for j, k in enumerate(keys):
                     srv.push_async(k, w, src[(w, r, j)], dt, ack)
-                for j, k in enumerate(keys):
-                    srv.pull(k, outs[(w, r)][j])
+                if pull_mode == "into_async":   # every pull queued, answered later
+                    got = threading.Semaphore(0)
+                    for j, k in enumerate(keys):
+                        srv.pull_into_async(k, outs[(w, r)][j],
+                                            lambda kk, st: (bad.append((kk, st)) if st else None,
+                                                            got.release()))
+                    for _ in keys:
+                        assert got.acquire(timeout=60)
+                else:
+                    for j, k in enumerate(keys):
+                        srv.pull(k, outs[(w, r)][j])
                 bar.wait(timeout=120)
                 bar.wait(timeout=120)
         except Exception as e:  # surfaced below

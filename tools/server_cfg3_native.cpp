@@ -52,7 +52,14 @@
 
 namespace {
 constexpr int N = 8;
-std::atomic<long> acks{0};
+std::atomic<long> acks{0}, pulled{0};
+void on_pull(void*, uint64_t, const void*, size_t, int status) {
+  if (status) {
+    fprintf(stderr, "pull status %d\n", status);
+    exit(4);
+  }
+  pulled.fetch_add(1, std::memory_order_relaxed);
+}
 void on_push(void*, uint64_t, int, int status) {
   if (status) {
     fprintf(stderr, "push ack status %d\n", status);
@@ -92,8 +99,10 @@ int main(int argc, char** argv) {
   const double alg = (double)(N + 1) * (double)total;
   const char* names[] = {"push_ready", "push_d2d", "push_ready_many+pull_many",
                          "push_many_d2d+pull_many", "push_ready+device_view",
-                         "push_ready_many+device_view", "one_receive_thread:push_ready+device_view"};
-  constexpr int kVariants = 7;
+                         "push_ready_many+device_view", "one_receive_thread:push_ready+device_view",
+                         "one_receive_thread:push_async_d2d+pull_into_async",
+                         "push_async_d2d+pull_into_async"};
+  constexpr int kVariants = 9;
   std::vector<uint64_t> keys(np);
   std::vector<size_t> lens(np);
   for (int i = 0; i < np; ++i) {
@@ -102,9 +111,9 @@ int main(int argc, char** argv) {
   }
   for (int variant = 0; variant < kVariants; ++variant) {
     if (only >= 0 && variant != only) continue;
-    const bool view = variant >= 4;
+    const bool view = variant >= 4 && variant <= 6;
     const bool many = variant == 2 || variant == 3 || variant == 5;
-    const bool ready = variant != 1 && variant != 3;
+    const bool ready = variant != 1 && variant != 3 && variant < 7;
     byteps_server_config cfg;
     std::memset(&cfg, 0, sizeof(cfg));
     cfg.num_workers = N;
@@ -151,6 +160,25 @@ int main(int argc, char** argv) {
     };
     std::vector<double> push_ts;
     auto one_round = [&](int k, int r) {
+      if (variant >= 7) {  // non-blocking device pushes and pulls into device buffers
+        if (variant == 7 && k != 0) {
+          stamp(k);
+          return;
+        }
+        const int w0 = variant == 7 ? 0 : k, w1 = variant == 7 ? N : k + 1;
+        for (int i = 0; i < np; ++i)
+          for (int w = w0; w < w1; ++w)
+            CKR(byteps_server_push_async(srv, (uint64_t)i, w, grad[w] + parts[i].first,
+                                         parts[i].second, BYTEPS_REDUCE_FLOAT16,
+                                         BYTEPS_SERVER_DEVICE, on_push, nullptr));
+        stamp(k);
+        for (int i = 0; i < np; ++i)
+          for (int w = w0; w < w1; ++w)
+            CKR(byteps_server_pull_into_async(srv, (uint64_t)i, out[w] + parts[i].first,
+                                              parts[i].second, BYTEPS_SERVER_DEVICE, on_pull,
+                                              nullptr));
+        return;
+      }
       if (variant == 6) {  // ps-lite's shape: ONE receive thread makes every call
         if (k != 0) {
           stamp(k);
@@ -232,6 +260,7 @@ int main(int argc, char** argv) {
       });
     for (int r = 0; r < total_rounds; ++r) {
       acks = 0;
+      pulled = 0;
       auto t0 = std::chrono::steady_clock::now();
       {
         std::lock_guard<std::mutex> lk(m);
@@ -243,8 +272,10 @@ int main(int argc, char** argv) {
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return left == 0; });
       }
-      if (variant == 1)
+      if (variant == 1 || variant >= 7)
         while (acks.load() < (long)N * np) std::this_thread::yield();
+      if (variant >= 7)
+        while (pulled.load() < (long)N * np) std::this_thread::yield();
       const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (r >= 2 && r < rounds + 2) {
         ts.push_back(s);
