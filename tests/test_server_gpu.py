@@ -415,6 +415,50 @@ def test_push_async_rounds(port, policy):
     srv.close()
 
 
+def test_pull_into_async_rules_and_cancel(port):
+    """byteps_server_pull_into_async: refused for host memory, in async mode,
+    with scheduling or engine blocking, and for more bytes than the key; a
+    pull parked for a round that never finishes is answered ECANCELED at
+    shutdown; one queued after the round finished is copied and answered."""
+    from prophet_amd.reducer import ECANCELED, ReduceError
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 5003
+    dev = torch.device("cuda:0")
+    for kw in ({"async_mode": True}, {"enable_schedule": True}, {"engine_blocking": True}):
+        srv = PSServer(N, **kw)
+        srv.init_key(1, n * 4, dt)
+        with pytest.raises(ReduceError):
+            srv.pull_into_async(1, torch.empty(n * 4, dtype=torch.uint8, device=dev))
+        srv.close()
+    srv = PSServer(N)
+    srv.push_async(1, 0, data(dt, n, 0, 0, 1), dt)         # init: worker 1 arrives last
+    srv.push(1, 1, data(dt, n, 1, 0, 1), dt)
+    with pytest.raises(ReduceError):                       # host memory
+        srv.pull_into_async(1, np.zeros(n * 4, np.uint8))
+    with pytest.raises(ReduceError):                       # more than the key
+        srv.pull_into_async(1, torch.empty(n * 4 + 4, dtype=torch.uint8, device=dev))
+    got, done = [], threading.Semaphore(0)
+
+    def cb(k, st):
+        got.append((k, st))
+        done.release()
+    out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    srv.pull_into_async(1, out, cb)                        # the init round is finished
+    assert done.acquire(timeout=30)
+    assert got == [(1, 0)]
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), data(dt, n, 1, 0, 1))  # the last init push
+    srv.pull_into_async(1, out, cb)                        # the second worker's pull
+    assert done.acquire(timeout=30)
+    srv.push(1, 0, data(dt, n, 0, 1, 1), dt)               # round 1: one push of two
+    srv.pull_into_async(1, out, cb)                        # parked: never finishes
+    time.sleep(0.2)
+    assert len(got) == 2
+    srv.close()
+    assert done.acquire(timeout=30)
+    assert got[2] == (1, ECANCELED)
+
+
 def test_push_async_init_store_is_last_call(port):
     from prophet_amd.server import PSServer
     dt, N, n = DType.FLOAT16, 3, 4099
