@@ -443,14 +443,20 @@ def test_pull_into_async_rules_and_cancel(port):
         got.append((k, st))
         done.release()
     out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
-    srv.pull_into_async(1, out, cb)                        # the init round is finished
+    srv.pull_into_async(1, out, cb)                        # parked until round 1 finishes
+    time.sleep(0.2)
+    assert got == []
+    for w in (1, 0):                                       # round 1, worker 1 first
+        srv.push(1, w, data(dt, n, w, 1, 1), dt)
     assert done.acquire(timeout=30)
     assert got == [(1, 0)]
     torch.cuda.synchronize()
-    assert np.array_equal(out.cpu().numpy(), data(dt, n, 1, 0, 1))  # the last init push
-    srv.pull_into_async(1, out, cb)                        # the second worker's pull
+    want = np.zeros(n * 4, np.uint8)
+    port.sum_n(want, [data(dt, n, w, 1, 1) for w in (1, 0)], n * 4, dt)
+    assert np.array_equal(out.cpu().numpy(), want)
+    srv.pull_into_async(1, out, cb)                        # the round is finished: at once
     assert done.acquire(timeout=30)
-    srv.push(1, 0, data(dt, n, 0, 1, 1), dt)               # round 1: one push of two
+    srv.push(1, 0, data(dt, n, 0, 2, 1), dt)               # round 2: one push of two
     srv.pull_into_async(1, out, cb)                        # parked: never finishes
     time.sleep(0.2)
     assert len(got) == 2
