@@ -16,6 +16,7 @@
 #include <limits>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -215,7 +216,8 @@ struct byteps_server {
   std::atomic<uint64_t> n_fold_launches{0}, n_rounds_folded{0}, n_pull_launches{0},
       n_pulls{0}, issuer_ns{0}, n_copy_launches{0};
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
-  std::mutex map_mu;
+  // every call looks its key up; keys are added once: lookups share the lock
+  std::shared_mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
   std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
   // responder thread: SendPullResponse of queued pulls (server.cc:100-114)
@@ -303,10 +305,15 @@ int pick_lane(byteps_server* s, size_t len) {
 }
 
 KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
-  std::lock_guard<std::mutex> g(s->map_mu);
-  auto it = s->keys.find(key);
+  {
+    std::shared_lock<std::shared_mutex> g(s->map_mu);
+    auto it = s->keys.find(key);
+    if (it != s->keys.end()) return it->second.get();
+    if (!create) return nullptr;
+  }
+  std::unique_lock<std::shared_mutex> g(s->map_mu);
+  auto it = s->keys.find(key);  // another caller may have added it meanwhile
   if (it != s->keys.end()) return it->second.get();
-  if (!create) return nullptr;
   auto ks = std::make_unique<KeyState>();
   ks->key = key;
   KeyState* p = ks.get();
@@ -353,7 +360,7 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   ks->len = len;
   ks->dtype = dtype;
   {
-    std::lock_guard<std::mutex> g(s->map_mu);
+    std::unique_lock<std::shared_mutex> g(s->map_mu);
     ks->lane = pick_lane(s, len);
   }
   ks->allocated = true;
