@@ -819,7 +819,10 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     alg = (N + 1) * total
     res = {"workload": (f"config 3: {N}-way fp16 ResNet-50 ({total} B per worker), "
                         f"{len(parts)} partitions in {nb} Prophet blocks, block queue "
-                        "(one consumer launch per iteration)"),
+                        "(one consumer launch per iteration); live = the native PUSH loop "
+                        "(Prophet scheduler, stream-ordered release kernels, the release "
+                        "groups ready together as one kernel); live_per_block = one "
+                        "release kernel per block"),
            "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
     rel_kernels = {"live_per_block": nb, "pre_released": 1, "live_host_releases": 0}
     for name, fn in (("live", live), ("live_per_block", live_per_block),
