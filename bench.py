@@ -346,6 +346,32 @@ class _Clock:
             fn(i)
         return (time.perf_counter() - t0) * 1e3 / reps
 
+    def blocks(self, fn, n_blocks: int, per_block: int, first: int = 0) -> list[float]:
+        """ms per call in each of ``n_blocks`` consecutive blocks of
+        ``per_block`` back-to-back calls fn(first + i), one event at every
+        block boundary (median and min over repetitions).  Not
+        one event pair per launch: an event between two launches cost the
+        second ≈ 27 µs on MI355X (r03s31: per-launch pairs 0.397 ms median vs
+        0.370 averaged back to back, which rocprofv3's kernel durations
+        confirm), so per-launch brackets would time the events."""
+        if self.cuda:
+            import torch
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(n_blocks + 1)]
+            ev[0].record(self.stream)
+            for b in range(n_blocks):
+                for i in range(per_block):
+                    fn(first + b * per_block + i)
+                ev[b + 1].record(self.stream)
+            torch.cuda.synchronize()
+            return [ev[b].elapsed_time(ev[b + 1]) / per_block for b in range(n_blocks)]
+        out = []
+        for b in range(n_blocks):
+            t0 = time.perf_counter()
+            for i in range(per_block):
+                fn(first + b * per_block + i)
+            out.append((time.perf_counter() - t0) * 1e3 / per_block)
+        return out
+
 
 def _max_over_ranks(dist, dev, vals: list[float]) -> list[float]:
     import torch
@@ -1039,6 +1065,14 @@ def main(argv=None):
     wall = time.perf_counter() - t0
     t_step = wall / args.steps
     t_step, kern_ms = _max_over_ranks(dist, dev, [t_step, kern_ms])
+    # Spread of the per-launch time (median / min / max over blocks of
+    # back-to-back launches), a separate pass after the timed region; it ends
+    # on the same input set as the timed steps did.
+    n_blk, per_blk = 5, max(1, min(args.steps // 5, 10))
+    pl = sorted(clock.blocks(step, n_blk, per_blk,
+                             first=args.steps + args.warmup - n_blk * per_blk))
+    pl_med, pl_min, pl_max = _max_over_ranks(
+        dist, dev, [statistics.median(pl), pl[0], pl[-1]])
 
     # Correctness spot check of the last set against torch's own left fold.
     dst, srcs = sets[(args.steps + args.warmup - 1) % len(sets)]
@@ -1089,6 +1123,11 @@ def main(argv=None):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 5),
+                     # per-launch average of each of n_blk blocks of per_blk
+                     # back-to-back launches, a separate pass (max over ranks)
+                     "kernel_ms_blocks": {"median": round(pl_med, 5), "min": round(pl_min, 5),
+                                          "max": round(pl_max, 5), "blocks": n_blk,
+                                          "launches_per_block": per_blk},
                      # also the read stream alone (N * B of the
                      # (N + 1) * B), against the same peak
                      "read_only_GBps": round(N * B / (kern_ms * 1e-3) / 1e9, 1),

@@ -38,6 +38,8 @@ def test_launcher_one_line_n_ranks(n):
     assert len(line["config"]["devices"]) == n
     assert line["check_vs_torch_fold"] is True
     assert "NOT a measurement" in line["device"]
+    pl = line["roofline"]["kernel_ms_blocks"]   # median and min
+    assert 0 < pl["min"] <= pl["median"] <= pl["max"] and pl["blocks"] == 5
     sc = line["scaling_cfg4"]
     assert sc["exact_vs_torch_fold"] is True
     assert len(sc["shard_elems"]) == n and sum(sc["shard_elems"]) == 10007
