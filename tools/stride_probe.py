@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--skew", type=int, default=16 * 1024)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--pads-mib", default="0", help="extra MiB between slots (spacing test)")
     a = ap.parse_args()
     import torch
     from prophet_amd.dtypes import DType
@@ -38,9 +39,10 @@ def main():
     for B in [int(x) for x in a.sizes.split(",")]:
         B = B // 4 * 4
         for rnd in range(a.rounds):
-            for akib in [int(x) for x in a.aligns_kib.split(",")]:
+            for akib, pad in [(int(x), int(y)) for x in a.aligns_kib.split(",")
+                              for y in a.pads_mib.split(",")]:
                 align = akib * 1024
-                stride = (B + align - 1) // align * align + a.skew
+                stride = (B + align - 1) // align * align + (pad << 20) + a.skew
                 sets = []
                 for s in range(3):
                     slab = torch.empty(stride * (N + 1), dtype=torch.uint8, device=dev)
@@ -75,7 +77,7 @@ def main():
                     ref.add_(x.view(torch.float32)[w])
                 ok = bool(torch.equal(ref.view(torch.int32), d.view(torch.float32)[w].view(torch.int32)))
                 med = statistics.median(ts)
-                print(json.dumps({"probe": "stride", "bucket_bytes": B, "align_kib": akib,
+                print(json.dumps({"probe": "stride", "bucket_bytes": B, "align_kib": akib, "pad_mib": pad, "stride": stride,
                                   "stride_mod_align": stride % align if align else None,
                                   "round": rnd, "us": round(med * 1e3, 2),
                                   "frac": round((N + 1) * B / (med * 1e-3) / 8e12, 4),
