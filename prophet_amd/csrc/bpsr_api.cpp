@@ -382,6 +382,14 @@ static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti) {
   L.recs = static_cast<const unsigned char*>(dev_table) + ti.recs_off;
   L.rec_stride = ti.rec_stride;
   L.tiles = ti.tiles;
+  // record prefetch distance (bpsr_kernels_impl.h prefetch_record): one
+  // resident round of the 256-CU chip; BPSR_REC_PREFETCH=0 turns it off (A/B)
+  static const uint32_t ahead = [] {
+    const char* v = getenv("BPSR_REC_PREFETCH");
+    const long x = v ? atol(v) : (long)kPrefetchAhead;
+    return x > 0 ? (uint32_t)((x + 7) & ~7L) : 0u;  // a multiple of 8: the same XCD
+  }();
+  L.pf_ahead = ahead;
   return L;
 }
 

@@ -79,11 +79,13 @@ static_assert(sizeof(TileHead) == kTileHeadBytes, "TileHead layout");
 inline uint32_t tile_rec_stride(int nmax) {
   return (kTileHeadBytes + 8u * (uint32_t)(nmax < 8 ? 8 : nmax) + 31u) & ~31u;
 }
+constexpr uint32_t kPrefetchAhead = 256;  // tile-record prefetch distance: MI355X's 256 CUs
 struct BatchLaunch {
   const unsigned char* recs;    // tiles records
   const BatchEntry* entries;    // per-bucket geometry
   uint32_t rec_stride;
   uint32_t tiles;
+  uint32_t pf_ahead;            // L2 prefetch of record blockIdx + pf_ahead (0 = off)
 };
 
 // Block consumer (byteps_reduce_blockq_*).  One launch folds the whole table;

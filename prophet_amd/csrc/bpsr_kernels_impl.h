@@ -422,13 +422,38 @@ __device__ __forceinline__ RecRegs regs_from_words(const uint32_t* w) {
   return r;
 }
 
+// L2 prefetch of the tile record that workgroup `t` will read: the record
+// fetch is a dependent round trip at the head of every workgroup (nothing
+// else can issue before the pointers arrive), and at one or two resident
+// workgroups per CU it is not hidden behind another workgroup's loads.  A
+// workgroup touches the record of the workgroup dispatched kPrefetchAhead
+// later (L.pf_ahead, default kPrefetchAhead) — the same XCD (workgroups go
+// to the 8 XCDs round-robin, and the distance is a multiple of 8), about one
+// resident round ahead — so
+// that record is in the XCD's L2 when its workgroup starts.  Two lanes, one
+// dword at each end of the record (a 96-B record may straddle two 128-B
+// lines).  The values are consumed by keep_prefetch at the very end, after
+// the tile's own loads and stores were issued, so no wait lands earlier.
+__device__ __forceinline__ uint32_t prefetch_record(const BatchLaunch& L, uint64_t b) {
+  uint32_t v = 0;
+  const uint64_t t = b + L.pf_ahead;
+  if (L.pf_ahead != 0 && threadIdx.x < 2 && t < L.tiles) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(L.recs + t * L.rec_stride);
+    v = p[threadIdx.x == 0 ? 0 : L.rec_stride / 4 - 1];
+  }
+  return v;
+}
+__device__ __forceinline__ void keep_prefetch(uint32_t v) { asm volatile("" ::"v"(v)); }
+
 // Batched: workgroup b runs record b of the launch.
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void batched_kernel(BatchLaunch L) {
   const unsigned char* rec = L.recs + (uint64_t)blockIdx.x * L.rec_stride;
-  run_record<Op, VPT, NT>(load_record(rec),
-                          reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes),
+  const RecRegs r = load_record(rec);
+  const uint32_t pf = prefetch_record(L, blockIdx.x);
+  run_record<Op, VPT, NT>(r, reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes),
                           L.entries);
+  keep_prefetch(pf);
 }
 
 // Persistent block consumer (byteps_reduce_blockq_*).  Q.grid resident
@@ -585,6 +610,7 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
   uint32_t w = lane < Q.nblocks ? ld_sys(Q.flags + lane) : Q.epoch;
   const RecRegs r = load_record(rec);
   const uint32_t blk = reinterpret_cast<const TileHead*>(rec)->block;
+  const uint32_t pf = prefetch_record(Q.L, t);
   // every block b <= blk released for this epoch (blocks past 64: rare, more loads)
   auto released = [&](uint32_t w0) __attribute__((always_inline)) {
     if (__ballot(lane <= blk && !epoch_reached(w0, Q.epoch)) != 0) return false;
@@ -611,6 +637,7 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
   }
   run_record<Op, VPT, NT>(r, reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes),
                           Q.L.entries);
+  keep_prefetch(pf);
 }
 
 // ------------------------------------------------------------- launchers ----
