@@ -3,7 +3,8 @@
 // interleaved slot layout (chunk c of every operand side by side) help?
 // Same tile shape as the product (256 threads x VPT 2 x 16 B, one workgroup
 // per CU via LDS, nt loads and stores).
-//   hipcc -O3 --offload-arch=gfx950 -o tools/hbm_probe3 tools/hbm_probe3.hip
+//   hipcc -O3 --offload-arch=gfx950 -mllvm -amdgpu-kernarg-preload-count=16 \
+//         -o tools/hbm_probe3 tools/hbm_probe3.hip
 //   tools/hbm_probe3 <bucket MiB> [reps]
 // Layouts (one slab per input set, 3 sets rotated):
 //   contig:<pad MiB>   operand k at k * (B + pad + 16 KiB)   (pad 0 = the product's arena)
@@ -36,6 +37,40 @@ struct Geo {
 };
 
 __global__ __launch_bounds__(256) void fold_geo(Geo g) {
+  const unsigned t = blockIdx.x;
+  const unsigned c = t / g.tiles_per_chunk, w = t % g.tiles_per_chunk;
+  char* tb = g.base + (unsigned long long)c * g.group_stride + (unsigned long long)w * kTile;
+  const unsigned off = threadIdx.x * 16u;
+  __amdgpu_buffer_rsrc_t r[kN + 1];
+#pragma unroll
+  for (int k = 0; k <= kN; ++k)
+    r[k] = __builtin_amdgcn_make_buffer_rsrc(tb + (unsigned long long)k * g.op_stride, 0, kTile,
+                                             0x00020000);
+  f4 acc[kVpt];
+#pragma unroll
+  for (int j = 0; j < kVpt; ++j)
+    acc[j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r[0], off + j * 4096u, 0, 2));
+#pragma unroll
+  for (int k = 1; k < kN; ++k) {
+    f4 x[kVpt];
+#pragma unroll
+    for (int j = 0; j < kVpt; ++j)
+      x[j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r[k], off + j * 4096u, 0, 2));
+#pragma unroll
+    for (int j = 0; j < kVpt; ++j) acc[j] += x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < kVpt; ++j)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[j]), r[kN], off + j * 4096u, 0, 2);
+}
+
+// Same tile, arguments as scalars: with -mllvm -amdgpu-kernarg-preload-count
+// they arrive in SGPRs at wave launch (a struct argument is not preloaded), so
+// no kernarg round trip precedes the first data load.
+__global__ __launch_bounds__(256) void fold_geo_sc(char* base, unsigned long long op_stride,
+                                                   unsigned long long group_stride,
+                                                   unsigned tiles_per_chunk) {
+  Geo g{base, op_stride, group_stride, tiles_per_chunk};
   const unsigned t = blockIdx.x;
   const unsigned c = t / g.tiles_per_chunk, w = t % g.tiles_per_chunk;
   char* tb = g.base + (unsigned long long)c * g.group_stride + (unsigned long long)w * kTile;
@@ -96,8 +131,13 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   CK(hipFuncSetAttribute((const void*)fold_geo, hipFuncAttributeMaxDynamicSharedMemorySize,
                          160 * 1024));
+  CK(hipFuncSetAttribute((const void*)fold_geo_sc, hipFuncAttributeMaxDynamicSharedMemorySize,
+                         160 * 1024));
   const unsigned tiles = (unsigned)(B / kTile);
-  for (const std::string& L : layouts) {
+  for (std::string L : layouts) {
+    // "sc-" prefix: the scalar-argument kernel
+    const bool sc = L.rfind("sc-", 0) == 0;
+    if (sc) L = L.substr(3);
     const bool inter = L.rfind("inter:", 0) == 0;
     const size_t arg = (size_t)atol(L.c_str() + L.find(':') + 1);
     Geo g{};
@@ -126,7 +166,11 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e0, st));
       for (int r = 0; r < reps; ++r) {
         g.base = slab[r % 3];
-        hipLaunchKernelGGL(fold_geo, dim3(tiles), dim3(256), 160 * 1024, st, g);
+        if (sc)
+          hipLaunchKernelGGL(fold_geo_sc, dim3(tiles), dim3(256), 160 * 1024, st, g.base,
+                             g.op_stride, g.group_stride, g.tiles_per_chunk);
+        else
+          hipLaunchKernelGGL(fold_geo, dim3(tiles), dim3(256), 160 * 1024, st, g);
       }
       CK(hipEventRecord(e1, st));
       CK(hipEventSynchronize(e1));
@@ -140,8 +184,8 @@ int main(int argc, char** argv) {
     }
     const float avg = sum / 3;
     printf("{\"probe\": \"hbm_probe3\", \"layout\": \"%s\", \"bucket_mib\": %zu, \"ms_avg\": %.4f, "
-           "\"ms_best\": %.4f, \"frac_avg\": %.4f}\n",
-           L.c_str(), B >> 20, avg, best, (kN + 1.0) * B / (avg * 1e-3) / 8e12);
+           "\"ms_best\": %.4f, \"frac_avg\": %.4f, \"scalar_args\": %d}\n",
+           L.c_str(), B >> 20, avg, best, (kN + 1.0) * B / (avg * 1e-3) / 8e12, (int)sc);
     fflush(stdout);
     for (int s = 0; s < 3; ++s) CK(hipFree(slab[s]));
   }
