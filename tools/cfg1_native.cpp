@@ -57,6 +57,7 @@ void on_push(void*, uint64_t, int, int status) {
 int main(int argc, char** argv) {
   const int lanes = argc > 1 ? atoi(argv[1]) : 4;
   const int rounds = argc > 2 ? atoi(argv[2]) : 20;
+  const int only = argc > 3 ? atoi(argv[3]) : -1;  // run one mode only (traces)
   std::vector<float*> host(N);
   for (int k = 0; k < N; ++k) {
     CK(hipHostMalloc(reinterpret_cast<void**>(&host[k]), B, hipHostMallocDefault));
@@ -70,6 +71,7 @@ int main(int argc, char** argv) {
   for (size_t o = 0; o < B; o += kPart) parts17.push_back({o, std::min(kPart, B - o)});
 
   for (int mode = 0; mode < 4; ++mode) {
+    if (only >= 0 && mode != only) continue;
     const int view_pulls = mode == 1;
     const bool device = mode >= 2;
     const auto& parts = mode == 3 ? parts1 : parts17;
