@@ -6,6 +6,8 @@ compared by class against the reference fixtures, whose choice is
 schedule-dependent, but bit-exact against the oracle restatement); ACCUM_F32
 mode within 1 ulp of the exactly rounded sum.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -255,6 +257,55 @@ def test_batched_large_table_vpt4_equals_torch(red, dev):
         for s in srcs[1:]:
             want.add_(s)
         assert torch.equal(dst.view(torch.int32), want.view(torch.int32))
+
+
+_PREFETCH_SCRIPT = r"""
+import hashlib, sys, torch
+sys.path.insert(0, {root!r})
+from prophet_amd.reducer import GpuReducer
+from prophet_amd.dtypes import DType
+red, dev = GpuReducer(device=0), torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(11)
+buckets = []
+for i in range(5):
+    ne = (3 << 20) // 2 + 7 * i
+    srcs = [torch.randn(ne, device=dev, generator=g).half() for _ in range(8)]
+    buckets.append((torch.empty_like(srcs[0]), srcs, ne * 2))
+red.sum_batched(buckets, DType.FLOAT16)
+plan = red.make_plan(buckets, DType.FLOAT16)
+outs = [b[0].clone() for b in buckets]
+for b in buckets:
+    b[0].zero_()
+plan.launch()
+torch.cuda.synchronize()
+h = hashlib.sha256()
+for o, b in zip(outs, buckets):
+    assert torch.equal(o, b[0])
+    h.update(o.view(torch.uint8).cpu().numpy().tobytes())
+print(h.hexdigest())
+"""
+
+
+def test_record_prefetch_knob_changes_no_bits():
+    """BPSR_REC_PREFETCH (the tile-record L2 prefetch of batched launches,
+    plans and block queues) is read once per process: the same batched fold
+    and plan (fp16, 5 ragged buckets, > 256 tiles so the prefetch reaches
+    records) in two child processes, prefetch off and at its default, give
+    the same bytes."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    digests = []
+    for pf in ("0", None):
+        env = dict(os.environ)
+        env.pop("BPSR_REC_PREFETCH", None)
+        if pf is not None:
+            env["BPSR_REC_PREFETCH"] = pf
+        r = subprocess.run([sys.executable, "-c", _PREFETCH_SCRIPT.format(root=root)], env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        digests.append(r.stdout.strip().splitlines()[-1])
+    assert digests[0] == digests[1]
 
 
 @pytest.mark.parametrize("mib", [95, 97])
