@@ -98,6 +98,60 @@ __global__ __launch_bounds__(256) void fold_geo_sc(char* base, unsigned long lon
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[j]), r[kN], off + j * 4096u, 0, 2);
 }
 
+// T consecutive tiles per workgroup (grid = tiles / T), one after the other:
+// PIPE = false: load, add, store each tile in turn; PIPE = true: the next
+// tile's loads are issued before the current tile's adds and stores (two
+// register sets), so the CU's load stream does not pause at tile boundaries
+// and a workgroup is launched / retired once per T tiles.
+template <int T, bool PIPE>
+__global__ __launch_bounds__(256) void fold_multi(char* base, unsigned long long op_stride) {
+  const unsigned off = threadIdx.x * 16u;
+  auto rs = [&](unsigned t, int k) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(base + (unsigned long long)t * kTile +
+                                                 (unsigned long long)k * op_stride, 0, kTile, 0x00020000);
+  };
+  auto issue = [&](f4 (&x)[kN][kVpt], unsigned t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < kN; ++k) {
+      const auto r = rs(t, k);
+#pragma unroll
+      for (int j = 0; j < kVpt; ++j)
+        x[k][j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off + j * 4096u, 0, 2));
+    }
+  };
+  auto finish = [&](f4 (&x)[kN][kVpt], unsigned t) __attribute__((always_inline)) {
+    const auto rd = rs(t, kN);
+#pragma unroll
+    for (int j = 0; j < kVpt; ++j) {
+      f4 acc = x[0][j];
+#pragma unroll
+      for (int k = 1; k < kN; ++k) acc += x[k][j];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc), rd, off + j * 4096u, 0, 2);
+    }
+  };
+  const unsigned t0 = blockIdx.x * T;
+  if constexpr (!PIPE) {
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+      f4 x[kN][kVpt];
+      issue(x, t0 + i);
+      finish(x, t0 + i);
+    }
+  } else {
+    f4 a[kN][kVpt], b[kN][kVpt];
+    issue(a, t0);
+#pragma unroll
+    for (int i = 0; i < T; i += 2) {
+      if (i + 1 < T) issue(b, t0 + i + 1);
+      finish(a, t0 + i);
+      if (i + 1 < T) {
+        if (i + 2 < T) issue(a, t0 + i + 2);
+        finish(b, t0 + i + 1);
+      }
+    }
+  }
+}
+
 __global__ void fill_random(unsigned* p, size_t n, unsigned seed) {
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     unsigned x = (unsigned)i * 2654435761u ^ seed;
@@ -133,11 +187,23 @@ int main(int argc, char** argv) {
                          160 * 1024));
   CK(hipFuncSetAttribute((const void*)fold_geo_sc, hipFuncAttributeMaxDynamicSharedMemorySize,
                          160 * 1024));
+  for (const void* k : {(const void*)fold_multi<1, false>, (const void*)fold_multi<2, false>,
+                        (const void*)fold_multi<4, false>, (const void*)fold_multi<2, true>,
+                        (const void*)fold_multi<4, true>})
+    CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   const unsigned tiles = (unsigned)(B / kTile);
   for (std::string L : layouts) {
     // "sc-" prefix: the scalar-argument kernel
     const bool sc = L.rfind("sc-", 0) == 0;
     if (sc) L = L.substr(3);
+    // "multi:T" / "pipe:T": T tiles per workgroup (contiguous slots)
+    int multi = 0;
+    bool pipe = false;
+    if (L.rfind("multi:", 0) == 0 || L.rfind("pipe:", 0) == 0) {
+      pipe = L[0] == 'p';
+      multi = atoi(L.c_str() + L.find(':') + 1);
+      L = "contig:0";
+    }
     const bool inter = L.rfind("inter:", 0) == 0;
     const size_t arg = (size_t)atol(L.c_str() + L.find(':') + 1);
     Geo g{};
@@ -166,7 +232,15 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e0, st));
       for (int r = 0; r < reps; ++r) {
         g.base = slab[r % 3];
-        if (sc)
+        if (multi) {
+          const unsigned grid = tiles / (unsigned)multi;
+          auto k = pipe ? (multi == 2 ? (const void*)fold_multi<2, true> : (const void*)fold_multi<4, true>)
+                        : (multi == 1 ? (const void*)fold_multi<1, false>
+                                      : multi == 2 ? (const void*)fold_multi<2, false>
+                                                   : (const void*)fold_multi<4, false>);
+          void* args[] = {&g.base, &g.op_stride};
+          CK(hipLaunchKernel(k, dim3(grid), dim3(256), args, 160 * 1024, st));
+        } else if (sc)
           hipLaunchKernelGGL(fold_geo_sc, dim3(tiles), dim3(256), 160 * 1024, st, g.base,
                              g.op_stride, g.group_stride, g.tiles_per_chunk);
         else
@@ -184,8 +258,8 @@ int main(int argc, char** argv) {
     }
     const float avg = sum / 3;
     printf("{\"probe\": \"hbm_probe3\", \"layout\": \"%s\", \"bucket_mib\": %zu, \"ms_avg\": %.4f, "
-           "\"ms_best\": %.4f, \"frac_avg\": %.4f, \"scalar_args\": %d}\n",
-           L.c_str(), B >> 20, avg, best, (kN + 1.0) * B / (avg * 1e-3) / 8e12, (int)sc);
+           "\"ms_best\": %.4f, \"frac_avg\": %.4f, \"scalar_args\": %d, \"tiles_per_wg\": %d, \"pipelined\": %d}\n",
+           L.c_str(), B >> 20, avg, best, (kN + 1.0) * B / (avg * 1e-3) / 8e12, (int)sc, multi ? multi : 1, (int)pipe);
     fflush(stdout);
     for (int s = 0; s < 3; ++s) CK(hipFree(slab[s]));
   }
