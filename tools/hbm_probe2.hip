@@ -197,7 +197,16 @@ int main(int argc, char** argv) {
       {"n1_copy", L<2, 2, 4, false, 1>},
       {"n16_v2_wg1cu", L<2, 2, 2, false, 16, false, 160>},
   };
+  std::vector<V> vs_xmap = {  // blockIdx -> tile maps by bucket size (round 3)
+      {"n8_v2_wg1cu", L<2, 2, 2, false, 8, false, 160>},
+      {"n8_product", PROD<8>},
+      {"n8_v2_wg1cu_xcdchunk4", L<2, 2, 2, false, 8, false, 160, 4>},
+      {"n8_v2_wg1cu_xcdchunk16", L<2, 2, 2, false, 8, false, 160, 16>},
+      {"n8_v2_wg1cu_xcdchunk64", L<2, 2, 2, false, 8, false, 160, 64>},
+      {"n8_v2_wg1cu_xcdchunk256", L<2, 2, 2, false, 8, false, 160, 256>},
+  };
   if (getenv("PROBE_POLICY")) vs = vs_policy;
+  if (getenv("PROBE_XMAP")) vs = vs_xmap;
   const size_t skews[] = {16384};
   for (int rep = 0; rep < 2; ++rep) {
     for (size_t skew : skews) {
