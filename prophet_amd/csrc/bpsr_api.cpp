@@ -376,7 +376,11 @@ static int build_table(const byteps_bucket_desc* buckets, int nbuckets, int dtyp
   return BYTEPS_REDUCE_OK;
 }
 
-static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti) {
+// `in_hbm`: the records live in device memory.  A table read zero-copy from
+// pinned host staging (batched_with_ring, small tables) is not prefetched:
+// host pages are not cached in L2, so the touch would only add a PCIe round
+// trip that every workgroup waits for before it retires.
+static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti, bool in_hbm = true) {
   BatchLaunch L;
   L.entries = static_cast<const BatchEntry*>(dev_table);
   L.recs = static_cast<const unsigned char*>(dev_table) + ti.recs_off;
@@ -389,7 +393,7 @@ static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti) {
     const long x = v ? atol(v) : (long)kPrefetchAhead;
     return x > 0 ? (uint32_t)((x + 7) & ~7L) : 0u;  // a multiple of 8: the same XCD
   }();
-  L.pf_ahead = ahead;
+  L.pf_ahead = in_hbm ? ahead : 0u;
   return L;
 }
 
@@ -415,7 +419,8 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
     table = slot->dev;
   }
-  e = launch_batched(batch_launch(table, ti), ti.vpt, dtype, mode, tuning_for_n(ti.nmax), s);
+  e = launch_batched(batch_launch(table, ti, table == slot->dev), ti.vpt, dtype, mode,
+                     tuning_for_n(ti.nmax), s);
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
   e = hipEventRecord(slot->done, s);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");
