@@ -394,6 +394,7 @@ static BatchLaunch batch_launch(const void* dev_table, const TableInfo& ti, bool
     return x > 0 ? (uint32_t)((x + 7) & ~7L) : 0u;  // a multiple of 8: the same XCD
   }();
   L.pf_ahead = in_hbm ? ahead : 0u;
+  L.stop = nullptr;
   return L;
 }
 
@@ -419,6 +420,10 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
     table = slot->dev;
   }
+  // (The slot's event stays a separate record: completing it by the launch
+  // itself, like the block queue's join, made the server's lane issuers see
+  // completions sooner and split config 3's rounds into more, smaller
+  // launches — 33-43 instead of 23-31 per round at 4 lanes, r03s57.)
   e = launch_batched(batch_launch(table, ti, table == slot->dev), ti.vpt, dtype, mode,
                      tuning_for_n(ti.nmax), s);
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
@@ -862,8 +867,8 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(own, q->fork_ev, 0);
   }
+  if (fork) Q.L.stop = q->join_ev;  // the consumer's own completion joins `s` back
   if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16), lds, gated, q->dtype, q->mode, ls);
-  if (fork && e == hipSuccess) e = hipEventRecord(q->join_ev, own);
   if (fork && e == hipSuccess) e = hipStreamWaitEvent(s, q->join_ev, 0);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
 }

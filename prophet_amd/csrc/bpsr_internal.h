@@ -86,6 +86,11 @@ struct BatchLaunch {
   uint32_t rec_stride;
   uint32_t tiles;
   uint32_t pf_ahead;            // L2 prefetch of record blockIdx + pf_ahead (0 = off)
+  // Host side only (the kernels ignore it): when set, the launch itself
+  // completes this event (hipExtLaunchKernel's stop event) instead of a
+  // separate hipEventRecord behind it — a marker packet between two kernels
+  // costs 3-5 us of the stream's device time (profiles/r03_event_marker_cost.jsonl).
+  hipEvent_t stop;
 };
 
 // Block consumer (byteps_reduce_blockq_*).  One launch folds the whole table;

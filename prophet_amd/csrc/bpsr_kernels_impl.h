@@ -25,6 +25,7 @@
 //     path with the reference's tail semantics.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -642,6 +643,18 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
 
 // ------------------------------------------------------------- launchers ----
 
+// One launch of `kernel(arg)`; with `stop`, the kernel's own completion
+// signal completes the event (hipExtLaunchKernel) — no marker packet behind it.
+template <class K, class A>
+static hipError_t launch_with_stop(K kernel, uint32_t grid, size_t lds, hipStream_t s,
+                                   hipEvent_t stop, const A& arg) {
+  if (stop)
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), (uint32_t)lds, s, nullptr, stop, 0, arg);
+  else
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, s, arg);
+  return hipGetLastError();
+}
+
 template <class Op, int VPT, int NT, int NS>
 static hipError_t launch_fold_ns(const FoldArgs& a, const Tuning& tu, hipStream_t s) {
   static KernelAttr attr;
@@ -706,17 +719,10 @@ static hipError_t launch_batched_vpt(const BatchLaunch& L, const Tuning& tu, hip
   if (L.tiles == 0) return hipSuccess;
   const size_t lds = occ_lds_bytes(launch_occ(tu, L.tiles, true));
   switch (cache_pol(tu, (uint64_t)L.tiles * VPT * kBlock * 16)) {
-    case kPolNt:
-      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolNt>), dim3(L.tiles), dim3(kBlock), lds, s, L);
-      break;
-    case kPolWt:
-      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolWt>), dim3(L.tiles), dim3(kBlock), lds, s, L);
-      break;
-    default:
-      hipLaunchKernelGGL((batched_kernel<Op, VPT, kPolPlain>), dim3(L.tiles), dim3(kBlock), lds, s,
-                         L);
+    case kPolNt: return launch_with_stop(batched_kernel<Op, VPT, kPolNt>, L.tiles, lds, s, L.stop, L);
+    case kPolWt: return launch_with_stop(batched_kernel<Op, VPT, kPolWt>, L.tiles, lds, s, L.stop, L);
+    default: return launch_with_stop(batched_kernel<Op, VPT, kPolPlain>, L.tiles, lds, s, L.stop, L);
   }
-  return hipGetLastError();
 }
 
 template <class Op>
@@ -736,8 +742,7 @@ static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated,
     const hipError_t okg =
         allow_lds(attr_g, reinterpret_cast<const void*>(&blockq_gate_kernel<Op, VPT, NT>));
     if (okg != hipSuccess) return okg;
-    hipLaunchKernelGGL((blockq_gate_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
-    return hipGetLastError();
+    return launch_with_stop(blockq_gate_kernel<Op, VPT, NT>, Q.grid, lds, s, Q.L.stop, Q);
   }
   // the kernel's own static LDS (the record staging words) comes on top of the
   // dynamic residency request, so allow 256 B less than the CU's 160 KiB
@@ -745,8 +750,7 @@ static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated,
   const hipError_t ok = allow_lds(attr_p, reinterpret_cast<const void*>(&blockq_kernel<Op, VPT, NT>),
                                   (int)kLdsPerCU - 256);
   if (ok != hipSuccess) return ok;
-  hipLaunchKernelGGL((blockq_kernel<Op, VPT, NT>), dim3(Q.grid), dim3(kBlock), lds, s, Q);
-  return hipGetLastError();
+  return launch_with_stop(blockq_kernel<Op, VPT, NT>, Q.grid, lds, s, Q.L.stop, Q);
 }
 
 template <class Op, int VPT>

@@ -239,6 +239,13 @@ int main(int argc, char** argv) {
     CKR(byteps_reduce_blockq_release(s.q, -1, cons));
     CKR(byteps_reduce_blockq_launch(s.q, cons));
   };
+  // launched from a caller's own stream: the library forks the consumer onto
+  // its own hardware queue and joins it back (byteps_reduce_blockq_launch)
+  const Fn pre_released_forked = [&](int i) {
+    Set& s = sets[i % kSets];
+    CKR(byteps_reduce_blockq_release(s.q, -1, rel[1]));
+    CKR(byteps_reduce_blockq_launch(s.q, rel[1]));
+  };
   const Fn live = [&](int i) {  // one release per block, behind the launch, on a second stream
     Set& s = sets[i % kSets];
     CKR(byteps_reduce_blockq_launch(s.q, cons));
@@ -358,6 +365,7 @@ int main(int argc, char** argv) {
   };
   std::vector<V> variants = {{"plan_all_partitions_no_blocks", &plan_no_blocks},
                              {"blockq_pre_released", &pre_released},
+                             {"blockq_pre_released_forked", &pre_released_forked},
                              {"blockq_live_release", &live},
                              {"blockq_live_release_2streams", &live_2streams},
                              {"blockq_live_release_ranges4", &live_ranges},
