@@ -955,6 +955,10 @@ def pmc_traffic(workload: str):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    # RCCL and cross-process device memory on this ROCm stack need dmabuf IPC
+    # (the legacy IPC path fails with `hipIpcGetMemHandle: invalid argument`):
+    # keep it on for every rank, whoever launched us, before any HIP call.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # Parent: start one process per GPU before anything touches the GPU.
         sys.exit(launch_ranks(args.gpus, argv))
