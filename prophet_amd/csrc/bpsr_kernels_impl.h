@@ -427,11 +427,11 @@ __device__ __forceinline__ RecRegs regs_from_words(const uint32_t* w) {
 // fetch is a dependent round trip at the head of every workgroup (nothing
 // else can issue before the pointers arrive), and at one or two resident
 // workgroups per CU it is not hidden behind another workgroup's loads.  A
-// workgroup touches the record of the workgroup dispatched kPrefetchAhead
-// later (L.pf_ahead, default kPrefetchAhead) — the same XCD (workgroups go
-// to the 8 XCDs round-robin, and the distance is a multiple of 8), about one
-// resident round ahead — so
-// that record is in the XCD's L2 when its workgroup starts.  Two lanes, one
+// workgroup touches the record of the workgroup dispatched L.pf_ahead later
+// (default kPrefetchAhead) — the same XCD (workgroups go to the 8 XCDs
+// round-robin, and the distance is a multiple of 8), about one resident round
+// ahead — so that record is in the XCD's L2 when its workgroup starts.  Tables
+// read zero-copy from host memory are not prefetched (pf_ahead 0).  Two lanes, one
 // dword at each end of the record (a 96-B record may straddle two 128-B
 // lines).  The values are consumed by keep_prefetch at the very end, after
 // the tile's own loads and stores were issued, so no wait lands earlier.
