@@ -55,6 +55,9 @@ def test_bench_one_gpu_line_has_every_object():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["check_vs_torch_fold"] is True
     assert "device" not in line                      # a measurement, not a self-test
+    blk = line["roofline"]["kernel_ms_blocks"]       # the spread object
+    assert 0 < blk["min"] <= blk["median"] <= blk["max"]
+    assert blk["median"] < 2 * line["roofline"]["kernel_ms"]
     assert line["scaling_cfg4"]["exact_vs_torch_fold"] is True
     f16 = line["fp16"]
     assert "error" not in f16, f16
