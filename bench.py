@@ -117,7 +117,8 @@ def parse(argv=None):
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N > 1 rehearsal on a 1-GPU box: every rank on cuda:0 with the HIP "
                         "fold, gloo for the barrier / max-over-ranks (RCCL refuses two ranks "
-                        "on one GPU); no scatter leg; the line is marked, not a measurement")
+                        "on one GPU); the scatter and local-reduce legs move CUDA tensors "
+                        "through gloo; the line is marked, not a measurement")
     return p.parse_args(argv)
 
 
@@ -983,8 +984,11 @@ def main(argv=None):
               file=sys.stderr)
     cuda = args.device == "cuda"
     rehearse = cuda and args.rehearse_one_gpu and world > 1
-    if rehearse:
-        args.no_scatter = True
+    # Exchange legs (scatter, local reduce) rehearsed on one GPU move CUDA
+    # tensors through gloo's host staging, far slower than RCCL over xGMI:
+    # there they run on a 4,000,037-element vector unless --scaling-elems
+    # says otherwise (the legs' code and checks are the point, not the rate).
+    xchg_elems = args.scaling_elems or (4_000_037 if rehearse else None)
     gpu = 0 if rehearse else local_rank
     if cuda:
         # Bind this rank's GPU before the process group exists, so RCCL's
@@ -1142,7 +1146,8 @@ def main(argv=None):
         line["device"] = "cpu plumbing self-test (torch CPU add, gloo): NOT a measurement"
     if rehearse:
         line["device"] = (f"rehearsal: {world} ranks sharing cuda:0 over gloo (HIP fold, "
-                          "no RCCL, no scatter leg): NOT a measurement")
+                          "no RCCL: the scatter and local-reduce legs move CUDA tensors "
+                          f"through gloo, {xchg_elems} elements): NOT a measurement")
 
     def extra_legs(state=None):
         def leg(name):
@@ -1159,7 +1164,7 @@ def main(argv=None):
                 leg("scatter")
                 try:
                     line["scaling_cfg4"]["scatter"] = scatter_leg(
-                        dev, world, rank, N, n_elems=args.scaling_elems or None,
+                        dev, world, rank, N, n_elems=xchg_elems,
                         fold=None if cuda else _torch_fold)
                 except Exception as e:  # report, never hide
                     line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
@@ -1167,7 +1172,7 @@ def main(argv=None):
             leg("local_reduce")
             try:
                 line["local_reduce"] = local_reduce_leg(
-                    dev, world, rank, n_elems=args.scaling_elems or None,
+                    dev, world, rank, n_elems=xchg_elems,
                     fold=None if cuda else _torch_fold)
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}

@@ -2,7 +2,8 @@
 rank processes (the launcher the driver's scaling run uses), both fold with
 the HIP kernel on cuda:0, gloo carries the barrier and max-over-ranks (RCCL
 refuses two ranks on one GPU), and the config-4 sharded fold runs at world
-size 2 with its G=1 reference measured on rank 0.  One JSON line comes back."""
+size 2 with its G=1 reference measured on rank 0, and the scatter and
+local-reduce legs run over gloo with CUDA tensors.  One JSON line comes back."""
 import json
 import os
 import subprocess
@@ -36,7 +37,11 @@ def test_bench_two_ranks_rehearsed_on_one_gpu():
     assert sc["exact_vs_torch_fold"] is True, sc
     assert sum(sc["shard_elems"]) == 4000037 and len(sc["shard_elems"]) == 2
     assert sc["g1_fold_ms"] > 0 and sc["per_gpu_fold_ms"] > 0
-    assert "scatter" not in sc
+    # the N > 1 exchange legs' code on one GPU: gloo moves the CUDA tensors
+    assert sc["scatter"]["exact_vs_torch_fold"] is True, sc["scatter"]
+    lr = line["local_reduce"]
+    assert "error" not in lr, lr
+    assert lr["exact_vs_rank_order_fold"] is True
 
 
 def test_bench_one_gpu_line_has_every_object():
@@ -57,7 +62,7 @@ def test_bench_one_gpu_line_has_every_object():
     assert "device" not in line                      # a measurement, not a self-test
     blk = line["roofline"]["kernel_ms_blocks"]       # the spread object
     assert 0 < blk["min"] <= blk["median"] <= blk["max"]
-    assert blk["median"] < 2 * line["roofline"]["kernel_ms"]
+    assert blk["median"] < 3 * line["roofline"]["kernel_ms"]
     assert line["scaling_cfg4"]["exact_vs_torch_fold"] is True
     f16 = line["fp16"]
     assert "error" not in f16, f16
