@@ -517,8 +517,14 @@ void queue_pull_copy(byteps_server* s, KeyState* ks, void* dst, size_t len,
   L.comb_cv.notify_one();
 }
 
+// Set on the responder thread, which runs the callers' callbacks: a blocking
+// call made from inside a callback takes its own direct path, since routing it
+// through the responder would wait on itself.
+thread_local bool t_responder = false;
+
 void responder_main(byteps_server* s) {
   (void)hipSetDevice(s->cfg.device);
+  t_responder = true;
   for (;;) {
     Response r;
     {
@@ -1252,11 +1258,67 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
   return allocate(s, ks, len, dtype);
 }
 
+}  // extern "C"
+
+namespace bpsr {
+namespace {
+// A blocking call served by the non-blocking machinery: the lane issuer
+// batches the copy with whatever else piled up, the completer and responder
+// finish it, and the caller waits here without making a HIP call.  (HIP
+// calls serialise across threads: eight workers each making 4-5 calls per
+// key paid ~8 us per call)
+struct SyncWait {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  int status = 0;
+  int wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+    return status;
+  }
+  void finish(int st) {
+    std::lock_guard<std::mutex> g(mu);
+    status = st;
+    done = true;
+    cv.notify_all();
+  }
+};
+void sync_push_cb(void* ctx, uint64_t, int, int status) {
+  static_cast<SyncWait*>(ctx)->finish(status);
+}
+void sync_pull_cb(void* ctx, uint64_t, const void*, size_t, int status) {
+  static_cast<SyncWait*>(ctx)->finish(status);
+}
+// The caller's thread-local message for a status that came back through a callback.
+int sync_status(byteps_server* s, uint64_t key, int status, const char* what) {
+  if (status == 0) return 0;
+  KeyState* ks = get_key(s, key, false);
+  std::string msg = "?";
+  if (ks) {
+    std::lock_guard<std::mutex> g(ks->mu);
+    msg = ks->error_msg;
+  }
+  return fail(status, "key %llu: %s failed: %s", (unsigned long long)key, what, msg.c_str());
+}
+}  // namespace
+}  // namespace bpsr
+
+extern "C" {
+
 int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
                        int dtype, int location) {
   if (!s || !data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   if (worker < 0 || worker >= s->cfg.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  if (location == BYTEPS_SERVER_DEVICE && s->combine && !t_responder) {
+    // device data: the copy goes through the lane issuer (batched with the
+    // other pushes that piled up) and the push returns once it has landed
+    SyncWait w;
+    int rc = byteps_server_push_async(s, key, worker, data, len, dtype, location, sync_push_cb, &w);
+    if (rc) return rc;
+    return sync_status(s, key, w.wait(), "push");
+  }
   int rc = set_device(s);
   if (rc) return rc;
   KeyState* ks = get_key(s, key, true);
@@ -1390,6 +1452,14 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
 
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location) {
   if (!s || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  if (location == BYTEPS_SERVER_DEVICE && s->combine && !s->cfg.async_mode && !t_responder) {
+    // into device memory: one of the lane issuer's batched pull copies; the
+    // pull is counted (server.cc:105-113) before this call returns
+    SyncWait w;
+    int rc = byteps_server_pull_into_async(s, key, out, len, location, sync_pull_cb, &w);
+    if (rc) return rc;
+    return sync_status(s, key, w.wait(), "pull");
+  }
   int rc = set_device(s);
   if (rc) return rc;
   KeyState* ks = key_for_pull(s, key);

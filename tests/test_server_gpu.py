@@ -1198,3 +1198,39 @@ def test_engine_blocking_mode(port, policy):
         assert config_from_env().engine_blocking == 1
     finally:
         del os.environ["BYTEPS_SERVER_ENGINE_BLOCKING"]
+
+
+def test_blocking_device_calls_from_a_callback(port):
+    """Blocking device pushes and pulls are served by the lane issuer and the
+    responder (the caller waits without a HIP call).  One made from inside a
+    callback — on the responder thread itself — takes the direct path instead
+    of waiting on itself: a pull_async callback that makes the other worker's
+    blocking device pull completes, and both answers are the oracle's fold."""
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 100_003
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=1)
+    _init_round(srv, dt, N, [n])
+    dev = torch.device("cuda", 0)
+    for rnd in range(1, 3):
+        out = torch.zeros(n * es, dtype=torch.uint8, device=dev)
+        res, fired = {}, threading.Semaphore(0)
+
+        def cb(key, view, status):
+            res["async"] = (status, None if view is None else bytes(view))
+            srv.pull(key, out)                      # blocking, on the responder thread
+            torch.cuda.synchronize()
+            res["blocking"] = out.cpu().numpy().tobytes()
+            fired.release()
+        srv.pull_async(0, cb)
+        ins = [data(dt, n, w, rnd, 0) for w in range(N)]
+        for w in range(N):                          # blocking device pushes
+            srv.push(0, w, torch.from_numpy(ins[w].copy()).to(dev), dt)
+        assert fired.acquire(timeout=60)
+        want = np.zeros(n * es, np.uint8)
+        port.sum_n(want, ins, n * es, dt)
+        assert res["async"][0] == 0
+        assert np.array_equal(np.frombuffer(res["async"][1], np.uint8), want)
+        assert np.array_equal(np.frombuffer(res["blocking"], np.uint8), want)
+        assert srv.key_info(0)[0] == rnd
+    srv.close()
