@@ -120,7 +120,12 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
 int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 
 /* A worker's pull: blocks until the key's current round is finished (sync mode),
- * then copies the store (len bytes) to `out`. */
+ * then copies the store (len bytes) to `out`.  Into device memory with the
+ * default engine in sync mode, the copy is one of the lane issuer's batched
+ * pull copies and the call waits for the responder's answer (no HIP call on
+ * the caller's thread) — except when called from inside a callback (on the
+ * responder thread), which copies directly.  The same holds for blocking
+ * pushes of device data (byteps_server_push). */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
 /* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
