@@ -68,13 +68,41 @@ struct Response {
   size_t len = 0;
 };
 
+// A blocking call served by the non-blocking machinery: the lane issuer
+// batches the copy with whatever else piled up, the completer and responder
+// finish it, and the caller waits here without making a HIP call.  (HIP
+// calls serialise across threads: eight workers each making 4-5 calls per
+// key paid ~8 us per call, DESIGN.md §9.)
+struct Lane;
+struct SyncWait {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  int status = 0;
+  Lane* lane = nullptr;  // a direct pull: the launch its copy rides in
+  uint64_t seq = 0;
+  int wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+    return status;
+  }
+  void finish(int st) {
+    std::lock_guard<std::mutex> g(mu);
+    status = st;
+    done = true;
+    cv.notify_all();
+  }
+};
 // A non-blocking pull into a caller's device buffer (byteps_server_pull_into_async)
-// whose copy waits for the lane's issuer.
+// whose copy waits for the lane's issuer.  `direct`: a blocking pull's waiter,
+// told the launch's seq by the issuer and then waiting on the lane's
+// completion itself (no responder hop).
 struct PullJob {
   KeyState* ks = nullptr;
   void* dst = nullptr;
   size_t len = 0;
   Response resp;
+  SyncWait* direct = nullptr;
 };
 
 // A non-blocking push of device data whose copy into its slot waits for the
@@ -969,6 +997,12 @@ void issue_pull_copies(byteps_server* s, Lane& L, std::vector<PullJob>& jobs) {
   }
   s->n_pulls.fetch_add(jobs.size(), std::memory_order_relaxed);
   for (auto& j : jobs) {
+    if (j.direct) {  // a blocking pull waits on the lane itself, then counts
+      j.direct->lane = &L;
+      j.direct->seq = seq;
+      j.direct->finish(rc);
+      continue;
+    }
     if (rc) {
       j.resp.status = rc;
     } else {
@@ -1262,32 +1296,7 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
 
 namespace bpsr {
 namespace {
-// A blocking call served by the non-blocking machinery: the lane issuer
-// batches the copy with whatever else piled up, the completer and responder
-// finish it, and the caller waits here without making a HIP call.  (HIP
-// calls serialise across threads: eight workers each making 4-5 calls per
-// key paid ~8 us per call, DESIGN.md §9.)
-struct SyncWait {
-  std::mutex mu;
-  std::condition_variable cv;
-  bool done = false;
-  int status = 0;
-  int wait() {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done; });
-    return status;
-  }
-  void finish(int st) {
-    std::lock_guard<std::mutex> g(mu);
-    status = st;
-    done = true;
-    cv.notify_all();
-  }
-};
 void sync_push_cb(void* ctx, uint64_t, int, int status) {
-  static_cast<SyncWait*>(ctx)->finish(status);
-}
-void sync_pull_cb(void* ctx, uint64_t, const void*, size_t, int status) {
   static_cast<SyncWait*>(ctx)->finish(status);
 }
 // The caller's thread-local message for a status that came back through a callback.
@@ -1453,12 +1462,38 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location) {
   if (!s || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   if (location == BYTEPS_SERVER_DEVICE && s->combine && !s->cfg.async_mode && !t_responder) {
-    // into device memory: one of the lane issuer's batched pull copies; the
-    // pull is counted (server.cc:105-113) before this call returns
-    SyncWait w;
-    int rc = byteps_server_pull_into_async(s, key, out, len, location, sync_pull_cb, &w);
+    // into device memory: one of the lane issuer's batched pull copies; this
+    // thread waits for the launch to complete and counts the pull
+    // (server.cc:105-113) itself — no HIP call here, no responder hop
+    int rc = set_device(s);
     if (rc) return rc;
-    return sync_status(s, key, w.wait(), "pull");
+    KeyState* ks = key_for_pull(s, key);
+    if (!ks) return BYTEPS_REDUCE_EARGS;
+    std::unique_lock<std::mutex> lk(ks->mu);
+    if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
+    ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
+    if (ks->error) return key_error(ks);
+    SyncWait w;
+    PullJob j;
+    j.ks = ks;
+    j.dst = out;
+    j.len = len;
+    j.direct = &w;
+    {
+      Lane& L = *s->lanes[ks->lane];
+      std::lock_guard<std::mutex> g(L.comb_mu);
+      L.pulls.push_back(j);
+      L.comb_cv.notify_one();
+    }
+    lk.unlock();
+    if ((rc = w.wait())) return sync_status(s, key, rc, "pull");
+    {
+      std::unique_lock<std::mutex> dl(w.lane->done_mu);
+      w.lane->done_cv.wait(dl, [&] { return w.lane->done_seq >= w.seq; });
+    }
+    lk.lock();
+    count_pull(s, ks);  // as the old path: after the copy has completed
+    return BYTEPS_REDUCE_OK;
   }
   int rc = set_device(s);
   if (rc) return rc;
