@@ -79,7 +79,7 @@ struct SyncWait {
   std::condition_variable cv;
   bool done = false;
   int status = 0;
-  Lane* lane = nullptr;  // a direct pull: the launch its copy rides in
+  Lane* lane = nullptr;  // a direct pull or push: the launch its copy rides in
   uint64_t seq = 0;
   int wait() {
     std::unique_lock<std::mutex> lk(mu);
@@ -113,6 +113,7 @@ struct CopyJob {
   const void* src = nullptr;
   size_t len = 0;
   Response ack;
+  SyncWait* direct = nullptr;  // a blocking push's waiter (no responder hop)
 };
 
 struct Lane {
@@ -958,6 +959,12 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
       j.ack.wait_lane = &L;
       j.ack.wait_seq = seq;
     }
+    if (j.direct) {  // a blocking push waits on the lane itself
+      j.direct->lane = rc ? nullptr : &L;
+      j.direct->seq = seq;
+      j.direct->finish(rc);
+      continue;
+    }
     enqueue_response(s, j.ack);
   }
   jobs.clear();
@@ -1296,6 +1303,9 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
 
 namespace bpsr {
 namespace {
+int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
+                    int dtype, int location, byteps_server_push_cb cb, void* ctx,
+                    SyncWait* direct);
 void sync_push_cb(void* ctx, uint64_t, int, int status) {
   static_cast<SyncWait*>(ctx)->finish(status);
 }
@@ -1322,11 +1332,19 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
   if (location == BYTEPS_SERVER_DEVICE && s->combine && !t_responder) {
     // device data: the copy goes through the lane issuer (batched with the
-    // other pushes that piled up) and the push returns once it has landed
+    // other pushes that piled up) and the push returns once it has landed;
+    // an issuer-batched copy reports here directly and this thread waits for
+    // the launch to complete (no responder hop), other arrivals answer
+    // through the callback as a non-blocking push would
     SyncWait w;
-    int rc = byteps_server_push_async(s, key, worker, data, len, dtype, location, sync_push_cb, &w);
+    int rc = push_async_impl(s, key, worker, data, len, dtype, location, sync_push_cb, &w, &w);
     if (rc) return rc;
-    return sync_status(s, key, w.wait(), "push");
+    if ((rc = w.wait())) return sync_status(s, key, rc, "push");
+    if (w.lane) {
+      std::unique_lock<std::mutex> dl(w.lane->done_mu);
+      w.lane->done_cv.wait(dl, [&] { return w.lane->done_seq >= w.seq; });
+    }
+    return BYTEPS_REDUCE_OK;
   }
   int rc = set_device(s);
   if (rc) return rc;
@@ -1351,6 +1369,19 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
 int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
                              size_t len, int dtype, int location, byteps_server_push_cb cb,
                              void* ctx) {
+  return push_async_impl(s, key, worker, data, len, dtype, location, cb, ctx, nullptr);
+}
+
+}  // extern "C"
+
+namespace bpsr {
+namespace {
+// byteps_server_push_async; with `direct`, a blocking push's issuer-batched
+// copy reports to its waiter instead of the responder (cb/ctx serve the
+// other paths, answered through the responder as for any non-blocking push).
+int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
+                    int dtype, int location, byteps_server_push_cb cb, void* ctx,
+                    SyncWait* direct) {
   if (!s || !data || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   if (worker < 0 || worker >= s->cfg.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
@@ -1376,6 +1407,7 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
     cj.ack.ctx = ctx;
     cj.ack.push_cb = cb;
     cj.ack.worker = worker;
+    cj.direct = direct;
     {
       Lane& L = *s->lanes[ks->lane];
       std::lock_guard<std::mutex> g(L.comb_mu);
@@ -1419,6 +1451,10 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
   }
   return BYTEPS_REDUCE_OK;
 }
+}  // namespace
+}  // namespace bpsr
+
+extern "C" {
 
 int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** slot) {
   if (!s || !slot) return fail(BYTEPS_REDUCE_EARGS, "null argument");
