@@ -74,14 +74,44 @@ struct Response {
 // calls serialise across threads: eight workers each making 4-5 calls per
 // key paid ~8 us per call)
 struct Lane;
+// BPSR_SERVER_SPIN_US: how long a blocking call's waiter polls before it
+// sleeps on a condition variable (0: sleep at once).  A sleeping waiter's
+// wake-up is a futex round trip per hand-off.
+int64_t spin_ns() {
+  static const int64_t ns = [] {
+    const char* v = getenv("BPSR_SERVER_SPIN_US");
+    return v ? std::max(0L, atol(v)) * 1000L : 0L;
+  }();
+  return ns;
+}
+// Poll `ready` for up to spin_ns(); true once it holds.
+template <class F>
+bool spin_until(F ready) {
+  const int64_t budget = spin_ns();
+  if (budget == 0) return false;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    for (int i = 0; i < 64; ++i) {
+      if (ready()) return true;
+      __builtin_ia32_pause();
+    }
+    if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+            .count() > budget)
+      return ready();
+  }
+}
 struct SyncWait {
   std::mutex mu;
   std::condition_variable cv;
   bool done = false;
+  std::atomic<bool> flag{false};  // `done`, set under mu, for a spinning waiter
   int status = 0;
   Lane* lane = nullptr;  // a direct pull or push: the launch its copy rides in
   uint64_t seq = 0;
   int wait() {
+    // a waiter that saw the flag still takes mu, so it returns (and the
+    // caller's frame goes) only after finish() has let go of it
+    (void)spin_until([&] { return flag.load(std::memory_order_acquire); });
     std::unique_lock<std::mutex> lk(mu);
     cv.wait(lk, [&] { return done; });
     return status;
@@ -90,6 +120,7 @@ struct SyncWait {
     std::lock_guard<std::mutex> g(mu);
     status = st;
     done = true;
+    flag.store(true, std::memory_order_release);
     cv.notify_all();
   }
 };
@@ -155,6 +186,7 @@ struct Lane {
   std::condition_variable done_cv;  // completer -> waiters (and the issuer)
   std::deque<std::pair<uint64_t, hipEvent_t>> cq;
   uint64_t issued_seq = 0, done_seq = 0;
+  std::atomic<uint64_t> done_pub{0};  // done_seq, readable without done_mu (spinning waiters)
   bool cq_stop = false;
   std::thread completer;
   // copies recorded into copy_mark so far / seen by a fold's wait on it (a
@@ -315,6 +347,7 @@ void completer_main(byteps_server* s, int lane) {
     lk.lock();
     L.cq.pop_front();
     L.done_seq = seq;
+    L.done_pub.store(seq, std::memory_order_release);
     L.done_cv.notify_all();
   }
 }
@@ -1306,6 +1339,12 @@ namespace {
 int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
                     int dtype, int location, byteps_server_push_cb cb, void* ctx,
                     SyncWait* direct);
+// A blocking call's wait for the lane's launch `seq` to complete.
+void wait_lane_done(Lane& L, uint64_t seq) {
+  if (spin_until([&] { return L.done_pub.load(std::memory_order_acquire) >= seq; })) return;
+  std::unique_lock<std::mutex> dl(L.done_mu);
+  L.done_cv.wait(dl, [&] { return L.done_seq >= seq; });
+}
 void sync_push_cb(void* ctx, uint64_t, int, int status) {
   static_cast<SyncWait*>(ctx)->finish(status);
 }
@@ -1340,10 +1379,7 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
     int rc = push_async_impl(s, key, worker, data, len, dtype, location, sync_push_cb, &w, &w);
     if (rc) return rc;
     if ((rc = w.wait())) return sync_status(s, key, rc, "push");
-    if (w.lane) {
-      std::unique_lock<std::mutex> dl(w.lane->done_mu);
-      w.lane->done_cv.wait(dl, [&] { return w.lane->done_seq >= w.seq; });
-    }
+    if (w.lane) wait_lane_done(*w.lane, w.seq);
     return BYTEPS_REDUCE_OK;
   }
   int rc = set_device(s);
@@ -1523,10 +1559,7 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
     }
     lk.unlock();
     if ((rc = w.wait())) return sync_status(s, key, rc, "pull");
-    {
-      std::unique_lock<std::mutex> dl(w.lane->done_mu);
-      w.lane->done_cv.wait(dl, [&] { return w.lane->done_seq >= w.seq; });
-    }
+    wait_lane_done(*w.lane, w.seq);
     lk.lock();
     count_pull(s, ks);  // as the old path: after the copy has completed
     return BYTEPS_REDUCE_OK;
