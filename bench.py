@@ -186,11 +186,12 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
     ``sum`` calls (server.cc:127-130 SUM_RECV) and the ``copy`` to the store
     (server.cc:91 COPY_MERGED), timed with the clean-room restatement
     (oracle/bpsr_oracle.c, OpenMP like cpu_reducer.cc:85-92; bit-identical to
-    the reference on every golden vector).  Also, as a secondary field only,
-    the reference's own CpuReducer when oracle/_ref was built."""
+    the reference on every golden vector).  The reference's own build
+    (oracle/_ref) pins the restatement in the build container's tests; it
+    never travels to the GPU box (.gpurunignore)."""
     import numpy as np
 
-    from oracle.oracle import PortReducer, RefReducer
+    from oracle.oracle import PortReducer
     from prophet_amd import synth
 
     es = {0: 4, 1: 8, 2: 2, 3: 1, 4: 4, 5: 1, 6: 8, 11: 2}[dtype_id]
@@ -258,17 +259,8 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
         share = 0
     all_threads = max(1, min(share or ncpu, 64))
     impls = {"port": (_Baseline(4), 1.0), "all": (_Baseline(all_threads), 0.4)}
-    with_ref = dtype_id != 11 and RefReducer.available()
-    if with_ref:
-        impls["ref"] = (RefReducer(nthreads=4), 0.4)
     res = legs(impls, 10)
     default, allc = res["port"], res["all"]
-    ref = None
-    if with_ref:
-        r = res["ref"]
-        ref = {"value": round(r["gibps"], 3), "cores": 4, "reps": r["reps"],
-               "what": "the reference's own cpu_reducer.cc built from /root/reference "
-                       "(oracle/_ref), secondary only; timed interleaved with the port"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -290,7 +282,6 @@ def cpu_baseline(n_workers: int, dtype_id: int, sample_mib: float) -> dict | Non
                    f"BYTEPS_OMP_THREAD_PER_GPU default (cpu_reducer.cc:40-44)"),
         "all_cores": {"value": round(allc["gibps"], 3), "cores": all_threads,
                       "reps": allc["reps"]},
-        "reference_build": ref,
         "cpu_model": cpu_model, "host_cpus": ncpu,
     }
 
@@ -486,14 +477,47 @@ def scaling_leg(dev, world: int, rank: int, n_workers: int, fold, reps: int = 20
     return res
 
 
+def shard_comm(dev):
+    """The shard C ABI's communicator (include/bpsr/shard.h) for this rank:
+    torch's own ProcessGroupNCCL communicator wrapped (the caller-owned
+    ncclComm_t a core_loops.cc caller passes from NcclManager::GetComm), else
+    a communicator of the library's own (unique id carried over the torch
+    group, NcclManager::ConstructRings).  Returns (ShardComm, how)."""
+    import torch.distributed as dist
+    from prophet_amd.shard import ShardComm
+    try:
+        ptr = dist.group.WORLD._get_backend(dev)._comm_ptr()
+        if ptr:
+            return ShardComm.wrap(ptr), "wrapped torch ProcessGroupNCCL communicator"
+    except Exception:  # noqa: BLE001 — fall back to a communicator of our own
+        pass
+    return (ShardComm.from_group(device=dev.index),
+            "library-owned RCCL communicator (unique id over the torch group)")
+
+
+def _transport(comm) -> str:
+    return "rccl-shard-abi" if comm is not None else "torch-p2p"
+
+
+def uses_shard_abi(world: int, cuda: bool, rehearse: bool) -> bool:
+    """Do the N > 1 exchange legs run through the shard C ABI over RCCL?  On
+    GPUs, one rank per GPU: yes.  Rehearsals with every rank on one GPU (RCCL
+    refuses two ranks on one device) and the CPU self-test: torch P2P over gloo."""
+    return world > 1 and cuda and not rehearse
+
+
 def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
-                n_elems: int | None = None, fold=None) -> dict:
+                n_elems: int | None = None, fold=None, comm=None) -> dict:
     """BASELINE config 4's exchange (N > 1 only): N workers' fp32 VGG-16
     gradient vectors (553,430,176 B each) land on GPU 0; RCCL grouped P2P over
     xGMI moves each owner its key-space slice (ShardedReducer.scatter_reduce:
     the only data-path collective), the owner folds; then the
-    all-gather return leg (core_loops.cc:249-254).  Verified bit-exact on GPU 0
-    against torch's own left fold of the whole vector."""
+    all-gather return leg (core_loops.cc:249-254).  With ``comm`` (GPU runs:
+    a :class:`ShardComm` over RCCL) every call is ONE byteps_shard_* call —
+    the code a core_loops.cc caller binds in place of PostNcclCalls; without
+    it (gloo rehearsals, CPU tests) torch.distributed P2P moves the slices.
+    Verified bit-exact on GPU 0 against torch's own left fold of the whole
+    vector."""
     import torch
     import torch.distributed as dist
     from prophet_amd.buckets import vgg16_param_sizes
@@ -501,7 +525,8 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
     if os.environ.get("BPSR_BENCH_TEST_STALL") == "scatter":
         time.sleep(3600)                # test hook: a collective that never returns
     E = n_elems or sum(vgg16_param_sizes())
-    sr = ShardedReducer(E, fold=fold)   # fold=None: the HIP fold (tests inject a CPU one)
+    # fold=None: the HIP fold (tests inject a CPU one); comm: the shard C ABI
+    sr = ShardedReducer(E, fold=fold, comm=comm)
     root = 0
     cuda = dev.type == "cuda"
 
@@ -538,6 +563,7 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
     egress = n_workers * (E - (hi - lo)) * 4
     return {"workload": f"{n_workers} x VGG-16-sized fp32 ({E * 4} B) landed on GPU 0, "
                         f"RCCL P2P scatter to {world} owners + owner fold, then all-gather",
+            "transport": _transport(comm),
             "scatter_fold_ms": round(t_scatter * 1e3, 3),
             "root_egress_GBps": round(egress / t_scatter / 1e9, 1),
             "allgather_ms": round(t_gather * 1e3, 3),
@@ -546,7 +572,7 @@ def scatter_leg(dev, world: int, rank: int, n_workers: int, reps: int = 5,
 
 
 def local_reduce_leg(dev, world: int, rank: int, reps: int = 5, n_elems: int | None = None,
-                     fold=None) -> dict:
+                     fold=None, comm=None) -> dict:
     """The worker's local reduce (core_loops.cc:184-263),
     N > 1 only: every GPU holds its own full fp32 VGG-16 gradient vector and
     all of them are summed across the node.  ``ShardedReducer.allreduce`` =
@@ -556,13 +582,14 @@ def local_reduce_leg(dev, world: int, rank: int, reps: int = 5, n_elems: int | N
     RCCL's own ``all_reduce`` on the same bytes is timed beside it for
     reference (its summation order follows the ring).  Exactness: strided
     windows of the result against torch's left fold, in rank order, of every
-    rank's vector regenerated from its seed."""
+    rank's vector regenerated from its seed.  ``comm`` as in scatter_leg:
+    byteps_shard_reduce_scatter + byteps_shard_allgather over RCCL."""
     import torch
     import torch.distributed as dist
     from prophet_amd.buckets import vgg16_param_sizes
     from prophet_amd.shard import ShardedReducer
     E = n_elems or sum(vgg16_param_sizes())
-    sr = ShardedReducer(E, fold=fold)   # fold=None: the HIP fold (tests inject a CPU one)
+    sr = ShardedReducer(E, fold=fold, comm=comm)
     cuda = dev.type == "cuda"
 
     def vec(r):
@@ -607,6 +634,7 @@ def local_reduce_leg(dev, world: int, rank: int, reps: int = 5, n_elems: int | N
     return {"workload": (f"worker local reduce: {world} GPUs each holding a {nbytes} B fp32 "
                          f"(VGG-16-sized) gradient; rank-order P2P reduce-scatter + HIP fold + "
                          f"all-gather (ShardedReducer.allreduce) vs RCCL all_reduce"),
+            "transport": _transport(comm),
             "allreduce_ms": round(t_det * 1e3, 3),
             "busbw_GBps": round(2 * (world - 1) / world * nbytes / t_det / 1e9, 1),
             "rccl_allreduce_ms": round(t_ring * 1e3, 3),
@@ -1149,6 +1177,17 @@ def main(argv=None):
                           "no RCCL: the scatter and local-reduce legs move CUDA tensors "
                           f"through gloo, {xchg_elems} elements): NOT a measurement")
 
+    # N > 1 on GPUs: the exchange legs go through the shard C ABI over RCCL
+    # (byteps_shard_*), the path a core_loops.cc caller binds; gloo
+    # rehearsals and the CPU self-test keep torch.distributed P2P
+    comm = None
+    if uses_shard_abi(world, cuda, rehearse) and not args.no_scatter:
+        try:
+            comm, how = shard_comm(dev)
+            line["shard_comm"] = how
+        except Exception as e:  # report, never hide
+            line["shard_comm"] = {"error": repr(e)}
+
     def extra_legs(state=None):
         def leg(name):
             if state is not None:
@@ -1165,7 +1204,7 @@ def main(argv=None):
                 try:
                     line["scaling_cfg4"]["scatter"] = scatter_leg(
                         dev, world, rank, N, n_elems=xchg_elems,
-                        fold=None if cuda else _torch_fold)
+                        fold=None if cuda else _torch_fold, comm=comm)
                 except Exception as e:  # report, never hide
                     line["scaling_cfg4"]["scatter"] = {"error": repr(e)}
         if world > 1 and not args.no_scatter:
@@ -1173,7 +1212,7 @@ def main(argv=None):
             try:
                 line["local_reduce"] = local_reduce_leg(
                     dev, world, rank, n_elems=xchg_elems,
-                    fold=None if cuda else _torch_fold)
+                    fold=None if cuda else _torch_fold, comm=comm)
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}
         if cuda and not args.no_e2e:

@@ -122,10 +122,15 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 /* A worker's pull: blocks until the key's current round is finished (sync mode),
  * then copies the store (len bytes) to `out`.  Into device memory with the
  * default engine in sync mode, the copy is one of the lane issuer's batched
- * pull copies and the call waits for the responder's answer (no HIP call on
- * the caller's thread) — except when called from inside a callback (on the
- * responder thread), which copies directly.  The same holds for blocking
- * pushes of device data (byteps_server_push). */
+ * pull copies: the issuer tells the caller which of its launches carries the
+ * copy, and the caller waits for the lane's completer to see that launch
+ * complete (no HIP call on the caller's thread, no responder hop), then counts
+ * the pull.  Pulls parked before the round finishes are queued together when
+ * it does, so the pulls one round completion answers ride in one launch.  A
+ * call made from inside a callback (on the responder thread) copies directly.
+ * The same holds for blocking pushes of device data (byteps_server_push).
+ * BPSR_SERVER_SPIN_US=n: such a waiter polls the lane's completion for up to
+ * n µs before it sleeps (default 0: it sleeps at once). */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
 /* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
@@ -179,7 +184,8 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
  * launch), and the responder thread calls cb(ctx, key, out, len, 0) when the
  * copy has completed, counting the pull just before (as byteps_server_pull_async).
  * Later folds of the key wait for the copy before rewriting the store.  Sync
- * mode and the default engine only (EARGS otherwise); device memory only.
+ * mode and the default engine only (EARGS otherwise); device memory, or pinned
+ * host memory (written through its device view; EARGS for pageable memory).
  * Pulls still waiting at byteps_server_destroy get BYTEPS_REDUCE_ECANCELED. */
 int byteps_server_pull_into_async(byteps_server* s, uint64_t key, void* out, size_t len,
                                   int location, byteps_server_pull_cb cb, void* ctx);
@@ -189,6 +195,15 @@ int byteps_server_pull_into_async(byteps_server* s, uint64_t key, void* out, siz
  * (waits until every round the key completed has been issued). */
 int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int* lane,
                            int* last_order, int max_order);
+
+/* Order the server's device work after the caller's: every copy into a slot,
+ * copy out of a store and fold that the lanes of keys[0..n) (n = 0: every
+ * lane) issue from now on runs after `event` (a hipEvent_t the caller recorded
+ * on the stream that produced a push's data or last touched a pull's
+ * destination) — hipStreamWaitEvent on the lanes' streams, no host wait.  The
+ * event may be re-recorded or destroyed once the call returns.  Call it before
+ * the push / pull calls it orders. */
+int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, void* event);
 
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
@@ -238,13 +253,23 @@ int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* lo
  *       tail to the last instance — so each GPU owns a contiguous slice of
  *       every large partition; smaller keys go whole by hash.  Piece starts
  *       are multiples of 128 B (of 8 elements for every dtype), so the fp16
- *       body/tail rule of cpu_reducer.cc:103,118 holds piece by piece.  Each
- *       piece is a strict left fold in the arrival order ITS instance saw; when
- *       workers race, a key's pieces may fold in different orders (the
- *       reference has one order per key, since one server holds it).
- * Pushes scatter the pieces (each instance copies its piece into its own
- * HBM); pulls gather them back into the caller's buffer.  All calls are
- * thread-safe like the single-instance ones and block like them. */
+ *       body/tail rule of cpu_reducer.cc:103,118 holds piece by piece.  A
+ *       split key keeps ONE arrival order, as in the reference where one
+ *       server holds it (server.cc:216-250): the group stamps every push with
+ *       the next position of its worker's round and every instance folds its
+ *       piece in those positions (fused policy; the init round's store comes
+ *       from the push stamped last).  With the incremental policy or engine
+ *       blocking, each piece follows its own instance's arrival order.
+ * The group records each key's length and dtype (init_key, or its first push):
+ * a push of another length is refused, and a pull of fewer bytes is cut from
+ * the same pieces.  Pushes scatter the pieces (each instance copies its piece
+ * into its own HBM), every piece validated before any is queued; one that
+ * still fails fails the key on every instance.  Pulls gather the pieces back,
+ * all instances at once (pull_into_async) into device or pinned host memory
+ * with the default engine, else piece by piece.  Batched calls queue every
+ * piece of every key at once.  The group enables peer access between its
+ * devices.  All calls are thread-safe like the single-instance ones and block
+ * like them. */
 enum byteps_server_split { BYTEPS_SERVER_SPLIT_HASH = 0, BYTEPS_SERVER_SPLIT_RANGE = 1 };
 /* BYTEPS_KEY_HASH_FN values (global.cc:541-554). */
 enum byteps_key_hash { BYTEPS_KEY_HASH_DJB2 = 0, BYTEPS_KEY_HASH_NAIVE = 1,
@@ -298,6 +323,12 @@ int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
                                   int dtype, int location);
 int byteps_server_group_pull_many(byteps_server_group* g, const uint64_t* keys,
                                   void* const* outs, const size_t* lens, int n, int location);
+
+/* byteps_server_order_after for the instances that hold keys[0..n) (their
+ * declared lengths decide the pieces; n = 0 or an undeclared key: every
+ * instance). */
+int byteps_server_group_order_after(byteps_server_group* g, const uint64_t* keys, int n,
+                                    void* event);
 
 #ifdef __cplusplus
 }

@@ -4,8 +4,8 @@
   (oracle/bpsr_oracle.c), available everywhere (it is built on the GPU box too).
 * :class:`RefReducer` — the reference's own ``CpuReducer`` compiled from
   /root/reference by oracle/Makefile into ``oracle/_ref/libbpsr_ref.so``
-  (present when that build ran in the development container; the .so travels to
-  the GPU box with the snapshot).
+  (present when that build ran in the build container; .gpurunignore keeps it
+  off the GPU box, where nothing loads it).
 
 Both expose ``sum(dst, src, len, dtype)``, ``sum3``, ``copy`` and the server
 fold ``sum_n`` on numpy arrays (host memory), mirroring

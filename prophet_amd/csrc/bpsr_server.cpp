@@ -218,6 +218,8 @@ struct KeyState {
   std::vector<int> order;     // arrival order this round
   int arrived = 0;
   int init_count = 0;
+  int init_last = -1;         // the init round's last arrival (its push initialises the store)
+  bool stamped = false;       // this round's arrivals carry positions (a group's range split)
   std::vector<Response> init_acks;  // non-blocking init pushes, answered together (server.cc:184-198)
   int pending = 0;            // jobs queued on the lane, not yet issued (scheduling only)
   int error = 0;              // sticky failure of an issued fold: every later call returns it
@@ -253,10 +255,12 @@ struct KeyState {
   std::vector<Waiting> waiting;
   // byteps_server_pull_into_async requests waiting for this round
   struct WaitingCopy {
-    void* dst;
+    void* dst;           // as the device addresses it
     size_t len;
     byteps_server_pull_cb cb;
     void* ctx;
+    const void* view;    // what the callback reports (the caller's pointer)
+    SyncWait* direct;    // a blocking pull parked until the round finishes
   };
   std::vector<WaitingCopy> waiting_copies;
 };
@@ -549,7 +553,10 @@ void fail_key(byteps_server* s, KeyState* ks, int rc) {
   }
   for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, nullptr, rc);
   ks->waiting.clear();
-  for (auto& wc : ks->waiting_copies) respond_later(s, ks, wc.cb, wc.ctx, nullptr, rc);
+  for (auto& wc : ks->waiting_copies) {
+    if (wc.direct) wc.direct->finish(rc);
+    else respond_later(s, ks, wc.cb, wc.ctx, nullptr, rc);
+  }
   ks->waiting_copies.clear();
   for (auto& a : ks->init_acks) {
     a.status = rc;
@@ -559,23 +566,29 @@ void fail_key(byteps_server* s, KeyState* ks, int rc) {
   ks->cv.notify_all();
 }
 
-// Queue a pull into a caller's device buffer for the lane's issuer (caller
-// holds ks->mu; the key's round is published, so its fold is issued).
-void queue_pull_copy(byteps_server* s, KeyState* ks, void* dst, size_t len,
-                     byteps_server_pull_cb cb, void* ctx) {
-  PullJob j;
-  j.ks = ks;
-  j.dst = dst;
-  j.len = len;
-  j.resp.key = ks->key;
-  j.resp.ks = ks;
-  j.resp.cb = cb;
-  j.resp.ctx = ctx;
-  j.resp.view = static_cast<const char*>(dst);
-  j.resp.len = len;
+// Queue pulls into callers' buffers for the lane's issuer (caller holds
+// ks->mu; the key's round is published, so its fold is issued): all of them
+// under one lock, so the pulls one round completion answers ride in one
+// launch.  `direct` ones are blocking pulls, whose waiters hear from the issuer.
+void queue_pull_copies(byteps_server* s, KeyState* ks, const KeyState::WaitingCopy* wcs, size_t n) {
+  if (n == 0) return;
   Lane& L = *s->lanes[ks->lane];
   std::lock_guard<std::mutex> g(L.comb_mu);
-  L.pulls.push_back(j);
+  for (size_t i = 0; i < n; ++i) {
+    const KeyState::WaitingCopy& wc = wcs[i];
+    PullJob j;
+    j.ks = ks;
+    j.dst = wc.dst;
+    j.len = wc.len;
+    j.direct = wc.direct;
+    j.resp.key = ks->key;
+    j.resp.ks = ks;
+    j.resp.cb = wc.cb;
+    j.resp.ctx = wc.ctx;
+    j.resp.view = static_cast<const char*>(wc.view);
+    j.resp.len = wc.len;
+    L.pulls.push_back(j);
+  }
   L.comb_cv.notify_one();
 }
 
@@ -659,7 +672,7 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
   const char* view = ks->mirror.empty() ? nullptr : ks->mirror[ks->rounds & 1];
   for (auto& wp : ks->waiting) respond_later(s, ks, wp.cb, wp.ctx, view, 0);
   ks->waiting.clear();
-  for (auto& wc : ks->waiting_copies) queue_pull_copy(s, ks, wc.dst, wc.len, wc.cb, wc.ctx);
+  queue_pull_copies(s, ks, ks->waiting_copies.data(), ks->waiting_copies.size());
   ks->waiting_copies.clear();
   ks->cv.notify_all();
   return 0;
@@ -771,16 +784,40 @@ void dispatcher_main(byteps_server* s, int lane) {
 // With `defer` (a batched call, no scheduling), a round's fused fold is not
 // issued here but handed back, to go out with the call's other keys in one
 // batched launch per lane (flush_folds); the key counts it as pending.
-int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = nullptr) {
+// May an arrival of the current (non-init) round take position `pos`?
+int check_pos(const byteps_server* s, const KeyState* ks, int pos) {
+  const int N = s->cfg.num_workers;
+  if (pos >= N) return fail(BYTEPS_REDUCE_EARGS, "arrival position %d outside [0, %d)", pos, N);
+  const bool stamp = pos >= 0 && s->cfg.policy == BYTEPS_SERVER_FUSED;
+  if (!ks->inited || s->cfg.async_mode) return 0;
+  if (ks->arrived > 0 && stamp != ks->stamped)
+    return fail(BYTEPS_REDUCE_EARGS, "key %llu: stamped and unstamped arrivals in one round",
+                (unsigned long long)ks->key);
+  if (stamp && ks->arrived > 0 && ks->order[pos] >= 0)
+    return fail(BYTEPS_REDUCE_EARGS, "key %llu: arrival position %d taken twice",
+                (unsigned long long)ks->key, pos);
+  return 0;
+}
+
+// `pos` >= 0 (a server group's range split, fused policy): the arrival takes
+// that position of the round's order, which the group stamped for the whole
+// key, instead of its position here — every piece of the key then folds in the
+// same order (server.cc:216-250 has one order per key).
+int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = nullptr,
+           int pos = -1) {
   if (ks->error) return key_error(ks);
   const int N = s->cfg.num_workers;
   Lane& L = *s->lanes[ks->lane];
+  if (int rc = check_pos(s, ks, pos)) return rc;
   if (!ks->inited) {
     // Round 0: server.cc:175-199 — after all NumWorkers init pushes the store
-    // is initialised by copying the LAST arrived push, in the handler itself.
+    // is initialised by copying the LAST arrived push, in the handler itself
+    // (stamped: the push at the last position).
     if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d sent two init pushes", w);
     ks->got[w] = 1;
+    if (pos < 0 || pos == N - 1) ks->init_last = w;
     if (++ks->init_count < N) return 0;
+    w = ks->init_last;
     // every init push is counted: a failure from here on fails the key (the
     // other workers' init pushes wait for `inited || error`)
     int rc = injected_failure(s);
@@ -819,8 +856,15 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     return rc;
   }
   if (ks->got[w]) return fail(BYTEPS_REDUCE_EARGS, "worker %d pushed twice in one round", w);
+  const bool stamp = pos >= 0 && s->cfg.policy == BYTEPS_SERVER_FUSED;
+  if (stamp) {
+    if (ks->arrived == 0) ks->order.assign(N, -1);
+    ks->order[pos] = w;
+  } else {
+    ks->order.push_back(w);
+  }
+  ks->stamped = stamp;
   ks->got[w] = 1;
-  ks->order.push_back(w);
   ks->arrived++;
   if (ks->arrived > 1 && s->cfg.policy == BYTEPS_SERVER_INCREMENTAL) {
     FoldJob j;  // SUM_RECV (server.cc:245-251)
@@ -841,7 +885,11 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
   j.order = ks->order;
   ks->order.clear();
   ks->arrived = 0;
-  if (defer && !q && j.kind == kFinishFused && N <= kMaxSrcs) {
+  // Combining: EVERY finished round goes to the lane's issuer (a fold that
+  // writes the store must queue behind the lane's queued copies into the
+  // slots and pull copies out of the store, which only the issuer orders);
+  // otherwise the batchable fused rounds of a batched call.
+  if (defer && !q && (s->combine || (j.kind == kFinishFused && N <= kMaxSrcs))) {
     ks->pending++;
     defer->push_back(std::move(j));
     return 0;
@@ -854,12 +902,28 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
 // Issue deferred fused folds: per (lane, dtype) ONE batched launch whose
 // buckets are the keys' rounds (dst = store, sources = slots in arrival order),
 // then each key's round is published.  Returns the first error.
+int issue_one(byteps_server* s, FoldJob& j);
 int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
   if (jobs.empty()) return 0;
+  int first_rc = 0;
+  // rounds a batched launch cannot carry (incremental COPY_MERGED, more than
+  // kMaxSrcs sources) go out one by one, in their arrival order
+  {
+    std::vector<FoldJob> keep;
+    keep.reserve(jobs.size());
+    for (auto& j : jobs) {
+      if (j.kind == kFinishFused && (int)j.order.size() <= kMaxSrcs) {
+        keep.push_back(std::move(j));
+      } else {
+        const int rc = issue_one(s, j);
+        if (rc && !first_rc) first_rc = rc;
+      }
+    }
+    jobs.swap(keep);
+  }
   std::stable_sort(jobs.begin(), jobs.end(), [](const FoldJob& a, const FoldJob& b) {
     return a.ks->lane != b.ks->lane ? a.ks->lane < b.ks->lane : a.ks->dtype < b.ks->dtype;
   });
-  int first_rc = 0;
   size_t i = 0;
   while (i < jobs.size()) {
     size_t e = i + 1;
@@ -949,6 +1013,16 @@ int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs) {
   }
   jobs.clear();
   return 0;
+}
+
+// The rounds a batched call (push_many / push_ready_many) completed.  When
+// combining they go to the lane issuers like any other call's: another
+// worker's non-blocking push may still have its copy into a slot of the same
+// key queued there, or a pull its copy out of the store, and only the issuer
+// issues those before the fold (issuer_main).  Otherwise this thread issues
+// them as one batched launch per lane.
+int issue_deferred(byteps_server* s, std::vector<FoldJob>& jobs) {
+  return s->combine ? issue_combined(s, jobs) : flush_folds(s, jobs);
 }
 
 // Issue the non-blocking device pushes that piled up on a lane: ONE wait for
@@ -1088,11 +1162,19 @@ void issuer_main(byteps_server* s, int lane) {
       (void)issue_one(s, folds[0]);
     else if (!folds.empty())
       (void)flush_folds(s, folds);  // a failed fold fails its keys (fail_key)
+    folds.clear();
+    lk.lock();
+    if (!L.pulls.empty()) {
+      // the pulls parked on the rounds just published go out now, in one
+      // launch behind the folds, rather than after another wake-up
+      pulls.swap(L.pulls);
+      lk.unlock();
+      issue_pull_copies(s, L, pulls);
+      lk.lock();
+    }
     s->issuer_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - t0).count(),
                            std::memory_order_relaxed);
-    folds.clear();
-    lk.lock();
   }
 }
 
@@ -1279,8 +1361,10 @@ int byteps_server_destroy(byteps_server* s) {
       for (auto& wp : ks->waiting)
         respond_later(s, ks, wp.cb, wp.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
       ks->waiting.clear();
-      for (auto& wc : ks->waiting_copies)
-        respond_later(s, ks, wc.cb, wc.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
+      for (auto& wc : ks->waiting_copies) {
+        if (wc.direct) wc.direct->finish(BYTEPS_REDUCE_ECANCELED);
+        else respond_later(s, ks, wc.cb, wc.ctx, nullptr, BYTEPS_REDUCE_ECANCELED);
+      }
       ks->waiting_copies.clear();
       for (auto& a : ks->init_acks) {  // init pushes whose round never completed
         a.status = BYTEPS_REDUCE_ECANCELED;
@@ -1338,7 +1422,7 @@ namespace bpsr {
 namespace {
 int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
                     int dtype, int location, byteps_server_push_cb cb, void* ctx,
-                    SyncWait* direct);
+                    SyncWait* direct, int pos = -1);
 // A blocking call's wait for the lane's launch `seq` to complete.
 void wait_lane_done(Lane& L, uint64_t seq) {
   if (spin_until([&] { return L.done_pub.load(std::memory_order_acquire) >= seq; })) return;
@@ -1417,7 +1501,7 @@ namespace {
 // other paths, answered through the responder as for any non-blocking push).
 int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
                     int dtype, int location, byteps_server_push_cb cb, void* ctx,
-                    SyncWait* direct) {
+                    SyncWait* direct, int pos) {
   if (!s || !data || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   if (worker < 0 || worker >= s->cfg.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
@@ -1428,6 +1512,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
   if ((rc = allocate(s, ks, len, dtype))) return rc;
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
+  if ((rc = check_pos(s, ks, pos))) return rc;  // before any copy is queued
   if (s->combine && location == BYTEPS_SERVER_DEVICE && ks->inited && !s->cfg.async_mode &&
       s->cfg.policy == BYTEPS_SERVER_FUSED && s->cfg.num_workers <= kMaxSrcs) {
     // the copy goes to the lane's issuer, batched with the other pushes that
@@ -1453,7 +1538,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
     std::vector<FoldJob> defer;
     // cannot fail here: no error (checked under this lock), the slot is free
     // (can_push), and the fused policy defers the round's fold
-    if ((rc = arrive(s, ks, worker, &defer))) return rc;
+    if ((rc = arrive(s, ks, worker, &defer, pos))) return rc;
     if (!defer.empty()) {
       lk.unlock();
       issue_combined(s, defer);
@@ -1463,7 +1548,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
   if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
   const bool init_push = !ks->inited;
   std::vector<FoldJob> defer;
-  if ((rc = arrive(s, ks, worker, s->combine ? &defer : nullptr))) {  // arrival order = call order
+  if ((rc = arrive(s, ks, worker, s->combine ? &defer : nullptr, pos))) {  // arrival order = call order
     // the caller gets its buffer back on error: let the queued copy finish first
     (void)hipEventSynchronize(ks->copied);
     return rc;
@@ -1543,20 +1628,13 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
     if (!ks) return BYTEPS_REDUCE_EARGS;
     std::unique_lock<std::mutex> lk(ks->mu);
     if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
-    ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
     if (ks->error) return key_error(ks);
     SyncWait w;
-    PullJob j;
-    j.ks = ks;
-    j.dst = out;
-    j.len = len;
-    j.direct = &w;
-    {
-      Lane& L = *s->lanes[ks->lane];
-      std::lock_guard<std::mutex> g(L.comb_mu);
-      L.pulls.push_back(j);
-      L.comb_cv.notify_one();
-    }
+    const KeyState::WaitingCopy wc{out, len, nullptr, nullptr, out, &w};
+    if (pull_ready(s, ks))
+      queue_pull_copies(s, ks, &wc, 1);
+    else  // parked: queued with the round's other parked pulls when it finishes
+      ks->waiting_copies.push_back(wc);
     lk.unlock();
     if ((rc = w.wait())) return sync_status(s, key, rc, "pull");
     wait_lane_done(*w.lane, w.seq);
@@ -1706,23 +1784,27 @@ int byteps_server_pull_async(byteps_server* s, uint64_t key, byteps_server_pull_
 int byteps_server_pull_into_async(byteps_server* s, uint64_t key, void* out, size_t len,
                                   int location, byteps_server_pull_cb cb, void* ctx) {
   if (!s || !out || !cb) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  if (location != BYTEPS_SERVER_DEVICE)
-    return fail(BYTEPS_REDUCE_EARGS, "pull_into_async copies into device memory only "
-                                     "(host transports: byteps_server_pull_async views)");
   if (s->cfg.async_mode || !s->combine)
     return fail(BYTEPS_REDUCE_EARGS, "pull_into_async needs sync mode and the default engine "
                                      "(no scheduling, no engine blocking, BPSR_SERVER_COMBINE!=0)");
   int rc = set_device(s);
   if (rc) return rc;
+  // pinned host memory: the issuer's copy kernel writes it through its device
+  // view (over PCIe); pageable memory is not addressable by the device
+  void* dv = device_view(out, location);
+  if (!dv)
+    return fail(BYTEPS_REDUCE_EARGS, "pull_into_async: host destination is not pinned "
+                                     "(host transports: byteps_server_pull_async views)");
   KeyState* ks = key_for_pull(s, key);
   if (!ks) return BYTEPS_REDUCE_EARGS;
   std::lock_guard<std::mutex> g(ks->mu);
   if (ks->error) return key_error(ks);
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
+  const KeyState::WaitingCopy wc{dv, len, cb, ctx, out, nullptr};
   if (ks->push_finished)  // server.cc:293-301: the round is finished
-    queue_pull_copy(s, ks, out, len, cb, ctx);
+    queue_pull_copies(s, ks, &wc, 1);
   else                    // server.cc:303-304: answered once it finishes
-    ks->waiting_copies.push_back({out, len, cb, ctx});
+    ks->waiting_copies.push_back(wc);
   return BYTEPS_REDUCE_OK;
 }
 
@@ -1753,37 +1835,37 @@ int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n,
   for (int i = 0; i < n; ++i) {
     KeyState* ks = get_key(s, keys[i], false);
     if (!ks || !ks->allocated) {
-      (void)flush_folds(s, defer);
+      (void)issue_deferred(s, defer);
       return fail(BYTEPS_REDUCE_EARGS, "key %llu not initialised", (unsigned long long)keys[i]);
     }
     std::unique_lock<std::mutex> lk(ks->mu);
     if (!can_push(s, ks, worker)) {
       // never block while holding deferred rounds: others may wait on them
       lk.unlock();
-      if ((rc = flush_folds(s, defer))) return rc;
+      if ((rc = issue_deferred(s, defer))) return rc;
       lk.lock();
       ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
     }
     if (ks->error) {
       lk.unlock();
-      (void)flush_folds(s, defer);
+      (void)issue_deferred(s, defer);
       return key_error(ks);
     }
     const bool init_round = !ks->inited;
     if ((rc = arrive(s, ks, worker, &defer))) {
       lk.unlock();
-      (void)flush_folds(s, defer);
+      (void)issue_deferred(s, defer);
       return rc;
     }
     if (init_round && !ks->inited) {
       lk.unlock();
-      if ((rc = flush_folds(s, defer))) return rc;
+      if ((rc = issue_deferred(s, defer))) return rc;
       lk.lock();
       ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
       if (ks->error) return key_error(ks);
     }
   }
-  return flush_folds(s, defer);
+  return issue_deferred(s, defer);
 }
 
 int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* const* datas,
@@ -1848,18 +1930,18 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     const bool init_round = !ks->inited;
     if ((rc = arrive(s, ks, worker, &defer))) {
       lk.unlock();
-      (void)flush_folds(s, defer);
+      (void)issue_deferred(s, defer);
       return rc;
     }
     if (init_round && !ks->inited) {
       lk.unlock();
-      if ((rc = flush_folds(s, defer))) return rc;
+      if ((rc = issue_deferred(s, defer))) return rc;
       lk.lock();
       ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
       if (ks->error) return key_error(ks);
     }
   }
-  if ((rc = flush_folds(s, defer))) return rc;
+  if ((rc = issue_deferred(s, defer))) return rc;
   if (s->blocking)  // engine blocking mode: the folds issued above have completed
     for (size_t l = 0; l < by_lane.size(); ++l)
       if (!by_lane[l].empty()) {
@@ -1978,6 +2060,35 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
   return BYTEPS_REDUCE_OK;
 }
 
+int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, void* event) {
+  if (!s || !event || n < 0 || (n > 0 && !keys)) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  // the lanes of the named keys (every lane when a key is not allocated yet:
+  // its lane is picked at its first push)
+  std::vector<char> on(s->lanes.size(), n == 0 ? 1 : 0);
+  for (int i = 0; i < n; ++i) {
+    KeyState* ks = get_key(s, keys[i], false);
+    if (!ks || !ks->allocated) {
+      std::fill(on.begin(), on.end(), 1);
+      break;
+    }
+    on[ks->lane] = 1;
+  }
+  const hipEvent_t ev = static_cast<hipEvent_t>(event);
+  for (size_t l = 0; l < on.size(); ++l) {
+    if (!on[l]) continue;
+    Lane& L = *s->lanes[l];
+    // push copies (and the issuer's), pull copies and mirrors, and the folds
+    // of push_ready rounds whose slots the caller wrote on its own stream
+    for (hipStream_t st : {L.copy, L.d2h, L.fold}) {
+      const hipError_t e = hipStreamWaitEvent(st, ev, 0);
+      if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(caller event)");
+    }
+  }
+  return BYTEPS_REDUCE_OK;
+}
+
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
   if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   const uint64_t v[6] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
@@ -2005,3 +2116,38 @@ int byteps_server_debug_lane(byteps_server* s, int lane, int pause, uint64_t* lo
 }
 
 }  // extern "C"
+
+// ------------------------------------------- server group internals --
+// (bpsr_server_internal.h: not part of the C ABI)
+
+namespace bpsr {
+
+int server_push_async_at(byteps_server* s, uint64_t key, int worker, const void* data,
+                         size_t len, int dtype, int location, byteps_server_push_cb cb, void* ctx,
+                         int pos) {
+  return push_async_impl(s, key, worker, data, len, dtype, location, cb, ctx, nullptr, pos);
+}
+
+int server_check_key(byteps_server* s, uint64_t key, size_t len, int dtype) {
+  if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
+  if (elem_size(dtype) == 0) return fail(BYTEPS_REDUCE_EDTYPE, "Unsupported data type: %d", dtype);
+  if (len == 0) return fail(BYTEPS_REDUCE_EARGS, "init tensor size not larger than 0");
+  KeyState* ks = get_key(s, key, false);
+  if (!ks) return 0;
+  std::lock_guard<std::mutex> g(ks->mu);
+  if (ks->error) return key_error(ks);
+  if (ks->allocated && (len != ks->len || dtype != ks->dtype))
+    return fail(BYTEPS_REDUCE_EARGS, "key %llu pushed with len %zu dtype %d (declared %zu, %d)",
+                (unsigned long long)key, len, dtype, ks->len, ks->dtype);
+  return 0;
+}
+
+void server_fail_key(byteps_server* s, uint64_t key, int rc) {
+  KeyState* ks = get_key(s, key, true);
+  std::lock_guard<std::mutex> g(ks->mu);
+  fail_key(s, ks, rc);
+}
+
+bool server_pulls_async(const byteps_server* s) { return s->combine && !s->cfg.async_mode; }
+
+}  // namespace bpsr

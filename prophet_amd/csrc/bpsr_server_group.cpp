@@ -6,16 +6,24 @@
 // data moves and folds inside the instances.
 #include "bpsr/server.h"
 
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "bpsr_error.h"
+#include "bpsr_internal.h"
+#include "bpsr_server_internal.h"
 
 namespace bpsr {
 namespace {
@@ -27,12 +35,29 @@ struct Piece {
   size_t off, len;
 };
 
+// What the group knows of a key: its declared length and dtype (the split is
+// computed from them, so a shorter pull is cut from the same pieces), and the
+// arrival stamps of its rounds.  A range-split key has ONE arrival order for
+// all its pieces (server.cc:216-250: one left fold per key in arrival order):
+// the group gives each push the next position of its worker's round, and every
+// instance folds its piece in those positions (bpsr::server_push_async_at).
+struct GroupKey {
+  std::mutex mu;
+  size_t len = 0;  // 0: not declared yet
+  int dtype = -1;
+  std::vector<uint64_t> pushes;   // per worker: pushes stamped so far (= its round)
+  std::map<uint64_t, int> taken;  // round -> positions handed out (erased when full)
+};
+
 }  // namespace
 }  // namespace bpsr
 
 struct byteps_server_group {
   byteps_server_group_config cfg;
   std::vector<byteps_server*> inst;
+  bool pulls_async = false;  // every instance answers pull_into_async (parallel gathers)
+  std::shared_mutex mu;
+  std::unordered_map<uint64_t, std::unique_ptr<bpsr::GroupKey>> keys;
 };
 
 namespace bpsr {
@@ -104,6 +129,168 @@ int check_group(const byteps_server_group* g) {
   return g ? 0 : fail(BYTEPS_REDUCE_EARGS, "null server group");
 }
 
+void pull_ack_cb(void* ctx, uint64_t, const void*, size_t, int status) {
+  ack_cb(ctx, 0, 0, status);
+}
+
+// Wait for every acknowledgement counted so far.
+int wait_acks(Acks& a, int rc) {
+  std::unique_lock<std::mutex> lk(a.mu);
+  a.cv.wait(lk, [&] { return a.remaining == 0; });
+  return rc ? rc : a.status;
+}
+
+bpsr::GroupKey* group_key(byteps_server_group* g, uint64_t key, bool create) {
+  {
+    std::shared_lock<std::shared_mutex> lk(g->mu);
+    auto it = g->keys.find(key);
+    if (it != g->keys.end()) return it->second.get();
+    if (!create) return nullptr;
+  }
+  std::unique_lock<std::shared_mutex> lk(g->mu);
+  auto& slot = g->keys[key];
+  if (!slot) slot = std::make_unique<bpsr::GroupKey>();
+  return slot.get();
+}
+
+// Declare (first sight) or check a key's length and dtype.
+int declare(byteps_server_group* g, uint64_t key, size_t len, int dtype) {
+  bpsr::GroupKey* gk = group_key(g, key, true);
+  std::lock_guard<std::mutex> lk(gk->mu);
+  if (gk->len == 0) {
+    if (len == 0) return fail(BYTEPS_REDUCE_EARGS, "init tensor size not larger than 0");
+    gk->len = len;
+    gk->dtype = dtype;
+    gk->pushes.assign((size_t)g->cfg.server.num_workers, 0);
+    return 0;
+  }
+  if (len != gk->len || dtype != gk->dtype)
+    return fail(BYTEPS_REDUCE_EARGS, "key %llu pushed with len %zu dtype %d (declared %zu, %d)",
+                (unsigned long long)key, len, dtype, gk->len, gk->dtype);
+  return 0;
+}
+
+// The key's declared length (0: never declared to the group).
+size_t declared_len(byteps_server_group* g, uint64_t key) {
+  bpsr::GroupKey* gk = group_key(g, key, false);
+  if (!gk) return 0;
+  std::lock_guard<std::mutex> lk(gk->mu);
+  return gk->len;
+}
+
+// The position of worker w's next push of the key in its round's order.
+int stamp(byteps_server_group* g, uint64_t key, int w) {
+  if (g->cfg.server.async_mode) return -1;  // no rounds
+  bpsr::GroupKey* gk = group_key(g, key, true);
+  std::lock_guard<std::mutex> lk(gk->mu);
+  const int N = g->cfg.server.num_workers;
+  if (gk->pushes.size() != (size_t)N) gk->pushes.assign((size_t)N, 0);
+  const uint64_t round = gk->pushes[(size_t)w]++;
+  const int pos = gk->taken[round]++;
+  if (pos + 1 == N) gk->taken.erase(round);
+  return pos;
+}
+
+// The pieces of a pull of `len` bytes: the key's pieces (by its declared
+// length) cut to [0, len).
+int pull_pieces(byteps_server_group* g, uint64_t key, size_t len, std::vector<Piece>* ps) {
+  const size_t klen = declared_len(g, key);
+  if (klen == 0) {  // never declared here: the instance reports it (server.cc:282-283)
+    route(g, key, len, ps);
+    return 0;
+  }
+  if (len > klen)
+    return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, klen);
+  std::vector<Piece> all;
+  route(g, key, klen, &all);
+  ps->clear();
+  for (const Piece& p : all)
+    if (p.off < len) ps->push_back({p.server, p.off, std::min(p.len, len - p.off)});
+  return 0;
+}
+
+// Can instances write `p` with their copy kernels (device memory, or pinned
+// host memory through its device view)?
+bool addressable(const void* p, int location) {
+  if (location == BYTEPS_SERVER_DEVICE) return true;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) == hipSuccess && d) return true;
+  (void)hipGetLastError();
+  return false;
+}
+
+// Scatter pushes: every piece validated on its instance first (nothing is
+// queued if one would be refused), then queued at once on its instance (its
+// own device and lanes), a range-split key's pieces with the group's stamp;
+// then wait for every acknowledgement — the data is in HBM and (init round)
+// every worker's init push has arrived, as a blocking push guarantees.  A
+// piece that fails once others are queued fails the key on every instance, so
+// none waits for a round that cannot complete.
+struct PushPiece {
+  byteps_server* s;
+  uint64_t key;
+  const void* data;
+  size_t len;
+  int pos;
+};
+int scatter_pushes(byteps_server_group* g, const std::vector<PushPiece>& pcs, int worker,
+                   int dtype, int location) {
+  for (const PushPiece& p : pcs)
+    if (int rc = bpsr::server_check_key(p.s, p.key, p.len, dtype)) return rc;
+  Acks acks;
+  int rc = 0;
+  size_t queued = 0;
+  for (const PushPiece& p : pcs) {
+    {
+      std::lock_guard<std::mutex> lk(acks.mu);
+      ++acks.remaining;
+    }
+    rc = bpsr::server_push_async_at(p.s, p.key, worker, p.data, p.len, dtype, location, ack_cb,
+                                    &acks, p.pos);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(acks.mu);
+      --acks.remaining;
+      break;
+    }
+    ++queued;
+  }
+  if (rc) {
+    const std::string msg = byteps_reduce_last_error();
+    for (const PushPiece& p : pcs) bpsr::server_fail_key(p.s, p.key, rc);
+    (void)wait_acks(acks, rc);  // queued pieces still read the caller's data
+    return fail(rc, "%s", msg.c_str());
+  }
+  (void)queued;
+  return wait_acks(acks, 0);
+}
+
+// Gather pulls: every piece's copy queued at once (pull_into_async: the
+// instances' issuers copy their pieces in parallel, each batched with the
+// pulls that piled up on its lane), then wait for all answers.
+struct PullPiece {
+  byteps_server* s;
+  uint64_t key;
+  void* out;
+  size_t len;
+};
+int gather_pulls(const std::vector<PullPiece>& pcs, int location) {
+  Acks acks;
+  int rc = 0;
+  for (const PullPiece& p : pcs) {
+    {
+      std::lock_guard<std::mutex> lk(acks.mu);
+      ++acks.remaining;
+    }
+    rc = byteps_server_pull_into_async(p.s, p.key, p.out, p.len, location, pull_ack_cb, &acks);
+    if (rc) {
+      std::lock_guard<std::mutex> lk(acks.mu);
+      --acks.remaining;
+      break;
+    }
+  }
+  return wait_acks(acks, rc);
+}
+
 }  // namespace
 }  // namespace bpsr
 
@@ -173,6 +360,33 @@ int byteps_server_group_create(const byteps_server_group_config* cfg, byteps_ser
     }
     g->inst.push_back(s);
   }
+  g->pulls_async = true;
+  for (byteps_server* s : g->inst) g->pulls_async = g->pulls_async && bpsr::server_pulls_async(s);
+  // Instances copy with kernels between their own HBM and buffers on the
+  // other GPUs (a worker's device tensors, another instance's pieces): every
+  // pair of the group's devices gets peer access where the link allows it.
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int i = 0; i < cfg->num_servers; ++i)
+      for (int j = 0; j < cfg->num_servers; ++j) {
+        const int a = cfg->devices[i], b = cfg->devices[j];
+        int can = 0;
+        if (a == b || a >= ndev || b >= ndev) continue;
+        if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+        if (hipSetDevice(a) == hipSuccess) {
+          const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipSetDevice(cur);
+            byteps_server_group_destroy(g.release());
+            return hip_fail(e, "hipDeviceEnablePeerAccess");
+          }
+          (void)hipGetLastError();
+        }
+      }
+    (void)hipSetDevice(cur);
+  }
   *out = g.release();
   return BYTEPS_REDUCE_OK;
 }
@@ -220,9 +434,9 @@ int byteps_server_group_init_key(byteps_server_group* g, uint64_t key, size_t le
   if (rc) return rc;
   std::vector<Piece> ps;
   route(g, key, len, &ps);
-  for (const Piece& p : ps)
+  for (const Piece& p : ps)  // the instances refuse a bad dtype / length first
     if ((rc = byteps_server_init_key(g->inst[p.server], key, p.len, dtype))) return rc;
-  return BYTEPS_REDUCE_OK;
+  return declare(g, key, len, dtype);
 }
 
 int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, const void* data,
@@ -230,38 +444,26 @@ int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, c
   int rc = check_group(g);
   if (rc) return rc;
   if (!data) return fail(BYTEPS_REDUCE_EARGS, "null data");
+  if (worker < 0 || worker >= g->cfg.server.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker,
+                g->cfg.server.num_workers);
+  if ((rc = declare(g, key, len, dtype))) return rc;
   std::vector<Piece> ps;
   route(g, key, len, &ps);
   const char* d = static_cast<const char*>(data);
   if (ps.size() == 1 || g->cfg.server.engine_blocking) {
-    // one instance, or the engine's blocking contract piece by piece
+    // one instance, or the engine's blocking contract piece by piece (each
+    // piece in its own instance's arrival order)
     for (const Piece& p : ps)
       if ((rc = byteps_server_push(g->inst[p.server], key, worker, d + p.off, p.len, dtype,
                                    location)))
         return rc;
     return BYTEPS_REDUCE_OK;
   }
-  // Scatter: every piece's copy queued at once on its instance (its own
-  // device and lanes), then wait for all acknowledgements — the data is in
-  // HBM and (init round) every worker's init push has arrived, as a
-  // blocking push guarantees.
-  Acks acks;
-  for (const Piece& p : ps) {
-    {
-      std::lock_guard<std::mutex> lk(acks.mu);
-      ++acks.remaining;
-    }
-    rc = byteps_server_push_async(g->inst[p.server], key, worker, d + p.off, p.len, dtype,
-                                  location, ack_cb, &acks);
-    if (rc) {
-      std::lock_guard<std::mutex> lk(acks.mu);
-      --acks.remaining;
-      break;
-    }
-  }
-  std::unique_lock<std::mutex> lk(acks.mu);
-  acks.cv.wait(lk, [&] { return acks.remaining == 0; });  // queued pieces still read `data`
-  return rc ? rc : acks.status;
+  const int pos = stamp(g, key, worker);
+  std::vector<PushPiece> pcs;
+  for (const Piece& p : ps) pcs.push_back({g->inst[p.server], key, d + p.off, p.len, pos});
+  return scatter_pushes(g, pcs, worker, dtype, location);
 }
 
 int byteps_server_group_pull(byteps_server_group* g, uint64_t key, void* out, size_t len,
@@ -270,8 +472,15 @@ int byteps_server_group_pull(byteps_server_group* g, uint64_t key, void* out, si
   if (rc) return rc;
   if (!out) return fail(BYTEPS_REDUCE_EARGS, "null out");
   std::vector<Piece> ps;
-  route(g, key, len, &ps);
+  if ((rc = pull_pieces(g, key, len, &ps))) return rc;
   char* o = static_cast<char*>(out);
+  if (ps.size() > 1 && g->pulls_async && addressable(out, location)) {
+    std::vector<PullPiece> pcs;
+    for (const Piece& p : ps) pcs.push_back({g->inst[p.server], key, o + p.off, p.len});
+    return gather_pulls(pcs, location);
+  }
+  // one piece; or pageable host memory, or an engine that answers each pull
+  // by its own rules (scheduling, engine blocking, async mode): piece by piece
   for (const Piece& p : ps)
     if ((rc = byteps_server_pull(g->inst[p.server], key, o + p.off, p.len, location))) return rc;
   return BYTEPS_REDUCE_OK;
@@ -283,26 +492,47 @@ int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
   int rc = check_group(g);
   if (rc) return rc;
   if (n < 0 || (n > 0 && (!keys || !datas || !lens))) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  const size_t ns = g->inst.size();
-  std::vector<std::vector<uint64_t>> k(ns);
-  std::vector<std::vector<const void*>> d(ns);
-  std::vector<std::vector<size_t>> l(ns);
+  if (worker < 0 || worker >= g->cfg.server.num_workers)
+    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker,
+                g->cfg.server.num_workers);
   std::vector<Piece> ps;
   for (int i = 0; i < n; ++i) {
     if (!datas[i]) return fail(BYTEPS_REDUCE_EARGS, "null data for key %d", i);
-    route(g, keys[i], lens[i], &ps);
-    for (const Piece& p : ps) {
-      k[p.server].push_back(keys[i]);
-      d[p.server].push_back(static_cast<const char*>(datas[i]) + p.off);
-      l[p.server].push_back(p.len);
-    }
+    if ((rc = declare(g, keys[i], lens[i], dtype))) return rc;
   }
-  for (size_t s = 0; s < ns; ++s)
-    if (!k[s].empty() &&
-        (rc = byteps_server_push_many(g->inst[s], k[s].data(), d[s].data(), l[s].data(),
-                                      (int)k[s].size(), worker, dtype, location)))
-      return rc;
-  return BYTEPS_REDUCE_OK;
+  if (g->cfg.server.engine_blocking) {
+    // the engine's blocking contract: each instance's keys as one batched call
+    const size_t ns = g->inst.size();
+    std::vector<std::vector<uint64_t>> k(ns);
+    std::vector<std::vector<const void*>> d(ns);
+    std::vector<std::vector<size_t>> l(ns);
+    for (int i = 0; i < n; ++i) {
+      route(g, keys[i], lens[i], &ps);
+      for (const Piece& p : ps) {
+        k[p.server].push_back(keys[i]);
+        d[p.server].push_back(static_cast<const char*>(datas[i]) + p.off);
+        l[p.server].push_back(p.len);
+      }
+    }
+    for (size_t s = 0; s < ns; ++s)
+      if (!k[s].empty() &&
+          (rc = byteps_server_push_many(g->inst[s], k[s].data(), d[s].data(), l[s].data(),
+                                        (int)k[s].size(), worker, dtype, location)))
+        return rc;
+    return BYTEPS_REDUCE_OK;
+  }
+  // every piece of every key queued at once on its instance: the instances'
+  // copies and folds run in parallel (one PCIe link / HBM per GPU), each
+  // instance's lane issuers batching what piles up
+  std::vector<PushPiece> pcs;
+  for (int i = 0; i < n; ++i) {
+    route(g, keys[i], lens[i], &ps);
+    const int pos = ps.size() > 1 ? stamp(g, keys[i], worker) : -1;
+    for (const Piece& p : ps)
+      pcs.push_back({g->inst[p.server], keys[i], static_cast<const char*>(datas[i]) + p.off,
+                     p.len, pos});
+  }
+  return scatter_pushes(g, pcs, worker, dtype, location);
 }
 
 int byteps_server_group_pull_many(byteps_server_group* g, const uint64_t* keys, void* const* outs,
@@ -314,21 +544,54 @@ int byteps_server_group_pull_many(byteps_server_group* g, const uint64_t* keys, 
   std::vector<std::vector<uint64_t>> k(ns);
   std::vector<std::vector<void*>> o(ns);
   std::vector<std::vector<size_t>> l(ns);
+  std::vector<PullPiece> pcs;
+  bool gather = g->pulls_async;
   std::vector<Piece> ps;
   for (int i = 0; i < n; ++i) {
     if (!outs[i]) return fail(BYTEPS_REDUCE_EARGS, "null out for key %d", i);
-    route(g, keys[i], lens[i], &ps);
+    if ((rc = pull_pieces(g, keys[i], lens[i], &ps))) return rc;
+    gather = gather && addressable(outs[i], location);
     for (const Piece& p : ps) {
       k[p.server].push_back(keys[i]);
       o[p.server].push_back(static_cast<char*>(outs[i]) + p.off);
       l[p.server].push_back(p.len);
+      pcs.push_back({g->inst[p.server], keys[i], static_cast<char*>(outs[i]) + p.off, p.len});
     }
   }
+  if (gather) return gather_pulls(pcs, location);  // every instance at once
   for (size_t s = 0; s < ns; ++s)
     if (!k[s].empty() &&
         (rc = byteps_server_pull_many(g->inst[s], k[s].data(), o[s].data(), l[s].data(),
                                       (int)k[s].size(), location)))
       return rc;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_server_group_order_after(byteps_server_group* g, const uint64_t* keys, int n,
+                                    void* event) {
+  int rc = check_group(g);
+  if (rc) return rc;
+  if (!event || n < 0 || (n > 0 && !keys)) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  const size_t ns = g->inst.size();
+  std::vector<std::vector<uint64_t>> k(ns);
+  std::vector<char> all(ns, n == 0 ? 1 : 0);
+  std::vector<Piece> ps;
+  for (int i = 0; i < n; ++i) {
+    const size_t klen = declared_len(g, keys[i]);
+    if (klen == 0) {  // not declared yet: wherever it may land
+      std::fill(all.begin(), all.end(), 1);
+      break;
+    }
+    route(g, keys[i], klen, &ps);
+    for (const Piece& p : ps) k[p.server].push_back(keys[i]);
+  }
+  for (size_t s = 0; s < ns; ++s) {
+    if (all[s])
+      rc = byteps_server_order_after(g->inst[s], nullptr, 0, event);
+    else if (!k[s].empty())
+      rc = byteps_server_order_after(g->inst[s], k[s].data(), (int)k[s].size(), event);
+    if (rc) return rc;
+  }
   return BYTEPS_REDUCE_OK;
 }
 

@@ -29,6 +29,7 @@ SERVER_EXPORTS = (
     "byteps_server_group_create", "byteps_server_group_destroy", "byteps_server_group_route",
     "byteps_server_group_instance", "byteps_server_group_init_key", "byteps_server_group_push",
     "byteps_server_group_pull", "byteps_server_group_push_many", "byteps_server_group_pull_many",
+    "byteps_server_order_after", "byteps_server_group_order_after",
 )
 SPLIT_HASH, SPLIT_RANGE = 0, 1
 HASH_FNS = {"djb2": 0, "naive": 1, "sdbm": 2, "built_in": 3}
@@ -73,6 +74,8 @@ def _lib():
         L.byteps_server_group_push_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int, _int,
                                                     _int]
         L.byteps_server_group_pull_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int]
+        L.byteps_server_order_after.argtypes = [_vp, P(_u64), _int, _vp]
+        L.byteps_server_group_order_after.argtypes = [_vp, P(_u64), _int, _vp]
         L.byteps_server_config_from_env.argtypes = [ctypes.POINTER(ServerConfig)]
         L.byteps_server_create.argtypes = [ctypes.POINTER(ServerConfig), ctypes.POINTER(_vp)]
         L.byteps_server_destroy.argtypes = [_vp]
@@ -103,35 +106,49 @@ def _lib():
     return L
 
 
-def _buf(x, sync: bool = True):
+def _buf(x):
     """(pointer, nbytes, location) of a numpy array or torch tensor."""
     if isinstance(x, np.ndarray):
         assert x.flags["C_CONTIGUOUS"]
         return x.ctypes.data, x.nbytes, HOST
     if hasattr(x, "data_ptr"):
         loc = DEVICE if x.device.type == "cuda" else HOST
-        if loc == DEVICE and sync:
-            _sync_producers([x])
         return int(x.data_ptr()), x.numel() * x.element_size(), loc
     raise TypeError(f"unsupported buffer {type(x)!r}")
 
 
-def _sync_producers(xs) -> None:
-    """The server copies on streams of its own: whatever torch queued for
-    these device tensors on the calling thread's current stream (the kernel
-    that produced a push, a fill of a pull's destination) must be done first.
-    One wait per device per call (batched calls: not one per buffer); a
-    stream with nothing pending costs a query.  Work on other torch streams is
-    the caller's to order."""
+def _producer_events(xs) -> list:
+    """The server copies and folds on streams of its own: whatever torch
+    queued for these device tensors on the calling thread's current stream
+    (the kernel that produced a push, a fill of a pull's destination) must run
+    first.  Per device with work pending there, an event recorded on that
+    stream, for byteps_server_order_after (the server's streams wait on the
+    device, the host does not); a stream with nothing pending costs a query.
+    Work on other torch streams is the caller's to order."""
     import torch
-    seen = set()
+    seen, evs = set(), []
     for x in xs:
         if not hasattr(x, "data_ptr") or x.device.type != "cuda" or x.device in seen:
             continue
         seen.add(x.device)
         st = torch.cuda.current_stream(x.device)
         if not st.query():
-            st.synchronize()
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+    return evs
+
+
+def _order_after(fn, handle, keys, xs) -> None:
+    """byteps_server(_group)_order_after(keys, event) for the producer events
+    of xs (nothing when no stream has work pending)."""
+    evs = _producer_events(xs)
+    if not evs:
+        return
+    n = len(keys)
+    arr = (_u64 * max(1, n))(*keys)
+    for ev in evs:
+        _check(fn(handle, arr, n, ev.cuda_event))
 
 
 def key_hash(key: int, fn: str = "djb2", coef: int = 1) -> int:
@@ -196,8 +213,20 @@ class PSServer:
     def init_key(self, key: int, nbytes: int, dtype: int) -> None:
         _check(self.lib.byteps_server_init_key(self.handle, key, nbytes, int(dtype)))
 
+    def _order(self, keys, xs) -> None:
+        _order_after(self.lib.byteps_server_order_after, self.handle, keys, xs)
+
+    def order_after(self, event, keys=()) -> None:
+        """byteps_server_order_after: the server's later device work on the
+        lanes of ``keys`` (all lanes when empty) runs after ``event`` (a
+        torch.cuda.Event or a raw hipEvent_t)."""
+        n = len(keys)
+        ev = getattr(event, "cuda_event", event)
+        _check(self.lib.byteps_server_order_after(self.handle, (_u64 * max(1, n))(*keys), n, ev))
+
     def push(self, key: int, worker: int, data, dtype: int, nbytes: int | None = None) -> None:
         p, n, loc = _buf(data)
+        self._order([key], [data])
         _check(self.lib.byteps_server_push(self.handle, key, worker, p,
                                            n if nbytes is None else nbytes, int(dtype), loc))
 
@@ -208,6 +237,7 @@ class PSServer:
         the responder thread when ``data`` may be reused.  ``data`` is kept
         alive until then."""
         p, n, loc = _buf(data)
+        self._order([key], [data])
 
         def tramp(_ctx, k, w, status):
             try:
@@ -235,6 +265,7 @@ class PSServer:
 
     def pull(self, key: int, out, nbytes: int | None = None) -> None:
         p, n, loc = _buf(out)
+        self._order([key], [out])
         _check(self.lib.byteps_server_pull(self.handle, key, p, n if nbytes is None else nbytes,
                                            loc))
 
@@ -288,8 +319,10 @@ class PSServer:
         the lane's issuer copies the finished round into ``out`` (batched with
         the other pulls that piled up); ``callback(key, status)`` runs on the
         responder thread once the bytes are there.  ``out`` is kept alive until
-        then."""
-        p, n, loc = _buf(out, sync=False)
+        then.  Work torch queued on ``out`` on the current stream (a fill, a
+        kernel still reading it) is ordered before the copy."""
+        p, n, loc = _buf(out)
+        self._order([key], [out])
 
         def tramp(_ctx, k, _data, _n, status):
             try:
@@ -327,22 +360,22 @@ class PSServer:
         _check(self.lib.byteps_server_push_ready_many(self.handle, arr, len(keys), worker))
 
     def push_many(self, keys, worker: int, datas, dtype: int) -> None:
-        _sync_producers(datas)
-        bufs = [_buf(d, sync=False) for d in datas]
+        bufs = [_buf(d) for d in datas]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("push_many: all sources host, or all device")
+        self._order(keys, datas)
         n = len(keys)
         _check(self.lib.byteps_server_push_many(
             self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
             (_sz * n)(*[b for _, b, _ in bufs]), n, worker, int(dtype), locs.pop() if n else 0))
 
     def pull_many(self, keys, outs) -> None:
-        _sync_producers(outs)
-        bufs = [_buf(o, sync=False) for o in outs]
+        bufs = [_buf(o) for o in outs]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("pull_many: all destinations host, or all device")
+        self._order(keys, outs)
         n = len(keys)
         _check(self.lib.byteps_server_pull_many(
             self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
@@ -409,33 +442,38 @@ class PSServerGroup:
     def init_key(self, key: int, nbytes: int, dtype: int) -> None:
         _check(self.lib.byteps_server_group_init_key(self.handle, key, nbytes, int(dtype)))
 
+    def _order(self, keys, xs) -> None:
+        _order_after(self.lib.byteps_server_group_order_after, self.handle, keys, xs)
+
     def push(self, key: int, worker: int, data, dtype: int, nbytes: int | None = None) -> None:
         p, n, loc = _buf(data)
+        self._order([key], [data])
         _check(self.lib.byteps_server_group_push(self.handle, key, worker, p,
                                                  n if nbytes is None else nbytes, int(dtype), loc))
 
     def pull(self, key: int, out, nbytes: int | None = None) -> None:
         p, n, loc = _buf(out)
+        self._order([key], [out])
         _check(self.lib.byteps_server_group_pull(self.handle, key, p,
                                                  n if nbytes is None else nbytes, loc))
 
     def push_many(self, keys, worker: int, datas, dtype: int) -> None:
-        _sync_producers(datas)
-        bufs = [_buf(d, sync=False) for d in datas]
+        bufs = [_buf(d) for d in datas]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("push_many: all sources host, or all device")
+        self._order(keys, datas)
         n = len(keys)
         _check(self.lib.byteps_server_group_push_many(
             self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),
             (_sz * n)(*[b for _, b, _ in bufs]), n, worker, int(dtype), locs.pop() if n else 0))
 
     def pull_many(self, keys, outs) -> None:
-        _sync_producers(outs)
-        bufs = [_buf(o, sync=False) for o in outs]
+        bufs = [_buf(o) for o in outs]
         locs = {loc for _, _, loc in bufs}
         if len(locs) > 1:
             raise ValueError("pull_many: all destinations host, or all device")
+        self._order(keys, outs)
         n = len(keys)
         _check(self.lib.byteps_server_group_pull_many(
             self.handle, (_u64 * n)(*keys), (_vp * n)(*[p for p, _, _ in bufs]),

@@ -116,3 +116,65 @@ def test_local_reduce_leg_two_gloo_ranks_on_one_gpu():
     for r in (0, 1):
         assert "error" not in out[r], out[r]
         assert out[r]["exact_vs_rank_order_fold"] is True
+
+
+_RCCL_LEGS = r'''
+import json, os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["BPSR_ROOT"])
+import bench
+from oracle.oracle import PortReducer
+from prophet_amd.dtypes import DType
+from prophet_amd.shard import ShardedReducer
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+dist.barrier()
+comm, how = bench.shard_comm(dev)
+E = 1_000_003
+sc = bench.scatter_leg(dev, 1, 0, 8, reps=2, n_elems=E, comm=comm)
+lr = bench.local_reduce_leg(dev, 1, 0, reps=2, n_elems=E, comm=comm)
+# the same call, checked against the oracle's left fold of the 8 pushes
+g = torch.Generator(device=dev)
+g.manual_seed(11)
+pushes = [torch.randn(E, device=dev, generator=g) for _ in range(8)]
+recv = [torch.empty(E, device=dev) for _ in range(8)]
+owned = torch.empty(E, device=dev)
+ShardedReducer(E, comm=comm).scatter_reduce(0, pushes, recv, owned)
+torch.cuda.synchronize()
+want = np.zeros(E * 4, np.uint8)
+PortReducer(nthreads=4).sum_n(want, [p.cpu().numpy().view(np.uint8) for p in pushes], E * 4,
+                              DType.FLOAT32)
+oracle_ok = bool(np.array_equal(owned.cpu().numpy().view(np.uint8), want))
+comm.close()
+dist.destroy_process_group()
+print(json.dumps({"how": how, "scatter": sc, "local_reduce": lr, "oracle_ok": oracle_ok}))
+'''
+
+
+def test_exchange_legs_through_shard_abi_on_rccl_world1():
+    """The N > 1 bench legs as the driver's multi-GPU run takes them, at world
+    1 on this box: the communicator comes from the torch process group
+    (bench.shard_comm), every exchange is a byteps_shard_* call over RCCL
+    (transport "rccl-shard-abi"), and both legs' results are exact; the same
+    scatter_reduce call equals the oracle's left fold bit for bit."""
+    env = dict(os.environ, BPSR_ROOT=ROOT, MASTER_ADDR="127.0.0.1")
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    env["MASTER_PORT"] = str(s.getsockname()[1])
+    s.close()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", _RCCL_LEGS], env=env, capture_output=True,
+                       text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert "RCCL" in out["how"] or "NCCL" in out["how"], out["how"]
+    sc, lr = out["scatter"], out["local_reduce"]
+    assert sc["transport"] == lr["transport"] == "rccl-shard-abi"
+    assert sc["exact_vs_torch_fold"] is True and sc["scatter_fold_ms"] > 0
+    assert lr["exact_vs_rank_order_fold"] is True and lr["allreduce_ms"] > 0
+    assert out["oracle_ok"] is True

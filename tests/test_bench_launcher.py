@@ -53,6 +53,24 @@ def test_launcher_one_line_n_ranks(n):
         lr = line["local_reduce"]
         assert "error" not in lr, lr
         assert lr["exact_vs_rank_order_fold"] is True and lr["allreduce_ms"] > 0
+        # the CPU self-test moves slices with torch P2P over gloo
+        assert sc["scatter"]["transport"] == lr["transport"] == "torch-p2p"
+        assert "shard_comm" not in line
+
+
+def test_exchange_transport_rule():
+    """N > 1 on GPUs (one rank per GPU): the scatter and local-reduce legs go
+    through byteps_shard_* over RCCL (the code core_loops.cc binds); a
+    one-GPU rehearsal and the CPU self-test use torch P2P."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for n in (2, 4, 8):
+        assert bench.uses_shard_abi(n, cuda=True, rehearse=False)
+        assert not bench.uses_shard_abi(n, cuda=True, rehearse=True)
+        assert not bench.uses_shard_abi(n, cuda=False, rehearse=False)
+    assert not bench.uses_shard_abi(1, cuda=True, rehearse=False)
+    assert bench._transport(object()) == "rccl-shard-abi"
+    assert bench._transport(None) == "torch-p2p"
 
 
 def test_torchrun_launch_one_line():

@@ -416,7 +416,7 @@ def test_push_async_rounds(port, policy):
 
 
 def test_pull_into_async_rules_and_cancel(port):
-    """byteps_server_pull_into_async: refused for host memory, in async mode,
+    """byteps_server_pull_into_async: refused for pageable host memory, in async mode,
     with scheduling or engine blocking, and for more bytes than the key; a
     pull parked for a round that never finishes is answered ECANCELED at
     shutdown; one queued after the round finished is copied and answered."""
@@ -454,8 +454,10 @@ def test_pull_into_async_rules_and_cancel(port):
     want = np.zeros(n * 4, np.uint8)
     port.sum_n(want, [data(dt, n, w, 1, 1) for w in (1, 0)], n * 4, dt)
     assert np.array_equal(out.cpu().numpy(), want)
-    srv.pull_into_async(1, out, cb)                        # the round is finished: at once
-    assert done.acquire(timeout=30)
+    pinned = torch.zeros(n * 4, dtype=torch.uint8, pin_memory=True)
+    srv.pull_into_async(1, pinned, cb)      # the round is finished: at once, into pinned host
+    assert done.acquire(timeout=30)         # memory through its device view
+    assert np.array_equal(pinned.numpy(), want)
     srv.push(1, 0, data(dt, n, 0, 2, 1), dt)               # round 2: one push of two
     srv.pull_into_async(1, out, cb)                        # parked: never finishes
     time.sleep(0.2)
@@ -978,6 +980,86 @@ def test_push_async_device_copies_batched(port, combine, pull_mode, monkeypatch)
     if combine == "1":
         launches = st.get("push_copy_launches", 0) - st0.get("push_copy_launches", 0)
         assert 1 <= launches <= N * R * len(keys)
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
+def test_mixed_push_async_and_push_many_same_keys(port, dt):
+    """Combining mode, the advisor's round-3 race: half the workers push device
+    data with push_async (their copies into the slots queue on the lane
+    issuer), the other half with push_many on the SAME keys.  A push_many that
+    completes a round must not issue its fold ahead of a copy still queued on
+    the issuer: every pulled byte equals the oracle's fold in the recorded
+    arrival order, over several rounds of large keys (slow copies)."""
+    from prophet_amd.server import PSServer
+    N, R = 6, 4
+    sizes = [(256 << 10) + 17 * j for j in range(24)]   # elements per key
+    keys = list(range(900, 900 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    outs = {(w, r): [torch.empty(n * es, dtype=torch.uint8, device=dev) for n in sizes]
+            for w in range(N) for r in range(1, R + 1)}
+    torch.cuda.synchronize()
+    acks = threading.Semaphore(0)
+    bad = []
+
+    def ack(k, w, st):
+        if st:
+            bad.append((k, w, st))
+        acks.release()
+    bar = threading.Barrier(N + 1)
+    errors, orders = [], {}
+
+    def worker(w):
+        try:
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)          # init round: blocking
+            for r in range(1, R + 1):
+                if w % 2 == 0:
+                    for j, k in enumerate(keys):
+                        srv.push_async(k, w, src[(w, r, j)], dt, ack)
+                    got = threading.Semaphore(0)
+                    for j, k in enumerate(keys):
+                        srv.pull_into_async(k, outs[(w, r)][j],
+                                            lambda kk, st: (bad.append((kk, st)) if st else None,
+                                                            got.release()))
+                    for _ in keys:
+                        assert got.acquire(timeout=60)
+                else:
+                    srv.push_many(keys, w, [src[(w, r, j)] for j in range(len(keys))], dt)
+                    srv.pull_many(keys, outs[(w, r)])
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for r in range(1, R + 1):
+        bar.wait(timeout=240)
+        for j, k in enumerate(keys):
+            rounds, _, order = srv.key_info(k)
+            assert rounds == r
+            orders[(r, j)] = order
+        bar.wait(timeout=120)
+    for t in ts:
+        t.join(timeout=60)
+    assert not errors, errors
+    for _ in range((N // 2) * R * len(keys)):
+        assert acks.acquire(timeout=30)
+    assert not bad, bad[:5]
+    srv.close()
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, j) for w in orders[(r, j)]], n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, outs[(w, r)][j].cpu().numpy(), want,
+                                   nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
 
 
 def _copy_to_ptr(ptr, src):

@@ -130,10 +130,24 @@ def test_group_config_from_env(monkeypatch):
         server.group_config_from_env()
 
 
-def test_producer_sync_accepts_host_buffers():
-    """numpy 2 arrays carry a ``.device`` attribute too: the one-wait-per-call
-    producer sync of the batched calls must skip host buffers (numpy and CPU
-    tensors) without touching a GPU."""
+def test_producer_events_skip_host_buffers():
+    """numpy 2 arrays carry a ``.device`` attribute too: the producer ordering
+    of the calls (an event per device with pending work, for
+    byteps_server_order_after) must skip host buffers (numpy and CPU tensors)
+    without touching a GPU, and then order nothing."""
     import numpy as np
     import torch
-    server._sync_producers([np.zeros(4, np.uint8), torch.zeros(4), np.ones(2)])
+    assert server._producer_events([np.zeros(4, np.uint8), torch.zeros(4), np.ones(2)]) == []
+    calls = []
+    server._order_after(lambda *a: calls.append(a) or 0, None, [1, 2], [np.zeros(4)])
+    assert calls == []
+
+
+def test_order_after_argument_errors_without_gpu():
+    """byteps_server_order_after / _group_order_after refuse null handles and
+    events before any HIP call."""
+    import ctypes
+    lib = server._lib()
+    ev = ctypes.c_void_p(1)
+    assert lib.byteps_server_order_after(None, None, 0, ev) == reducer.EARGS
+    assert lib.byteps_server_group_order_after(None, None, 0, ev) == reducer.EARGS

@@ -2,9 +2,10 @@
 two instances on device 0 (both ordinals 0 — the routing, scatter and gather
 are the same for distinct GPUs), fp32 and fp16, three rounds in random
 arrival order from concurrent worker threads, whole-key hash and range split.
-Each piece of each key must equal the oracle's left fold in the arrival order
-ITS instance recorded (range pieces of one key may fold in different orders
-when workers race; whole keys have one order, as in the reference)."""
+Every key — a range-split one included — has ONE arrival order per round
+(server.cc:216-250): every instance holding a piece records the same order
+(the group's stamp), and the whole pulled key equals the oracle's left fold of
+the whole key in that order."""
 import random
 import threading
 import time
@@ -87,16 +88,20 @@ def test_group_rounds_bit_exact(dt, split, batched):
             assert not errors, errors
             for j, (k, n) in enumerate(zip(keys, sizes)):
                 ins = [data(dt, n, w, rnd, j) for w in range(N)]
+                orders = []
                 for inst, off, ln in routes[k]:
                     rounds, _, order = grp.instance(inst).key_info(k)
                     assert rounds == rnd, (k, inst, rounds, rnd)
-                    if rnd == 0:
-                        continue
-                    want = np.zeros(ln, np.uint8)
-                    port.sum_n(want, [ins[w][off:off + ln] for w in order], ln, dt)
-                    for w in range(N):
-                        assert np.array_equal(pulled[(w, rnd)][j][off:off + ln], want), \
-                            (k, inst, w, rnd)
+                    orders.append(order)
+                if rnd == 0:
+                    continue
+                # one order for the whole key, whichever instances hold it
+                assert all(o == orders[0] for o in orders), (k, rnd, orders)
+                assert sorted(orders[0]) == list(range(N))
+                want = np.zeros(n * es, np.uint8)
+                port.sum_n(want, [ins[w] for w in orders[0]], n * es, dt)
+                for w in range(N):
+                    assert np.array_equal(pulled[(w, rnd)][j], want), (k, w, rnd)
             bar.wait()
     finally:
         for t in ts:
@@ -138,4 +143,111 @@ def test_group_device_buffers_and_instances():
             assert np.array_equal(part, want)
         for w in range(N - 2):     # the round's remaining pulls (it re-arms after N)
             grp.pull(key, out)
+    grp.close()
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
+def test_group_split_key_racing_workers_device_pulls(dt):
+    """4 racing workers, range split over 3 instances, device pushes, and
+    every worker pulling the split key concurrently into device memory (the
+    gather queues every piece at once, pull_into_async) and, every other
+    round, into pinned host memory; three rounds.  Every pull equals the
+    oracle's fold of the WHOLE key in the group's single recorded order; a
+    short pull returns the same prefix."""
+    from prophet_amd.server import PSServerGroup
+    N, R, n = 4, 3, 1_000_003
+    es = elem_size(dt)
+    key = (3 << 16) + 1
+    grp = PSServerGroup(N, devices=[0, 0, 0], engine_lanes=2, split="range",
+                        split_min_bytes=64 * 1024)
+    assert len(grp.route(key, n * es)) == 3
+    port = PortReducer(nthreads=4)
+    dev = torch.device("cuda:0")
+    src = {(w, r): torch.from_numpy(data(dt, n, w, r, 5)).to(dev)
+           for w in range(N) for r in range(R + 1)}
+    torch.cuda.synchronize()
+    bar = threading.Barrier(N + 1)
+    errors, pulled = [], {}
+
+    def worker(w):
+        try:
+            rng = random.Random(7 + w)
+            for r in range(R + 1):
+                time.sleep(rng.random() * 0.003)
+                grp.push(key, w, src[(w, r)], dt)
+                if r == 0:
+                    bar.wait(timeout=120)
+                    continue
+                if (r + w) % 2:
+                    out = torch.zeros(n * es, dtype=torch.uint8, pin_memory=True)
+                else:
+                    out = torch.zeros(n * es, dtype=torch.uint8, device=dev)
+                grp.pull(key, out)
+                pulled[(w, r)] = out.cpu().numpy()
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    try:
+        bar.wait(timeout=240)                 # the init round
+        for r in range(1, R + 1):
+            bar.wait(timeout=240)
+            assert not errors, errors
+            orders = [grp.instance(i).key_info(key)[2] for i in range(3)]
+            assert orders[0] == orders[1] == orders[2], (r, orders)
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, 5) for w in orders[0]], n * es, dt)
+            for w in range(N):
+                assert np.array_equal(pulled[(w, r)], want), (r, w)
+            bar.wait(timeout=120)
+    finally:
+        for t in ts:
+            t.join(timeout=60)
+    assert not errors, errors
+    # a short pull (the group cuts it from the key's pieces, not its own length)
+    for w in range(N):
+        grp.push(key, w, src[(w, 1)], dt)
+    head = torch.zeros(n * es // 2 + 6, dtype=torch.uint8, device=dev)
+    grp.pull(key, head)
+    orders = grp.instance(0).key_info(key)[2]
+    want = np.zeros(n * es, np.uint8)
+    port.sum_n(want, [data(dt, n, w, 1, 5) for w in orders], n * es, dt)
+    assert np.array_equal(head.cpu().numpy(), want[:head.numel()])
+    grp.close()
+
+
+def test_group_push_validation_and_partial_failure():
+    """A push whose length differs from the key's declared length is refused
+    before any piece is queued (the round is untouched and completes
+    normally); a pull longer than the key is refused."""
+    from prophet_amd.reducer import ReduceError
+    from prophet_amd.server import PSServerGroup
+    dt, N, n = DType.FLOAT32, 2, 300_001
+    key = 77
+    grp = PSServerGroup(N, devices=[0, 0], split="range", split_min_bytes=4096)
+    grp.init_key(key, n * 4, dt)
+    ins = [data(dt, n, w, 0, 1) for w in range(N)]
+    with pytest.raises(ReduceError):
+        grp.push(key, 0, ins[0][:-4], dt)               # another length: refused
+    with pytest.raises(ReduceError):
+        grp.push(key, 0, ins[0], DType.INT32)           # another dtype: refused
+    ts = [threading.Thread(target=grp.push, args=(key, w, ins[w], dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    r1 = [data(dt, n, w, 1, 1) for w in range(N)]
+    for w in range(N):                                   # round 1, worker order 0, 1
+        grp.push(key, w, r1[w], dt)
+    with pytest.raises(ReduceError):
+        grp.pull(key, np.zeros(n * 4 + 4, np.uint8))
+    out = np.zeros(n * 4, np.uint8)
+    grp.pull(key, out)
+    want = np.zeros(n * 4, np.uint8)
+    PortReducer(nthreads=4).sum_n(want, r1, n * 4, dt)
+    assert np.array_equal(out, want)
     grp.close()
