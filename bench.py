@@ -103,6 +103,8 @@ def parse(argv=None):
                    help="N = 1: skip the config-3 (ResNet-50 fp16 Prophet blocks) object")
     p.add_argument("--no-e2e", action="store_true",
                    help="skip the config-5 host-resident (PCIe-inclusive) object")
+    p.add_argument("--no-server", action="store_true",
+                   help="skip the config-1 host-resident PS-server-group object")
     p.add_argument("--e2e-bucket-mib", type=int, default=256,
                    help="config-5 object: bucket MiB per worker (16 workers; BASELINE: 256)")
     p.add_argument("--no-scatter", action="store_true",
@@ -755,6 +757,92 @@ def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int =
 
 
 # --------------------------------------------------------------------------
+# config 1 through the PS server group, host-resident, one server per GPU
+
+
+def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
+                     bucket_bytes: int = 64 << 20, rounds: int = 10, lanes: int = 4) -> dict:
+    """BASELINE config 1's server rounds from host memory on every GPU of the
+    node: each rank's process is one PS server (a byteps_server_group_* group
+    with ONE instance, on this rank's GPU, whole keys by the reference's djb2
+    hash — server.cc:339-400 runs one server per process) serving one
+    cfg1-shaped bucket: 2 workers' 64 MiB fp32 gradients as the 17 BytePS
+    partitions of 4,096,000 B (operations.cc:99-136, declared key = rank), in
+    pinned host memory as ps-lite's receive buffers would be.  A round: every
+    worker thread pushes its 17 partitions (byteps_server_group_push_many: H2D
+    into the receive slots, the fold on the lane issuers) and pulls the 17
+    merged partitions back into pinned host memory
+    (byteps_server_group_pull_many: the instances' copy kernels write the
+    pinned pages over PCIe).  Weak scaling: at N GPUs, N buckets over N PCIe
+    links.  Node rate = all ranks' pushed bytes / the slowest rank's median
+    round.  PCIe-inclusive; compare with ``cpu_baseline`` (the reference's
+    host-core round).  Exactness: every worker's pull equals torch's sum of the
+    two pushes (fp32, two operands: the left fold in either arrival order)."""
+    import threading
+    import torch
+    from prophet_amd.buckets import partition_tensor
+    from prophet_amd.dtypes import DType
+    from prophet_amd.server import PSServerGroup
+    multi = world > 1
+    import torch.distributed as dist
+    n = bucket_bytes // 4
+    parts = [(p.key, p.offset, p.len) for p in partition_tensor(0, bucket_bytes,
+                                                                 declared_key=rank)]
+    keys = [k for k, _, _ in parts]
+    gen = torch.Generator(device="cpu")
+    host = []
+    for w in range(n_workers):
+        gen.manual_seed(12000 + 16 * rank + w)
+        host.append(torch.randn(n, generator=gen).pin_memory())
+    outs = [torch.zeros(bucket_bytes, dtype=torch.uint8).pin_memory() for _ in range(n_workers)]
+    grp = PSServerGroup(n_workers, devices=[dev.index], engine_lanes=lanes, split="hash")
+    srcs = [[host[w].view(torch.uint8)[o:o + ln] for _, o, ln in parts] for w in range(n_workers)]
+    dsts = [[outs[w][o:o + ln] for _, o, ln in parts] for w in range(n_workers)]
+    errors = []
+
+    def rnd(init=False):
+        def worker(w):
+            try:
+                grp.push_many(keys, w, srcs[w], DType.FLOAT32)
+                if not init:
+                    grp.pull_many(keys, dsts[w])
+            except Exception as e:  # noqa: BLE001 — reported below
+                errors.append(repr(e))
+        ts = [threading.Thread(target=worker, args=(w,)) for w in range(n_workers)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errors:
+            raise RuntimeError(errors[0])
+    rnd(init=True)
+    rnd()
+    times = []
+    for _ in range(rounds):
+        if multi:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rnd()
+        times.append(time.perf_counter() - t0)
+    t = _max_over_ranks(dist, dev, [statistics.median(times)])[0]
+    want = host[0].clone()
+    for h in host[1:]:
+        want += h
+    ok = all(bool(torch.equal(o, want.view(torch.uint8))) for o in outs)
+    ok = _all_true(dist, dev, ok)
+    grp.close()
+    total = world * n_workers * bucket_bytes
+    return {"workload": (f"config 1 per GPU: {n_workers} workers x {bucket_bytes >> 20} MiB fp32 "
+                         f"as {len(parts)} partitions in pinned host memory, one PS server "
+                         f"(byteps_server_group_*, one instance, djb2 hash) per GPU, "
+                         f"push_many + pull_many per worker thread, {world} GPU(s) / PCIe links"),
+            "node_GiBps": round(total / t / GIB, 2),
+            "per_gpu_GiBps": round(n_workers * bucket_bytes / t / GIB, 2),
+            "round_ms": round(t * 1e3, 3), "rounds": rounds, "lanes": lanes,
+            "pcie_inclusive": True, "exact_vs_torch_sum": ok}
+
+
+# --------------------------------------------------------------------------
 # config 3: ResNet-50 fp16 Prophet blocks through the block queue
 
 
@@ -1215,6 +1303,14 @@ def main(argv=None):
                     fold=None if cuda else _torch_fold, comm=comm)
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}
+        leg("server_cfg1")
+        if cuda and not args.no_server:
+            try:
+                line["server_cfg1"] = server_group_leg(dev, world, rank)
+            except Exception as e:  # report, never hide
+                line["server_cfg1"] = {"error": repr(e)}
+        elif not args.no_server:
+            line["server_cfg1"] = {"skipped": "the PS server needs a GPU (--device cpu)"}
         if cuda and not args.no_e2e:
             leg("e2e_cfg5")
             try:

@@ -72,6 +72,24 @@ typedef struct byteps_server byteps_server;
  * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
+/* Device releases (BPSR_SERVER_RELEASE=device; sync mode, fused policy, the
+ * default engine, num_workers <= 8): at the first round completion after the
+ * init round the server builds ONE keyed block queue over every declared key
+ * of that key's dtype (each key's receive slots in worker order and its
+ * store).  From then on a round's last arrival issues no launch: it stores
+ * the key's arrival order and release word — from the host when the pushes
+ * are in their slots already (byteps_server_push_ready), or by a one-lane
+ * kernel behind the round's copies — and one consumer launch per epoch (the
+ * epoch's first release launches it) folds every key of the queue, each key's
+ * tiles as soon as that key is released, in its arrival order (the same bits
+ * as the launch path).  Pulls and views of a released round are answered once
+ * that epoch's consumer has completed.  Contract: every key of the queue
+ * completes one round per epoch (BytePS pushes every key once per
+ * iteration); a key that is not pushed within BPSR_SERVER_RELEASE_TIMEOUT_S
+ * (default 5) seconds makes that epoch's consumer give up: the keys released
+ * in it fail with BYTEPS_REDUCE_ETIMEOUT and the server goes back to launches
+ * for good.  Keys declared after the queue was built, and keys of another
+ * dtype, always use launches. */
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
 int byteps_server_destroy(byteps_server* s);
 
@@ -208,7 +226,8 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
  * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
- * push-copy launches; the first n. */
+ * push-copy launches, out[6] keyed consumer launches and out[7] rounds
+ * released on the device (BPSR_SERVER_RELEASE=device); the first n (<= 8). */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

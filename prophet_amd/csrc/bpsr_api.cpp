@@ -668,6 +668,15 @@ struct byteps_reduce_blockq {
   uint32_t* hflags = nullptr;
   uint32_t* hflags_dev = nullptr;
   bool host_rel = false;
+  // Keyed queue (bpsr::keyq_*, the PS server's device releases): one block
+  // per key, (arrival order << 32 | epoch) words, the control word in pinned
+  // host memory so the server reads a timeout without a copy.
+  bool keyed = false;
+  uint64_t* kwords = nullptr;       // device, one per block
+  uint64_t* khwords = nullptr;      // pinned host, two per block (epoch parity)
+  uint64_t* khwords_dev = nullptr;
+  BlockqCtl* hctl = nullptr;        // pinned host
+  BlockqCtl* hctl_dev = nullptr;
 };
 
 // One consumer stream per device, created on first use, never destroyed:
@@ -704,6 +713,9 @@ static hipError_t blockq_events(byteps_reduce_blockq* q) {
 }
 
 static void blockq_free(byteps_reduce_blockq* q) {
+  if (q->kwords) (void)hipFree(q->kwords);
+  if (q->khwords) (void)hipHostFree(q->khwords);
+  if (q->hctl) (void)hipHostFree(q->hctl);
   if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
   if (q->join_ev) (void)hipEventDestroy(q->join_ev);
   if (q->dev_table) (void)hipFree(q->dev_table);
@@ -788,6 +800,8 @@ int byteps_reduce_blockq_create(const byteps_bucket_desc* buckets, int nbuckets,
 
 int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double timeout_s) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (q->keyed && wg_per_cu > 0)
+    return fail(BYTEPS_REDUCE_EARGS, "a keyed queue has the dispatch-ordered consumer");
   if (wg_per_cu > 8) return fail(BYTEPS_REDUCE_EARGS, "wg_per_cu %d > 8", wg_per_cu);
   if (wg_per_cu > 0 && q->host_rel)
     return fail(BYTEPS_REDUCE_EARGS, "host releases need the dispatch-ordered consumer");
@@ -830,6 +844,9 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.epoch = epoch;
   Q.helper = 0;
   Q.hflags = nullptr;
+  Q.keyed = 0;
+  Q.kwords = nullptr;
+  Q.khwords = nullptr;
   const Tuning tu = tuning_for_n(q->ti.nmax);
   const bool gated = q->occ == 0;
   size_t lds;
@@ -1035,3 +1052,119 @@ int byteps_reduce_sync(void* stream) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------- keyed queue --
+// (bpsr_internal.h keyq_*: the PS server's device releases)
+
+namespace bpsr {
+
+int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double timeout_s,
+                byteps_reduce_blockq** out) {
+  if (!out || nkeys < 1 || !buckets) return fail(BYTEPS_REDUCE_EARGS, "bad keyed queue table");
+  *out = nullptr;
+  for (int k = 0; k < nkeys; ++k)
+    if (buckets[k].n < 1 || buckets[k].n > kKeyedMaxSrcs)
+      return fail(BYTEPS_REDUCE_EARGS, "keyed queue: key %d has %d sources (1..%d)", k,
+                  buckets[k].n, kKeyedMaxSrcs);
+  std::vector<int> block_end((size_t)nkeys);
+  for (int k = 0; k < nkeys; ++k) block_end[(size_t)k] = k + 1;
+  byteps_reduce_blockq* q = nullptr;
+  int rc = byteps_reduce_blockq_create(buckets, nkeys, block_end.data(), nkeys, dtype,
+                                       kModeReference, &q);
+  if (rc) return rc;
+  q->keyed = true;
+  if (timeout_s > 0) q->timeout_s = timeout_s;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q->kwords), sizeof(uint64_t) * (size_t)nkeys);
+  if (e == hipSuccess) e = hipMemset(q->kwords, 0, sizeof(uint64_t) * (size_t)nkeys);
+  void* p = nullptr;
+  void* d = nullptr;
+  if (e == hipSuccess)
+    e = hipHostMalloc(&p, sizeof(uint64_t) * 2 * (size_t)nkeys,
+                      hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) {
+    q->khwords = static_cast<uint64_t*>(p);
+    for (int i = 0; i < 2 * nkeys; ++i) __atomic_store_n(q->khwords + i, (uint64_t)0, __ATOMIC_RELEASE);
+    e = hipHostGetDevicePointer(&d, p, 0);
+    q->khwords_dev = static_cast<uint64_t*>(d);
+  }
+  if (e == hipSuccess)
+    e = hipHostMalloc(&p, 256, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) {
+    q->hctl = static_cast<BlockqCtl*>(p);
+    std::memset(p, 0, 256);
+    e = hipHostGetDevicePointer(&d, p, 0);
+    q->hctl_dev = static_cast<BlockqCtl*>(d);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // words zeroed before any stream uses them
+  if (e != hipSuccess) {
+    blockq_free(q);
+    return hip_fail(e, "keyed queue setup");
+  }
+  *out = q;
+  return BYTEPS_REDUCE_OK;
+}
+
+int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, uint32_t* epoch) {
+  std::lock_guard<std::mutex> g(q->mu);
+  hipStream_t own = nullptr;
+  hipError_t e = consumer_stream(q->device, q->cus, &own);
+  if (e != hipSuccess) return hip_fail(e, "consumer stream");
+  const uint32_t ep = q->launch_epoch + 1;
+  BlockqLaunch Q;
+  Q.L = batch_launch(q->dev_table, q->ti);
+  Q.L.stop = stop;
+  Q.flags = q->flags;
+  Q.block_first = q->flags + q->nblocks;
+  Q.ctl = q->hctl_dev;
+  Q.nblocks = (uint32_t)q->nblocks;
+  Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
+  Q.epoch = ep;
+  Q.helper = 1;  // workgroup 0 forwards the host words
+  Q.hflags = nullptr;
+  Q.keyed = 1;
+  Q.kwords = q->kwords;
+  Q.khwords = q->khwords_dev;
+  Q.grid = q->ti.tiles + 1;
+  // residency capped as for the gated consumer: tiles waiting for a key's
+  // last push never take a CU's last registers (copies must still run)
+  const Tuning tu = tuning_for_n(q->ti.nmax);
+  int occ = launch_occ(tu, q->ti.tiles, true);
+  if (occ == 0 || occ > q->gate_occ) occ = q->gate_occ;
+  e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16),
+                    occ_lds_bytes(occ), true, q->dtype, q->mode, own);
+  if (e != hipSuccess) return hip_fail(e, "keyed queue launch");
+  q->launch_epoch = ep;
+  if (stream) *stream = own;
+  if (epoch) *epoch = ep;
+  return BYTEPS_REDUCE_OK;
+}
+
+uint32_t keyq_next_epoch(byteps_reduce_blockq* q, int key) {
+  std::lock_guard<std::mutex> g(q->mu);
+  return q->rel_epoch[(size_t)key] + 1;
+}
+
+uint32_t keyq_launched(byteps_reduce_blockq* q) {
+  std::lock_guard<std::mutex> g(q->mu);
+  return q->launch_epoch;
+}
+
+int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s) {
+  std::lock_guard<std::mutex> g(q->mu);
+  const uint32_t ep = q->rel_epoch[(size_t)key] + 1;
+  const uint64_t w = key_word(perm, ep);
+  if (s) {
+    const hipError_t e = launch_key_release(q->kwords, (uint32_t)key, w, s);
+    if (e != hipSuccess) return hip_fail(e, "keyed release");
+  } else {
+    __atomic_store_n(q->khwords + 2 * (size_t)key + (ep & 1u), w, __ATOMIC_RELEASE);
+  }
+  q->rel_epoch[(size_t)key] = ep;
+  return BYTEPS_REDUCE_OK;
+}
+
+bool keyq_failed(byteps_reduce_blockq* q) {
+  return __atomic_load_n(&q->hctl->err, __ATOMIC_ACQUIRE) != 0;
+}
+
+}  // namespace bpsr

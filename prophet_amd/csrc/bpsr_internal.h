@@ -7,6 +7,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "bpsr/reduce.h"
 #include "bpsr_error.h"
 
 namespace bpsr {
@@ -114,7 +115,21 @@ struct BlockqLaunch {
   uint32_t epoch;           // this launch's epoch (>= 1)
   uint32_t helper;          // 1: workgroup 0 forwards host release words (hflags)
   const uint32_t* hflags;   // host-written release words (pinned, device view)
+  // Keyed consumer (the PS server's device releases, bpsr_server.cpp): one
+  // block per key, a tile waits for its OWN block only, and the block's word
+  // (arrival order << 32 | epoch) says in which order its sources fold.
+  uint32_t keyed;
+  uint64_t* kwords;          // device words, one per block (helper / stream releases write them)
+  const uint64_t* khwords;   // host words (device view), two per block by epoch parity
 };
+// Arrival order of a keyed block: position m's source is worker
+// (perm >> 4m) & 7 (at most 8 sources); kKeySkip: the round is folded
+// elsewhere, the tiles only pass.
+constexpr uint32_t kKeySkip = 0xffffffffu;
+constexpr int kKeyedMaxSrcs = 8;
+inline uint64_t key_word(uint32_t perm, uint32_t epoch) {
+  return ((uint64_t)perm << 32) | epoch;
+}
 // Released for epoch e: the block's word holds e or a later epoch (wrap-safe).
 __host__ __device__ inline bool epoch_reached(uint32_t have, uint32_t e) {
   return (int32_t)(have - e) >= 0;
@@ -227,6 +242,8 @@ hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bo
                          int dtype, int mode, hipStream_t s);
 hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s);
+// Stream-ordered keyed release: kwords[block] = word (system scope, release).
+hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word, hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.
@@ -260,5 +277,23 @@ int fold_any_alias(void* dst, const void* const* srcs, int n, size_t len, int dt
 
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s);
+
+// Keyed block queue (bpsr_api.cpp): the PS server's device releases.  One
+// block per key (bucket k: dst = the key's store, srcs = its receive slots in
+// WORKER order, n <= kKeyedMaxSrcs); launch k folds every key once, each tile
+// as soon as its own key is released for epoch k, in the arrival order its
+// release carries.  keyq_release with s == nullptr stores the word from the
+// host (the round's data already visible to the device); with a stream, a
+// one-lane kernel stores it behind that stream's earlier work.  The k-th
+// release of a key carries epoch k.  keyq_failed: a launch gave up waiting
+// (timeout), read from pinned host memory without a copy.
+int keyq_create(const struct byteps_bucket_desc* buckets, int nkeys, int dtype, double timeout_s,
+                struct byteps_reduce_blockq** out);
+int keyq_launch(struct byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream,
+                uint32_t* epoch);
+uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
+uint32_t keyq_launched(struct byteps_reduce_blockq* q);
+int keyq_release(struct byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s);
+bool keyq_failed(struct byteps_reduce_blockq* q);
 
 }  // namespace bpsr

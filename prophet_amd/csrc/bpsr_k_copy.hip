@@ -122,6 +122,18 @@ hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count
   return hipGetLastError();
 }
 
+// Keyed release behind the stream's earlier work (a round whose pushes were
+// copied into their slots on that stream): one lane stores the block's word.
+__global__ void key_release_kernel(uint64_t* kwords, uint32_t block, uint64_t word) {
+  if (threadIdx.x == 0)
+    __hip_atomic_store(kwords + block, word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word, hipStream_t s) {
+  hipLaunchKernelGGL(key_release_kernel, dim3(1), dim3(64), 0, s, kwords, block, word);
+  return hipGetLastError();
+}
+
 hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bool g, int dtype,
                          int mode, hipStream_t s) {
   const bool acc = mode == kModeAccumF32;

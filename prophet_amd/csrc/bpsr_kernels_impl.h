@@ -641,6 +641,112 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
   keep_prefetch(pf);
 }
 
+// Keyed block consumer (the PS server's device releases): one block per key,
+// dispatch-ordered like blockq_gate_kernel, but a tile waits for its OWN
+// block's word only (keys complete in any order; server.cc folds each key
+// when its last push arrives), and that word carries the round's arrival
+// order, so the tile folds its sources as the left fold in arrival order
+// (server.cc:216-250) from slots laid out by worker.
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Workgroup 0: forward the host-written words of this launch's epoch (the
+// epoch's parity slot) into the device words, until every block holds this
+// epoch (or the sticky error / the timeout ends the launch).  A block
+// released by a stream kernel already holds it.  Vector atomics only.
+__device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t par = Q.epoch & 1u;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    bool pending = false;
+    for (uint32_t base = 0; base < Q.nblocks; base += 64) {
+      const uint32_t b = base + lane;
+      if (b < Q.nblocks && (uint32_t)ld_sys64(Q.kwords + b) != Q.epoch) {
+        const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);
+        if ((uint32_t)h == Q.epoch)
+          __hip_atomic_store(Q.kwords + b, h, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+          pending = true;
+      }
+    }
+    if (__ballot(pending) == 0) return;
+    if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+    if (wall_clock64() - t0 > Q.timeout_ticks) {
+      if (lane == 0) __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// The record's sources in arrival order: position m <- worker (perm >> 4m) & 7
+// (wave-uniform selects, no indexing).
+__device__ __forceinline__ void permute_srcs(const unsigned char* const (&p)[8], uint32_t perm,
+                                             const unsigned char* (&q)[8]) {
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const uint32_t w = (perm >> (4 * m)) & 7u;
+    const unsigned char* v = p[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = w == (uint32_t)k ? p[k] : v;
+    q[m] = v;
+  }
+}
+
+template <class Op, int VPT, int NT>
+__global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
+  if (Q.helper && blockIdx.x == 0) {  // dispatched first: resident for the whole launch
+    forward_host_keys(Q);
+    return;
+  }
+  const uint32_t t = blockIdx.x - Q.helper;
+  const unsigned char* rec = Q.L.recs + (uint64_t)t * Q.L.rec_stride;
+  const RecRegs r = load_record(rec);
+  const uint32_t blk = reinterpret_cast<const TileHead*>(rec)->block;
+  const uint32_t pf = prefetch_record(Q.L, t);
+  uint64_t w = ld_sys64(Q.kwords + blk);
+  if ((uint32_t)w != Q.epoch) {
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(4);
+      w = ld_sys64(Q.kwords + blk);
+      if ((uint32_t)w == Q.epoch) break;
+      if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+      if (wall_clock64() - t0 > Q.timeout_ticks) {
+        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+  }
+  // the word was written after the round's data landed (host store after
+  // the last push, or a stream release behind the copies): acquire before
+  // the tile's loads
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const uint32_t perm = (uint32_t)(w >> 32);
+  if (perm == kKeySkip) {
+    keep_prefetch(pf);
+    return;
+  }
+  RecRegs rp = r;
+  permute_srcs(r.p, perm, rp.p);
+  if (r.kind == kTileElem) {
+    const BatchEntry& e = Q.L.entries[r.b];
+    const unsigned char* es[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) es[m] = e.srcs[(perm >> (4 * m)) & 7u];
+    fold_elements<Op>(es, e.n, e.dst, e.g, e.aligned != 0,
+                      (uint64_t)r.a * kBlock + threadIdx.x, (uint64_t)r.c * kBlock);
+  } else if (r.kind == kTileFull) {
+    fold_tile_full_buf<Op, VPT, NT, -8>(rp.p, rp.p, (int)r.n, r.dst, 0, threadIdx.x);
+  } else {
+    fold_tile_body<Op, VPT, NT, -8, true>(rp.p, rp.p, (int)r.n, r.dst, 0, 0, r.a, threadIdx.x);
+  }
+  keep_prefetch(pf);
+}
+
 // ------------------------------------------------------------- launchers ----
 
 // One launch of `kernel(arg)`; with `stop`, the kernel's own completion
@@ -737,6 +843,13 @@ static hipError_t launch_batched_op(const BatchLaunch& L, int vpt, const Tuning&
 
 template <class Op, int VPT, int NT>
 static hipError_t launch_blockq_k(const BlockqLaunch& Q, size_t lds, bool gated, hipStream_t s) {
+  if (Q.keyed) {
+    static KernelAttr attr_k;
+    const hipError_t okk =
+        allow_lds(attr_k, reinterpret_cast<const void*>(&blockq_key_kernel<Op, VPT, NT>));
+    if (okk != hipSuccess) return okk;
+    return launch_with_stop(blockq_key_kernel<Op, VPT, NT>, Q.grid, lds, s, Q.L.stop, Q);
+  }
   if (gated) {
     static KernelAttr attr_g;
     const hipError_t okg =

@@ -40,7 +40,8 @@ struct KeyState;
 // One engine message (server.h:65-75 BytePSEngineMessage): the fold work of
 // one arrival (SUM_RECV), of a finished round (COPY_MERGED, or the fused
 // left fold) or of an async push.
-enum JobKind { kSumRecv = 0, kAsyncSum = 1, kFinishIncremental = 2, kFinishFused = 3 };
+enum JobKind { kSumRecv = 0, kAsyncSum = 1, kFinishIncremental = 2, kFinishFused = 3,
+               kKeyRelease = 4 };  // a device-released round whose pushes were copied
 struct FoldJob {
   KeyState* ks = nullptr;
   int kind = kSumRecv;
@@ -66,6 +67,7 @@ struct Response {
   Lane* wait_lane = nullptr;
   uint64_t wait_seq = 0;
   size_t len = 0;
+  uint64_t kseq = 0;  // a view of a keyed round: answered once its epoch is published
 };
 
 // A blocking call served by the non-blocking machinery: the lane issuer
@@ -184,7 +186,12 @@ struct Lane {
   std::mutex done_mu;
   std::condition_variable cq_cv;    // issuer -> completer
   std::condition_variable done_cv;  // completer -> waiters (and the issuer)
-  std::deque<std::pair<uint64_t, hipEvent_t>> cq;
+  struct Tracked {
+    uint64_t seq;
+    hipEvent_t ev;
+    uint32_t kq_epoch;  // != 0: the keyed consumer launch of that epoch (lane 0 only)
+  };
+  std::deque<Tracked> cq;
   uint64_t issued_seq = 0, done_seq = 0;
   std::atomic<uint64_t> done_pub{0};  // done_seq, readable without done_mu (spinning waiters)
   bool cq_stop = false;
@@ -235,6 +242,13 @@ struct KeyState {
   // lane's fold mark (a later record of it covers this fold too).
   hipEvent_t fold_ev = nullptr;
   uint64_t fold_seq = 0;      // lane completion seq of the last issued round (0: untracked)
+  int fold_lane = 0;          // the lane whose completer tracks fold_seq
+  // device releases: the key's block in the server's keyed queue (-1: none),
+  // whether this round's last fold is a keyed consumer's, and whether a push
+  // of the current round was copied into its slot (released behind the copy)
+  std::atomic<int> kq_key{-1};
+  bool keyed = false;
+  bool round_copied = false;
   hipEvent_t copied = nullptr;
   hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
   bool has_done = false;
@@ -297,6 +311,34 @@ struct byteps_server {
   // kernel launch would.  -1 = off.
   long fail_after = -1;
   std::atomic<long> issued{0};
+  // Device releases (BPSR_SERVER_RELEASE=device: sync mode, fused policy, the
+  // default engine, N <= 8).  At the first round completion after the init
+  // round, ONE keyed block queue is built over every allocated key of that
+  // dtype (bpsr::keyq_*: its slots in worker order and its store).  A round's
+  // last arrival then stores the key's arrival order and release word
+  // instead of issuing a launch (behind the round's copies, a one-lane
+  // release kernel on the lane's copy stream), and one consumer launch per
+  // epoch folds every key of the queue, each as soon as it is released.
+  // Nothing reads a keyed store before lane 0's completer has seen its
+  // epoch's consumer complete: pulls parked on it are handed to their lanes
+  // then, views wait for it.  A consumer that times out (a key of the queue
+  // not pushed within BPSR_SERVER_RELEASE_TIMEOUT_S) fails the keys released
+  // in its epoch and turns device releases off for good.
+  bool dev_release = false;
+  double kq_timeout_s = 5.0;
+  std::unique_ptr<bpsr::Lane> klane;  // its completer tracks the consumer launches (no streams)
+  std::mutex kq_mu;  // guards the kq_* state below (taken after a key's mu, never before)
+  byteps_reduce_blockq* kq = nullptr;
+  bool kq_tried = false;
+  std::atomic<bool> kq_off{false};
+  std::vector<bpsr::KeyState*> kq_keys;  // block -> key
+  static constexpr int kKqRing = 64;
+  hipEvent_t kq_ev[kKqRing] = {};       // stop event of epoch e at e % kKqRing
+  uint64_t kq_ev_seq[kKqRing] = {};     // lane-0 seq of that launch
+  uint32_t kq_ev_epoch[kKqRing] = {};
+  uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
+  std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
+  std::atomic<uint64_t> n_consumer_launches{0}, n_key_releases{0};
 };
 
 namespace bpsr {
@@ -331,23 +373,38 @@ hipError_t wait_copies(Lane& L) {
 uint64_t track(Lane& L, hipEvent_t ev) {
   std::lock_guard<std::mutex> g(L.done_mu);
   const uint64_t seq = ++L.issued_seq;
-  L.cq.emplace_back(seq, ev);
+  L.cq.push_back({seq, ev, 0});
   L.cq_cv.notify_one();
   return seq;
 }
 
+// A keyed consumer launch is tracked like a lane's launches, on the server's
+// keyed completer (s->klane), with its epoch.
+uint64_t track_keyed(Lane& L, hipEvent_t ev, uint32_t epoch) {
+  std::lock_guard<std::mutex> g(L.done_mu);
+  const uint64_t seq = ++L.issued_seq;
+  L.cq.push_back({seq, ev, epoch});
+  L.cq_cv.notify_one();
+  return seq;
+}
+
+void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq);
+
 // The lane's completer thread: waits for tracked launches in issue order and
-// publishes how far they have completed.
-void completer_main(byteps_server* s, int lane) {
+// publishes how far they have completed (a keyed consumer's epoch is settled
+// first: kq_epoch_done).
+void completer_main(byteps_server* s, Lane* Lp) {
   (void)hipSetDevice(s->cfg.device);
-  Lane& L = *s->lanes[lane];
+  Lane& L = *Lp;
   std::unique_lock<std::mutex> lk(L.done_mu);
   for (;;) {
     L.cq_cv.wait(lk, [&] { return L.cq_stop || !L.cq.empty(); });
     if (L.cq.empty()) return;  // stopping, drained
-    const auto [seq, ev] = L.cq.front();
+    const Lane::Tracked t = L.cq.front();
+    const uint64_t seq = t.seq;
     lk.unlock();
-    (void)hipEventSynchronize(ev);  // a failed launch failed its keys already
+    (void)hipEventSynchronize(t.ev);  // a failed launch failed its keys already
+    if (t.kq_epoch) kq_epoch_done(s, t.kq_epoch, t.seq);
     lk.lock();
     L.cq.pop_front();
     L.done_seq = seq;
@@ -447,6 +504,7 @@ bool can_push(const byteps_server* s, const KeyState* ks, int w) {
 int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc,
             bool wait = true) {
   Lane& L = *s->lanes[ks->lane];
+  ks->round_copied = true;
   hipError_t e = hipSuccess;
   if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
   if (e == hipSuccess)
@@ -522,6 +580,7 @@ void respond_later(byteps_server* s, KeyState* ks, byteps_server_pull_cb cb, voi
   r.ctx = ctx;
   r.view = view;
   r.status = status;
+  if (ks->keyed && status == 0) r.kseq = ks->fold_seq;
   enqueue_response(s, r);
 }
 
@@ -573,7 +632,15 @@ void fail_key(byteps_server* s, KeyState* ks, int rc) {
 void queue_pull_copies(byteps_server* s, KeyState* ks, const KeyState::WaitingCopy* wcs, size_t n) {
   if (n == 0) return;
   Lane& L = *s->lanes[ks->lane];
-  std::lock_guard<std::mutex> g(L.comb_mu);
+  std::unique_lock<std::mutex> kg(s->kq_mu, std::defer_lock);
+  bool park = false;
+  if (ks->keyed) {  // nothing reads a keyed store before its epoch is published
+    kg.lock();
+    park = s->kq_done_seq < ks->fold_seq;
+    if (!park) kg.unlock();
+  }
+  std::unique_lock<std::mutex> g(L.comb_mu, std::defer_lock);
+  if (!park) g.lock();
   for (size_t i = 0; i < n; ++i) {
     const KeyState::WaitingCopy& wc = wcs[i];
     PullJob j;
@@ -587,9 +654,10 @@ void queue_pull_copies(byteps_server* s, KeyState* ks, const KeyState::WaitingCo
     j.resp.ctx = wc.ctx;
     j.resp.view = static_cast<const char*>(wc.view);
     j.resp.len = wc.len;
-    L.pulls.push_back(j);
+    if (park) s->kq_parked.push_back(j);
+    else L.pulls.push_back(j);
   }
-  L.comb_cv.notify_one();
+  if (!park) L.comb_cv.notify_one();
 }
 
 // Set on the responder thread, which runs the callers' callbacks: a blocking
@@ -622,6 +690,14 @@ void responder_main(byteps_server* s) {
       continue;
     }
     int status = r.status;
+    if (status == 0 && r.kseq) {  // a view of a keyed round: its epoch first
+      Lane& K = *s->klane;
+      std::unique_lock<std::mutex> dl(K.done_mu);
+      K.done_cv.wait(dl, [&] { return K.done_seq >= r.kseq; });
+      dl.unlock();
+      std::lock_guard<std::mutex> g(r.ks->mu);
+      if (r.ks->error) status = r.ks->error;
+    }
     if (status == 0 && r.wait_lane) {  // a pull copied by the lane's issuer
       std::unique_lock<std::mutex> dl(r.wait_lane->done_mu);
       r.wait_lane->done_cv.wait(dl, [&] { return r.wait_lane->done_seq >= r.wait_seq; });
@@ -632,7 +708,7 @@ void responder_main(byteps_server* s) {
       hipError_t e = hipEventSynchronize(r.ks->mirrored);
       if (e != hipSuccess) status = hip_fail(e, "store mirror sync");
     }
-    if (r.status == 0) {
+    if (status == 0) {
       // Count BEFORE answering, under the key lock, as the reference counts
       // under flag_mu_ in the same step as SendPullResponse
       // (server.cc:100-113, 293-298): once the worker has its answer it may
@@ -648,9 +724,13 @@ void responder_main(byteps_server* s) {
 // A round's fold is issued: publish it (caller holds ks->mu).  `mark`: also
 // raise the lane's fold mark (a batched issue raises it once, before).
 int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
-                 bool mark = true, hipEvent_t batch = nullptr, uint64_t batch_seq = 0) {
+                 bool mark = true, hipEvent_t batch = nullptr, uint64_t batch_seq = 0,
+                 bool keyed = false) {
   Lane& L = *s->lanes[ks->lane];
   s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
+  ks->keyed = keyed;  // a keyed consumer's fold, tracked by the keyed completer
+  ks->fold_lane = keyed ? -1 : ks->lane;
+  ks->round_copied = false;
   if (mark) {  // a single fold: its own event, and the lane's mark
     hipError_t e = hipEventRecord(ks->done, L.fold);
     if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
@@ -684,6 +764,158 @@ int injected_failure(byteps_server* s) {
               s->fail_after);
 }
 
+// ------------------------------------------------------ device releases --
+
+// The keyed queue over every allocated key of `dtype` (block order = key
+// order), built once, at the first round completion after the init round
+// (caller holds s->kq_mu and that key's mu).  Keys declared later, and keys
+// of other dtypes, keep the lane launches.
+void build_kq(byteps_server* s, int dtype) {
+  std::vector<KeyState*> keys;
+  {
+    std::shared_lock<std::shared_mutex> g(s->map_mu);
+    for (auto& kv : s->keys) {
+      KeyState* k = kv.second.get();
+      if (k->allocated && k->dtype == dtype) keys.push_back(k);
+    }
+  }
+  if (keys.empty()) return;
+  std::sort(keys.begin(), keys.end(),
+            [](const KeyState* a, const KeyState* b) { return a->key < b->key; });
+  const int N = s->cfg.num_workers;
+  std::vector<byteps_bucket_desc> d(keys.size());
+  for (size_t i = 0; i < keys.size(); ++i) {
+    std::memset(&d[i], 0, sizeof(d[i]));
+    d[i].dst = keys[i]->store;
+    for (int w = 0; w < N; ++w) d[i].srcs[w] = keys[i]->slot[w];
+    d[i].len = keys[i]->len;
+    d[i].n = N;
+  }
+  if (keyq_create(d.data(), (int)d.size(), dtype, s->kq_timeout_s, &s->kq)) {
+    s->kq = nullptr;  // no queue: every round keeps the lane launches
+    return;
+  }
+  s->kq_keys = keys;
+  for (size_t i = 0; i < keys.size(); ++i) keys[i]->kq_key.store((int)i);
+}
+
+// Is this finished round of `ks` device-released?  Caller holds ks->mu.
+bool keyed_member(byteps_server* s, KeyState* ks) {
+  if (!s->dev_release || s->kq_off.load()) return false;
+  std::lock_guard<std::mutex> g(s->kq_mu);
+  if (!s->kq_tried) {
+    s->kq_tried = true;
+    build_kq(s, ks->dtype);
+  }
+  return ks->kq_key.load() >= 0;
+}
+
+// Release a finished round of a keyed key (caller holds ks->mu): the arrival
+// order and the release word go to the key's block — stored from the host
+// when the round's data is in its slots already (push_ready), or by a one-lane
+// kernel on `stream` behind the round's copies — after the consumer of the
+// block's epoch has been launched (the first release of an epoch launches
+// it).  Then the round is published like an issued fold.  Returns 1 when
+// device releases were turned off meanwhile (the caller folds with a launch).
+int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream) {
+  uint32_t perm = 0;
+  for (size_t m = 0; m < order.size(); ++m) perm |= (uint32_t)order[m] << (4 * m);
+  hipEvent_t ev = nullptr;
+  uint64_t seq = 0;
+  {
+    std::lock_guard<std::mutex> g(s->kq_mu);
+    if (s->kq_off.load()) return 1;
+    const uint32_t need = keyq_next_epoch(s->kq, ks->kq_key.load());
+    while (keyq_launched(s->kq) < need) {
+      const uint32_t next = keyq_launched(s->kq) + 1;
+      const int slot = (int)(next % byteps_server::kKqRing);
+      if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
+        return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
+                    byteps_server::kKqRing);
+      hipEvent_t& e = s->kq_ev[slot];
+      if (!e) {
+        const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (he != hipSuccess) {
+          e = nullptr;
+          return hip_fail(he, "hipEventCreate(consumer)");
+        }
+      }
+      uint32_t got = 0;
+      hipStream_t cs = nullptr;
+      if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
+      s->kq_ev_epoch[slot] = got;
+      s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
+      s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
+    }
+    if (stream) {
+      // behind the lane's pull copies too (a store is rewritten by the fold)
+      const hipError_t we = hipStreamWaitEvent(stream, s->lanes[ks->lane]->d2h_mark, 0);
+      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+    }
+    if (int rc = keyq_release(s->kq, ks->kq_key.load(), perm, stream)) return rc;
+    const int slot = (int)(need % byteps_server::kKqRing);
+    ev = s->kq_ev[slot];
+    seq = s->kq_ev_seq[slot];
+  }
+  s->n_key_releases.fetch_add(1, std::memory_order_relaxed);
+  return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
+}
+
+// The keyed completer saw epoch `epoch`'s consumer (lane seq `seq`) complete:
+// if a consumer gave up waiting, every key released at that epoch or later
+// fails (its store is not the round's fold) and device releases go off for
+// good; then the epoch is published and the pulls parked on it go to their
+// lanes' issuers (or fail with their key).
+void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
+  std::vector<PullJob> go, keep;
+  std::vector<KeyState*> failed;
+  {
+    std::lock_guard<std::mutex> g(s->kq_mu);
+    if (s->kq && keyq_failed(s->kq)) {
+      s->kq_off.store(true);
+      for (KeyState* k : s->kq_keys)
+        if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
+    }
+    s->kq_done_seq = seq;
+    for (PullJob& j : s->kq_parked) (j.ks->fold_seq <= seq ? go : keep).push_back(j);
+    s->kq_parked.swap(keep);
+  }
+  for (KeyState* k : failed) {
+    std::lock_guard<std::mutex> g(k->mu);
+    fail(BYTEPS_REDUCE_ETIMEOUT, "device release: a key of the queue was not pushed within %.3f s "
+         "(BPSR_SERVER_RELEASE_TIMEOUT_S); its epoch's folds are void", s->kq_timeout_s);
+    fail_key(s, k, BYTEPS_REDUCE_ETIMEOUT);
+  }
+  for (PullJob& j : go) {
+    int err = 0;
+    {
+      std::lock_guard<std::mutex> g(j.ks->mu);
+      err = j.ks->error;
+    }
+    if (err) {
+      if (j.direct) {
+        j.direct->finish(err);
+      } else {
+        j.resp.status = err;
+        enqueue_response(s, j.resp);
+      }
+      continue;
+    }
+    Lane& L = *s->lanes[j.ks->lane];
+    std::lock_guard<std::mutex> g(L.comb_mu);
+    L.pulls.push_back(j);
+    L.comb_cv.notify_one();
+  }
+}
+
+// Blocking readers of a keyed round's store wait for its epoch to be
+// published (caller holds no lock); then the key's error, if it failed.
+void wait_published(byteps_server* s, KeyState* ks, uint64_t seq) {
+  Lane& K = *s->klane;
+  std::unique_lock<std::mutex> dl(K.done_mu);
+  K.done_cv.wait(dl, [&] { return K.done_seq >= seq; });
+}
+
 // Issue a job's kernels on the lane's fold stream and apply its state
 // changes — the body of the engine thread (server.cc:70-145).  Caller holds
 // ks->mu.
@@ -692,6 +924,14 @@ int execute(byteps_server* s, const FoldJob& j) {
   KeyState* ks = j.ks;
   Lane& L = *s->lanes[ks->lane];
   void* fs = reinterpret_cast<void*>(L.fold);
+  FoldJob fallback;
+  if (j.kind == kKeyRelease) {  // a keyed round whose pushes were copied: behind the copies
+    const int rc = key_release(s, ks, j.order, L.copy);
+    if (rc <= 0) return rc;
+    fallback = j;  // device releases went off meanwhile: an ordinary fused fold
+    fallback.kind = kFinishFused;
+    return execute(s, fallback);
+  }
   // Folds run behind the slots' copies (byteps_server_push_async returns
   // before they finish; the copy stream is in order, so the lane's copy mark
   // covers every copy issued so far, batched ones included) and behind the
@@ -836,6 +1076,9 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     }
     ks->fold_ev = ks->done;
     ks->fold_seq = 0;
+    ks->fold_lane = ks->lane;
+    ks->keyed = false;
+    ks->round_copied = false;
     ks->has_done = true;
     ks->inited = true;
     std::fill(ks->got.begin(), ks->got.end(), 0);
@@ -878,6 +1121,32 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     q->count(ks->key);  // the SUM_RECV the reference would have queued
   }
   if (ks->arrived < N) return 0;
+  if (!q && keyed_member(s, ks)) {
+    // device release: no launch for this round
+    std::vector<int> order;
+    order.swap(ks->order);
+    ks->arrived = 0;
+    if (!ks->round_copied) {  // the pushes are in their slots already (push_ready)
+      const int rc = key_release(s, ks, order, nullptr);
+      if (rc <= 0) {
+        if (rc) fail_key(s, ks, rc);
+        return rc;
+      }
+    }
+    // copied pushes (released behind the copies, by the lane issuer), or
+    // device releases turned off meanwhile (an ordinary fold)
+    FoldJob j;
+    j.ks = ks;
+    j.kind = ks->round_copied ? kKeyRelease : kFinishFused;
+    j.acc = order[0];
+    j.order = order;
+    if (defer) {
+      ks->pending++;
+      defer->push_back(std::move(j));
+      return 0;
+    }
+    return submit(s, ks, std::move(j));
+  }
   FoldJob j;
   j.ks = ks;
   j.kind = s->cfg.policy == BYTEPS_SERVER_INCREMENTAL ? kFinishIncremental : kFinishFused;
@@ -1037,6 +1306,14 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
     std::lock_guard<std::mutex> bg(L.batch_mu);
     hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
     if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    hipEvent_t last = nullptr;
+    for (auto& j : jobs) {  // keyed folds run on the consumer's stream
+      std::lock_guard<std::mutex> g(j.ks->mu);
+      if (!rc && j.ks->keyed && j.ks->has_done && j.ks->fold_ev != last) {
+        last = j.ks->fold_ev;
+        if ((e = hipStreamWaitEvent(L.copy, last, 0)) != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+      }
+    }
     std::vector<byteps_bucket_desc> d(jobs.size());
     for (size_t k = 0; k < jobs.size(); ++k) {
       std::memset(&d[k], 0, sizeof(d[k]));
@@ -1290,6 +1567,14 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
   if (s->schedule || s->blocking) s->combine = false;
   if (const char* fl = getenv("BPSR_SERVER_INFLIGHT")) s->inflight = std::max(1L, atol(fl));
+  if (const char* r = getenv("BPSR_SERVER_RELEASE")) s->dev_release = std::string(r) == "device";
+  if (const char* t = getenv("BPSR_SERVER_RELEASE_TIMEOUT_S"))
+    if (atof(t) > 0) s->kq_timeout_s = atof(t);
+  // device releases: the fused left fold of a sync round, through the lane
+  // issuers, at most kKeyedMaxSrcs workers (the release word's arrival order)
+  if (!s->combine || cfg->async_mode || cfg->policy != BYTEPS_SERVER_FUSED ||
+      cfg->num_workers > kKeyedMaxSrcs)
+    s->dev_release = false;
   int rc = set_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
@@ -1336,9 +1621,13 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
     if (s->schedule)
       for (int i = 0; i < cfg->engine_lanes; ++i)
         s->lanes[i]->dispatcher = std::thread(dispatcher_main, s.get(), i);
+    if (s->dev_release) {
+      s->klane = std::make_unique<Lane>();
+      s->klane->completer = std::thread(completer_main, s.get(), s->klane.get());
+    }
     if (s->combine)
       for (int i = 0; i < cfg->engine_lanes; ++i) {
-        s->lanes[i]->completer = std::thread(completer_main, s.get(), i);
+        s->lanes[i]->completer = std::thread(completer_main, s.get(), s->lanes[i].get());
         s->lanes[i]->issuer = std::thread(issuer_main, s.get(), i);
       }
     s->responder = std::thread(responder_main, s.get());
@@ -1354,6 +1643,27 @@ int byteps_server_destroy(byteps_server* s) {
   if (!s) return BYTEPS_REDUCE_OK;
   (void)hipSetDevice(s->cfg.device);
   destroy_lanes(s);  // queued jobs are issued first (the dispatchers drain)
+  if (s->klane) {    // the keyed consumers complete (or time out) and settle their epochs
+    {
+      std::lock_guard<std::mutex> g(s->klane->done_mu);
+      s->klane->cq_stop = true;
+      s->klane->cq_cv.notify_all();
+    }
+    if (s->klane->completer.joinable()) s->klane->completer.join();
+    std::vector<PullJob> parked;
+    {
+      std::lock_guard<std::mutex> g(s->kq_mu);
+      parked.swap(s->kq_parked);
+    }
+    for (PullJob& j : parked) {  // pulls of epochs that never completed: cancelled
+      if (j.direct) {
+        j.direct->finish(BYTEPS_REDUCE_ECANCELED);
+      } else {
+        j.resp.status = BYTEPS_REDUCE_ECANCELED;
+        enqueue_response(s, j.resp);
+      }
+    }
+  }
   if (s->responder.joinable()) {
     for (auto& kv : s->keys) {  // pulls whose round never finished: cancelled
       KeyState* ks = kv.second.get();
@@ -1393,6 +1703,9 @@ int byteps_server_destroy(byteps_server* s) {
     for (char* m : ks->mirror) (void)hipHostFree(m);
     if (ks->arena) (void)hipFree(ks->arena);
   }
+  if (s->kq) (void)byteps_reduce_blockq_destroy(s->kq);
+  for (hipEvent_t e : s->kq_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto& Lp : s->lanes) {
     if (Lp->fold) (void)hipStreamDestroy(Lp->fold);
     if (Lp->copy) (void)hipStreamDestroy(Lp->copy);
@@ -1529,6 +1842,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
     cj.ack.push_cb = cb;
     cj.ack.worker = worker;
     cj.direct = direct;
+    ks->round_copied = true;
     {
       Lane& L = *s->lanes[ks->lane];
       std::lock_guard<std::mutex> g(L.comb_mu);
@@ -1650,6 +1964,13 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
+  if (ks->keyed) {  // its epoch published first
+    const uint64_t need = ks->fold_seq;
+    lk.unlock();
+    wait_published(s, ks, need);
+    lk.lock();
+    if (ks->error) return key_error(ks);
+  }
   s->n_pulls.fetch_add(1, std::memory_order_relaxed);
   s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
@@ -1699,6 +2020,13 @@ int byteps_server_pull_host_view(byteps_server* s, uint64_t key, const void** da
   std::unique_lock<std::mutex> lk(ks->mu);
   if (!s->cfg.async_mode) ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
   if (ks->error) return key_error(ks);
+  if (ks->keyed) {  // its epoch published first
+    const uint64_t need = ks->fold_seq;
+    lk.unlock();
+    wait_published(s, ks, need);
+    lk.lock();
+    if (ks->error) return key_error(ks);
+  }
   if ((rc = ensure_mirror(s, ks, !s->cfg.async_mode))) return rc;
   size_t idx = ks->rounds & 1;
   if (s->cfg.async_mode) {  // the store changes with every push: a fresh D2H per view
@@ -1738,10 +2066,11 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   const bool has = ks->has_done;
   hipEvent_t ev = ks->fold_ev;
   const uint64_t need = ks->fold_seq;
+  const int fl = ks->fold_lane;
   const void* view = ks->store;
   lk.unlock();
-  if (need) {  // tracked by the lane's completer: no HIP call here
-    Lane& L = *s->lanes[ks->lane];
+  if (need) {  // tracked by a completer (the lane's, or the keyed one): no HIP call here
+    Lane& L = fl < 0 ? *s->klane : *s->lanes[fl];
     std::unique_lock<std::mutex> dl(L.done_mu);
     L.done_cv.wait(dl, [&] { return L.done_seq >= need; });
   } else if (has) {
@@ -1749,6 +2078,7 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
     if (e != hipSuccess) return hip_fail(e, "store fold sync");
   }
   lk.lock();
+  if (ks->error) return key_error(ks);  // a keyed epoch that timed out
   s->n_pulls.fetch_add(1, std::memory_order_relaxed);
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   *data = view;
@@ -1898,6 +2228,17 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     std::lock_guard<std::mutex> bg(L.batch_mu);
     hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
     if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    {  // keyed folds run on the consumer's stream, not behind the fold mark
+      std::vector<hipEvent_t> waits;
+      for (int i : by_lane[l]) {
+        std::lock_guard<std::mutex> g(ks_of[i]->mu);
+        if (ks_of[i]->keyed && ks_of[i]->has_done) waits.push_back(ks_of[i]->fold_ev);
+      }
+      std::sort(waits.begin(), waits.end());
+      waits.erase(std::unique(waits.begin(), waits.end()), waits.end());
+      for (hipEvent_t w : waits)
+        if ((e = hipStreamWaitEvent(L.copy, w, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    }
     if (location == BYTEPS_SERVER_HOST) {
       for (int i : by_lane[l]) {
         e = hipMemcpyAsync(ks_of[i]->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice,
@@ -1927,6 +2268,7 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
   for (int i = 0; i < n; ++i) {
     KeyState* ks = ks_of[i];
     std::unique_lock<std::mutex> lk(ks->mu);
+    ks->round_copied = true;
     const bool init_round = !ks->inited;
     if ((rc = arrive(s, ks, worker, &defer))) {
       lk.unlock();
@@ -2038,6 +2380,12 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
       lk.lock();
       ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
     }
+    if (ks->keyed && !ks->error) {  // its epoch published first
+      const uint64_t need = ks->fold_seq;
+      lk.unlock();
+      wait_published(s, ks, need);
+      lk.lock();
+    }
     if (ks->error) {
       lk.unlock();
       (void)flush();
@@ -2091,10 +2439,11 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
 
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
   if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  const uint64_t v[6] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+  const uint64_t v[8] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
                          s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
-                         s->n_copy_launches.load()};
-  for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+                         s->n_copy_launches.load(), s->n_consumer_launches.load(),
+                         s->n_key_releases.load()};
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

@@ -42,6 +42,9 @@ def test_bench_two_ranks_rehearsed_on_one_gpu():
     lr = line["local_reduce"]
     assert "error" not in lr, lr
     assert lr["exact_vs_rank_order_fold"] is True
+    srv = line["server_cfg1"]          # one PS server per rank, host-resident rounds
+    assert "error" not in srv, srv
+    assert srv["exact_vs_torch_sum"] is True and srv["node_GiBps"] > 0
 
 
 def test_bench_one_gpu_line_has_every_object():
@@ -75,6 +78,48 @@ def test_bench_one_gpu_line_has_every_object():
     e2e = line["e2e_cfg5"]
     assert "error" not in e2e, e2e
     assert e2e["exact_vs_torch_fold_windows"] is True and e2e["pcie_inclusive"] is True
+    srv = line["server_cfg1"]
+    assert "error" not in srv, srv
+    assert srv["exact_vs_torch_sum"] is True and srv["node_GiBps"] > 0
+
+
+def test_server_group_leg_matches_oracle():
+    """The config-1 server-group object's rounds, checked against the oracle:
+    the same group calls on fresh data, every worker's pull equals the oracle's
+    fold of the pushes in the arrival order the instance recorded."""
+    import threading
+    import numpy as np
+    import torch
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import PortReducer
+    from prophet_amd.buckets import partition_tensor
+    from prophet_amd.dtypes import DType
+    from prophet_amd.server import PSServerGroup
+    N, B = 2, 8 << 20
+    parts = [(p.key, p.offset, p.len) for p in partition_tensor(0, B, bound=1 << 20)]
+    keys = [k for k, _, _ in parts]
+    grp = PSServerGroup(N, devices=[0], split="hash")
+    host = [torch.randn(B // 4).pin_memory() for _ in range(N)]
+    outs = [torch.zeros(B, dtype=torch.uint8).pin_memory() for _ in range(N)]
+    for rnd in range(3):
+        ts = [threading.Thread(target=lambda w=w: (
+            grp.push_many(keys, w, [host[w].view(torch.uint8)[o:o + ln] for _, o, ln in parts],
+                          DType.FLOAT32),
+            rnd and grp.pull_many(keys, [outs[w][o:o + ln] for _, o, ln in parts])))
+              for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+    port = PortReducer(nthreads=4)
+    for k, o, ln in parts:
+        order = grp.instance(0).key_info(k)[2]
+        want = np.zeros(ln, np.uint8)
+        port.sum_n(want, [host[w].view(torch.uint8)[o:o + ln].numpy() for w in order], ln,
+                   DType.FLOAT32)
+        for w in range(N):
+            assert np.array_equal(outs[w][o:o + ln].numpy(), want), (k, w)
+    grp.close()
 
 
 def _lr_rank(rank, world, port, q):

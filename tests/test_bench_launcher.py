@@ -40,6 +40,9 @@ def test_launcher_one_line_n_ranks(n):
     assert "NOT a measurement" in line["device"]
     pl = line["roofline"]["kernel_ms_blocks"]   # median and min
     assert 0 < pl["min"] <= pl["median"] <= pl["max"] and pl["blocks"] == 5
+    # the config-1 server-group object is in every line (it needs the GPU: on
+    # the CPU self-test it says so rather than disappearing)
+    assert "skipped" in line["server_cfg1"]
     sc = line["scaling_cfg4"]
     assert sc["exact_vs_torch_fold"] is True
     assert len(sc["shard_elems"]) == n and sum(sc["shard_elems"]) == 10007

@@ -1316,3 +1316,172 @@ def test_blocking_device_calls_from_a_callback(port):
         assert np.array_equal(np.frombuffer(res["blocking"], np.uint8), want)
         assert srv.key_info(0)[0] == rnd
     srv.close()
+
+
+def test_order_after_orders_running_producer_without_host_wait():
+    """The Python entry orders the caller's producers with an event the
+    server's streams wait on (byteps_server_order_after), not a host stall: a
+    producer still running on the caller's stream (a long spin, then the
+    fill) is ordered before the pushes, which return while it still runs, and
+    the round folds the filled values."""
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 1 << 20
+    srv = PSServer(N)
+    dev = torch.device("cuda:0")
+    xs = [torch.zeros(n, device=dev) for _ in range(N)]
+    torch.cuda.synchronize()
+    for w in range(N):
+        srv.push(5, w, xs[w], dt)                       # init round
+    torch.cuda.synchronize()
+    torch.cuda._sleep(400_000_000)                      # ~0.2 s on the current stream
+    xs[0].fill_(1.5)
+    xs[1].fill_(2.25)
+    acks = threading.Semaphore(0)
+    for w in range(N):
+        srv.push_async(5, w, xs[w], dt, lambda k, ww, st: acks.release())
+    still_running = not torch.cuda.current_stream(dev).query()
+    out = torch.empty(n, device=dev)
+    srv.pull(5, out)
+    for _ in range(N):
+        assert acks.acquire(timeout=30)
+    assert still_running, "the pushes waited for the producer on the host"
+    assert torch.all(out == 3.75)
+    srv.close()
+
+
+def _ptr_copy(ptr, src):
+    from prophet_amd.reducer import GpuReducer
+    GpuReducer().copy(ptr, src, src.numel() * src.element_size())
+
+
+@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
+def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
+    """BPSR_SERVER_RELEASE=device: after the init round one keyed block queue
+    folds every key, a round's last push_ready stores the release word (no
+    launch) and copied rounds are released behind their copies.  8 worker
+    threads, keys arriving in a different random order per worker and round
+    (never block order), 3 rounds from the slots (push_ready) and 1 of device
+    pushes; pulls as device views, blocking device copies and host copies.
+    Every pull equals the oracle's left fold in the recorded arrival order;
+    one consumer launch per round, every round released on the device."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    N, R = 8, 4
+    sizes = [1, 7, 1000, 4096 + 5, 65_536 + 3, 300_001]        # elements per key
+    keys = list(range(40, 40 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=3)
+    from prophet_amd.reducer import GpuReducer
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    bar = threading.Barrier(N + 1)
+    errors, pulled = [], {}
+
+    def worker(w):
+        try:
+            rng = random.Random(500 + w)
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)             # init round
+            for r in range(1, R + 1):
+                order = list(range(len(keys)))
+                rng.shuffle(order)
+                for j in order:
+                    time.sleep(rng.random() * 0.0005)
+                    if r == 3:                                 # a round of copied pushes
+                        srv.push(keys[j], w, src[(w, r, j)], dt)
+                    else:                                      # the transport wrote the slot
+                        ptr = srv.recv_slot(keys[j], w)
+                        _ptr_copy(ptr, src[(w, r, j)])
+                        torch.cuda.synchronize()
+                        srv.push_ready(keys[j], w)
+                outs = []
+                for j, k in enumerate(keys):
+                    n = sizes[j] * es
+                    if w % 3 == 0:                             # zero-copy view of the store
+                        p, ln = srv.pull_device_view(k)
+                        assert ln == n
+                        o = torch.empty(n, dtype=torch.uint8, device=dev)
+                        GpuReducer().copy(o, p, n)
+                        torch.cuda.synchronize()
+                        outs.append(o.cpu().numpy())
+                    elif w % 3 == 1:
+                        o = torch.empty(n, dtype=torch.uint8, device=dev)
+                        srv.pull(k, o)
+                        outs.append(o.cpu().numpy())
+                    else:
+                        o = np.zeros(n, np.uint8)
+                        srv.pull(k, o)
+                        outs.append(o)
+                pulled[(w, r)] = outs
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    st0 = None
+    try:
+        for r in range(1, R + 1):
+            bar.wait(timeout=240)
+            assert not errors, errors
+            for j, k in enumerate(keys):
+                rounds, _, order = srv.key_info(k)
+                assert rounds == r and sorted(order) == list(range(N))
+                n = sizes[j] * es
+                want = np.zeros(n, np.uint8)
+                port.sum_n(want, [data(dt, sizes[j], w, r, j) for w in order], n, dt)
+                for w in range(N):
+                    assert_bytes_match(dt, pulled[(w, r)][j], want, nan_class_f32_f64=False,
+                                       what=f"r{r} key {k} w{w}")
+            if r == 1:
+                st0 = srv.stats()
+            bar.wait(timeout=120)
+    finally:
+        for t in ts:
+            t.join(timeout=60)
+    assert not errors, errors
+    st = srv.stats()
+    srv.close()
+    assert st["key_releases"] == R * len(keys)                  # every round on the device
+    assert st["consumer_launches"] == R                          # one launch per epoch
+    assert st["fold_launches"] - st0["fold_launches"] == 0      # no lane fold launches
+
+
+def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
+    """The keyed queue's contract: every key completes one round per epoch.  A
+    round in which one key is never pushed makes that epoch's consumer give up
+    after BPSR_SERVER_RELEASE_TIMEOUT_S: the key released in it fails with
+    ETIMEOUT (no stale data), the server turns device releases off, and the
+    late key's round then folds with a launch, exactly."""
+    from prophet_amd.reducer import ETIMEOUT, ReduceError
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    monkeypatch.setenv("BPSR_SERVER_RELEASE_TIMEOUT_S", "0.5")
+    dt, N, n = DType.FLOAT32, 2, 50_003
+    srv = PSServer(N)
+    for r in range(2):                                   # init round + round 1, both keys
+        for k in (1, 2):
+            for w in range(N):
+                srv.push(k, w, data(dt, n, w, r, k), dt)
+    out = np.zeros(n * 4, np.uint8)
+    for k in (1, 2):
+        for w in range(N):
+            srv.pull(k, out)
+    for w in range(N):                                   # round 2: key 1 only
+        srv.push(1, w, data(dt, n, w, 2, 1), dt)
+    with pytest.raises(ReduceError) as e:
+        srv.pull(1, out)
+    assert e.value.code == ETIMEOUT
+    for w in range(N):                                   # key 2's round 2, late: a launch
+        srv.push(2, w, data(dt, n, w, 2, 2), dt)
+    srv.pull(2, out)
+    want = np.zeros(n * 4, np.uint8)
+    port.sum_n(want, [data(dt, n, w, 2, 2) for w in srv.key_info(2)[2]], n * 4, dt)
+    assert np.array_equal(out, want)
+    assert srv.stats()["consumer_launches"] == 2
+    srv.close()
