@@ -1330,8 +1330,8 @@ def test_order_after_orders_running_producer_without_host_wait():
     dev = torch.device("cuda:0")
     xs = [torch.zeros(n, device=dev) for _ in range(N)]
     torch.cuda.synchronize()
-    for w in range(N):
-        srv.push(5, w, xs[w], dt)                       # init round
+    srv.push_async(5, 0, xs[0], dt)                     # init round (answered when all are in)
+    srv.push(5, 1, xs[1], dt)
     torch.cuda.synchronize()
     torch.cuda._sleep(400_000_000)                      # ~0.2 s on the current stream
     xs[0].fill_(1.5)
@@ -1465,9 +1465,13 @@ def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     dt, N, n = DType.FLOAT32, 2, 50_003
     srv = PSServer(N)
     for r in range(2):                                   # init round + round 1, both keys
-        for k in (1, 2):
-            for w in range(N):
-                srv.push(k, w, data(dt, n, w, r, k), dt)
+        for k in (1, 2):                                 # (an init push waits for the others)
+            ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, n, w, r, k), dt))
+                  for w in range(N)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(timeout=60)
     out = np.zeros(n * 4, np.uint8)
     for k in (1, 2):
         for w in range(N):
