@@ -768,13 +768,15 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     hash — server.cc:339-400 runs one server per process) serving one
     cfg1-shaped bucket: 2 workers' 64 MiB fp32 gradients as the 17 BytePS
     partitions of 4,096,000 B (operations.cc:99-136, declared key = rank), in
-    pinned host memory as ps-lite's receive buffers would be.  A round: every
-    worker thread pushes its 17 partitions (byteps_server_group_push_many: H2D
-    into the receive slots, the fold on the lane issuers) and pulls the 17
-    merged partitions back into pinned host memory
-    (byteps_server_group_pull_many: the instances' copy kernels write the
-    pinned pages over PCIe).  Weak scaling: at N GPUs, N buckets over N PCIe
-    links.  Node rate = all ranks' pushed bytes / the slowest rank's median
+    pinned host memory as ps-lite's receive buffers would be.  A round, in
+    BytePS's worker loop shape (core_loops.cc:492-564: a push loop and a pull
+    loop per worker): each worker's push thread pushes its 17 partitions
+    (byteps_server_group_push: H2D into the receive slots, the fold on the
+    lane issuers) and its pull thread pulls each partition back into pinned
+    host memory as soon as that partition's push returned
+    (byteps_server_group_pull), so the D2H of partition k overlaps the H2D of
+    partition k + 1 (PCIe is full duplex).  Weak scaling: at N GPUs, N buckets
+    over N PCIe links.  Node rate = all ranks' pushed bytes / the slowest rank's median
     round.  PCIe-inclusive; compare with ``cpu_baseline`` (the reference's
     host-core round).  Exactness: every worker's pull equals torch's sum of the
     two pushes (fp32, two operands: the left fold in either arrival order)."""
@@ -801,14 +803,30 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     errors = []
 
     def rnd(init=False):
-        def worker(w):
+        pushed = [[threading.Event() for _ in parts] for _ in range(n_workers)]
+
+        def pusher(w):
             try:
-                grp.push_many(keys, w, srcs[w], DType.FLOAT32)
-                if not init:
-                    grp.pull_many(keys, dsts[w])
+                for i, k in enumerate(keys):
+                    grp.push(k, w, srcs[w][i], DType.FLOAT32)
+                    pushed[w][i].set()
             except Exception as e:  # noqa: BLE001 — reported below
                 errors.append(repr(e))
-        ts = [threading.Thread(target=worker, args=(w,)) for w in range(n_workers)]
+                for ev in pushed[w]:
+                    ev.set()
+
+        def puller(w):
+            try:
+                for i, k in enumerate(keys):
+                    pushed[w][i].wait()
+                    if errors:
+                        return
+                    grp.pull(k, dsts[w][i])
+            except Exception as e:  # noqa: BLE001 — reported below
+                errors.append(repr(e))
+        ts = [threading.Thread(target=pusher, args=(w,)) for w in range(n_workers)]
+        if not init:
+            ts += [threading.Thread(target=puller, args=(w,)) for w in range(n_workers)]
         for t in ts:
             t.start()
         for t in ts:
@@ -834,8 +852,8 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     total = world * n_workers * bucket_bytes
     return {"workload": (f"config 1 per GPU: {n_workers} workers x {bucket_bytes >> 20} MiB fp32 "
                          f"as {len(parts)} partitions in pinned host memory, one PS server "
-                         f"(byteps_server_group_*, one instance, djb2 hash) per GPU, "
-                         f"push_many + pull_many per worker thread, {world} GPU(s) / PCIe links"),
+                         f"(byteps_server_group_*, one instance, djb2 hash) per GPU, a push "
+                         f"thread and a pull thread per worker, {world} GPU(s) / PCIe links"),
             "node_GiBps": round(total / t / GIB, 2),
             "per_gpu_GiBps": round(n_workers * bucket_bytes / t / GIB, 2),
             "round_ms": round(t * 1e3, 3), "rounds": rounds, "lanes": lanes,

@@ -89,7 +89,12 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * (default 5) seconds makes that epoch's consumer give up: the keys released
  * in it fail with BYTEPS_REDUCE_ETIMEOUT and the server goes back to launches
  * for good.  Keys declared after the queue was built, and keys of another
- * dtype, always use launches. */
+ * dtype, always use launches.  While an epoch is in progress its consumer
+ * waits on the device for the releases, on a hardware queue of its own: a
+ * thread that still has to push must not wait for the whole device
+ * (hipDeviceSynchronize, hipFree), nor put work on the legacy NULL stream
+ * (it waits for every blocking stream, the consumer's included) — work on
+ * non-blocking streams, and stream or event syncs, are fine. */
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
 int byteps_server_destroy(byteps_server* s);
 

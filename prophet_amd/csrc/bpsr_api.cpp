@@ -847,6 +847,7 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.keyed = 0;
   Q.kwords = nullptr;
   Q.khwords = nullptr;
+  Q.herr = nullptr;
   const Tuning tu = tuning_for_n(q->ti.nmax);
   const bool gated = q->occ == 0;
   size_t lds;
@@ -1115,7 +1116,8 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   Q.L.stop = stop;
   Q.flags = q->flags;
   Q.block_first = q->flags + q->nblocks;
-  Q.ctl = q->hctl_dev;
+  Q.ctl = q->ctl;                // polled on the device (agent scope)
+  Q.herr = &q->hctl_dev->err;    // mirrored to the host by the helper
   Q.nblocks = (uint32_t)q->nblocks;
   Q.timeout_ticks = (uint64_t)(q->timeout_s * 1e3 * (double)q->clock_khz);
   Q.epoch = ep;
@@ -1125,13 +1127,14 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   Q.kwords = q->kwords;
   Q.khwords = q->khwords_dev;
   Q.grid = q->ti.tiles + 1;
-  // residency capped as for the gated consumer: tiles waiting for a key's
-  // last push never take a CU's last registers (copies must still run)
+  // Residency: at most 2 consumer workgroups per CU, and room left beside
+  // them for the work a missing release may still need — a push copy into a
+  // slot (the copy kernel asks for 40 KiB of LDS) or a release kernel: 58 KiB
+  // each (two fit in 160 KiB, three do not; 44 KiB stay free).
   const Tuning tu = tuning_for_n(q->ti.nmax);
-  int occ = launch_occ(tu, q->ti.tiles, true);
-  if (occ == 0 || occ > q->gate_occ) occ = q->gate_occ;
+  constexpr size_t kKeyedLds = 58u * 1024u;
   e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16),
-                    occ_lds_bytes(occ), true, q->dtype, q->mode, own);
+                    kKeyedLds, true, q->dtype, q->mode, own);
   if (e != hipSuccess) return hip_fail(e, "keyed queue launch");
   q->launch_epoch = ep;
   if (stream) *stream = own;
@@ -1165,6 +1168,31 @@ int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s)
 
 bool keyq_failed(byteps_reduce_blockq* q) {
   return __atomic_load_n(&q->hctl->err, __ATOMIC_ACQUIRE) != 0;
+}
+
+std::string keyq_debug(byteps_reduce_blockq* q) {
+  std::lock_guard<std::mutex> g(q->mu);
+  std::vector<uint64_t> dev((size_t)q->nblocks);
+  const hipError_t e = hipMemcpy(dev.data(), q->kwords, dev.size() * 8, hipMemcpyDeviceToHost);
+  char buf[512];
+  int dev_at = 0, rel_at = 0, host_at = 0;
+  const uint32_t ep = q->launch_epoch;
+  int first_missing = -1;
+  for (int b = 0; b < q->nblocks; ++b) {
+    if ((uint32_t)dev[(size_t)b] == ep) ++dev_at;
+    else if (first_missing < 0) first_missing = b;
+    if (q->rel_epoch[(size_t)b] >= ep) ++rel_at;
+    const uint64_t h = __atomic_load_n(q->khwords + 2 * (size_t)b + (ep & 1u), __ATOMIC_ACQUIRE);
+    if ((uint32_t)h == ep) ++host_at;
+  }
+  snprintf(buf, sizeof(buf),
+           "keyq: launch epoch %u, %d blocks: device words at epoch %d, host releases %d, "
+           "host words %d, err %u, copy %d, first missing block %d (device word %llx host %llx)",
+           ep, q->nblocks, dev_at, rel_at, host_at, q->hctl->err, (int)e, first_missing,
+           first_missing >= 0 ? (unsigned long long)dev[(size_t)first_missing] : 0ull,
+           first_missing >= 0 ? (unsigned long long)q->khwords[2 * (size_t)first_missing + (ep & 1u)]
+                              : 0ull);
+  return buf;
 }
 
 }  // namespace bpsr

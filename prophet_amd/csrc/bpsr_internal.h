@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <string>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -121,6 +122,7 @@ struct BlockqLaunch {
   uint32_t keyed;
   uint64_t* kwords;          // device words, one per block (helper / stream releases write them)
   const uint64_t* khwords;   // host words (device view), two per block by epoch parity
+  uint32_t* herr;            // host word (device view): the helper mirrors ctl->err there
 };
 // Arrival order of a keyed block: position m's source is worker
 // (perm >> 4m) & 7 (at most 8 sources); kKeySkip: the round is folded
@@ -295,5 +297,6 @@ uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
 uint32_t keyq_launched(struct byteps_reduce_blockq* q);
 int keyq_release(struct byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s);
 bool keyq_failed(struct byteps_reduce_blockq* q);
+std::string keyq_debug(struct byteps_reduce_blockq* q);  // state summary (synchronous copy)
 
 }  // namespace bpsr

@@ -78,9 +78,12 @@ constexpr int cmin(int a, int b) { return a < b ? a : b; }
 // through an empty asm so the compiler cannot merge these loads with the fast
 // path's (merging drops the loads' non-temporal hint and reorders the fast
 // path's load stream around the first adds).
-template <class Op, bool NT>
-__device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* srcs, int n,
-                                                   uint64_t off) {
+// XS: anything indexable as srcs[k] -> source pointer (a pointer array, or the
+// keyed consumer's arrival-order view of one, PermSrcs).
+using SrcPtrs = const unsigned char* const*;
+
+template <class Op, bool NT, class XS = SrcPtrs>
+__device__ __forceinline__ vec16 fold_vector_exact(const XS& srcs, int n, uint64_t off) {
   auto opaque = [](const unsigned char* p) {
     asm volatile("" : "+v"(p));
     return p;
@@ -103,9 +106,9 @@ __device__ __forceinline__ vec16 fold_vector_exact(const unsigned char* const* s
 // NS > 0: exactly NS sources; NS < 0: at most -NS (<= 8) sources, n at run
 // time, one load group with compile-time indices (so `srcs` may be a register
 // array); NS == 0: any n.  `xsrcs` (memory) serves the exact NaN replay.
-template <class Op, int VPT, int NT, int NS, bool GUARD>
+template <class Op, int VPT, int NT, int NS, bool GUARD, class XS = SrcPtrs>
 __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
-                                               const unsigned char* const* xsrcs, int n,
+                                               const XS& xsrcs, int n,
                                                unsigned char* dst, uint64_t vec_off,
                                                uint64_t v0, uint64_t nvec, int lane) {
   constexpr int NSA = NS < 0 ? -NS : NS;
@@ -154,7 +157,7 @@ __device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
     vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (valid[j] && Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, (NT != 0)>(xsrcs, ns, off0 + j * kStep);
+        out = fold_vector_exact<Op, (NT != 0), XS>(xsrcs, ns, off0 + j * kStep);
     }
     if (valid[j]) st16<(NT != 0)>(dst + off0 + j * kStep, out);
   }
@@ -171,9 +174,9 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <class Op, int VPT, int NT, int NS, class Mid = NoMid>
+template <class Op, int VPT, int NT, int NS, class Mid = NoMid, class XS = SrcPtrs>
 __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs,
-                                                   const unsigned char* const* xsrcs, int n,
+                                                   const XS& xsrcs, int n,
                                                    unsigned char* dst, uint64_t byte0, int lane,
                                                    const Mid& mid = Mid()) {
   constexpr int kAux = NT ? 2 : 0;               // loads: 2 = nt
@@ -229,7 +232,7 @@ __device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* s
     vec16 out = Op::finish_fast(acc[j]);
     if (__builtin_expect(bad, 0)) {
       if (Op::has_nan(acc[j]))
-        out = fold_vector_exact<Op, (NT != 0)>(xsrcs, ns, byte0 + voff + j * kBlock * 16);
+        out = fold_vector_exact<Op, (NT != 0), XS>(xsrcs, ns, byte0 + voff + j * kBlock * 16);
     }
     __builtin_amdgcn_raw_buffer_store_b128(bitcast<u4>(out), rd, voff + j * kBlock * 16, 0, kStAux);
   }
@@ -248,8 +251,8 @@ __device__ __forceinline__ void fold_tile(const unsigned char* const* srcs, int 
 // Element part: elements [0, head) and [tail_begin, n_elems) plus trailing
 // bytes; elements >= tail_sem_from get the F16C-tail NaN rule (fp16 only).
 // Each element's N loads are issued together (groups of 8) before the fold.
-template <class Op>
-__device__ __forceinline__ void fold_elements(const unsigned char* const* srcs, int n,
+template <class Op, class XS = SrcPtrs>
+__device__ __forceinline__ void fold_elements(const XS& srcs, int n,
                                               unsigned char* dst, const FoldGeom& g,
                                               bool aligned, uint64_t t, uint64_t stride) {
   using E = typename Op::E;
@@ -650,6 +653,14 @@ __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
 __device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// The device words are written on this agent only (the helper, a stream
+// release kernel): agent-scope polls are served by the L2, not HBM.
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_err(const BlockqLaunch& Q) {
+  return __hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Workgroup 0: forward the host-written words of this launch's epoch (the
 // epoch's parity slot) into the device words, until every block holds this
@@ -664,37 +675,41 @@ __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
     bool pending = false;
     for (uint32_t base = 0; base < Q.nblocks; base += 64) {
       const uint32_t b = base + lane;
-      if (b < Q.nblocks && (uint32_t)ld_sys64(Q.kwords + b) != Q.epoch) {
+      if (b < Q.nblocks && (uint32_t)ld_agent64(Q.kwords + b) != Q.epoch) {
         const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);
+        // relaxed: the word publishes no data of this workgroup (the round's
+        // data landed before the host's store), and a release at system
+        // scope would write back the XCD's whole L2 — once per key, while the
+        // consumer's own stores fill it (measured: the epoch's consumer took
+        // 0.49 ms instead of ~0.1 for config 3's 165 keys)
         if ((uint32_t)h == Q.epoch)
-          __hip_atomic_store(Q.kwords + b, h, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(Q.kwords + b, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
           pending = true;
       }
     }
     if (__ballot(pending) == 0) return;
-    if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
-    if (wall_clock64() - t0 > Q.timeout_ticks) {
-      if (lane == 0) __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // a tile gave up, or this wave does: the host reads the mirror word
+    const bool late = wall_clock64() - t0 > Q.timeout_ticks;
+    if (late || ld_err(Q)) {
+      if (lane == 0) {
+        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(Q.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return;
     }
     __builtin_amdgcn_s_sleep(2);
   }
 }
 
-// The record's sources in arrival order: position m <- worker (perm >> 4m) & 7
-// (wave-uniform selects, no indexing).
-__device__ __forceinline__ void permute_srcs(const unsigned char* const (&p)[8], uint32_t perm,
-                                             const unsigned char* (&q)[8]) {
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const uint32_t w = (perm >> (4 * m)) & 7u;
-    const unsigned char* v = p[0];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) v = w == (uint32_t)k ? p[k] : v;
-    q[m] = v;
+// A pointer array seen in arrival order: position k is worker (perm >> 4k) & 7.
+struct PermSrcs {
+  const unsigned char* const* m;
+  uint32_t perm;
+  __device__ __forceinline__ const unsigned char* operator[](int k) const {
+    return m[(perm >> (4 * k)) & 7u];
   }
-}
+};
 
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
@@ -707,42 +722,54 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
   const RecRegs r = load_record(rec);
   const uint32_t blk = reinterpret_cast<const TileHead*>(rec)->block;
   const uint32_t pf = prefetch_record(Q.L, t);
-  uint64_t w = ld_sys64(Q.kwords + blk);
+  uint64_t w = ld_agent64(Q.kwords + blk);
   if ((uint32_t)w != Q.epoch) {
     const uint64_t t0 = wall_clock64();
     for (;;) {
-      __builtin_amdgcn_s_sleep(4);
-      w = ld_sys64(Q.kwords + blk);
+      __builtin_amdgcn_s_sleep(8);
+      w = ld_agent64(Q.kwords + blk);
       if ((uint32_t)w == Q.epoch) break;
-      if (__hip_atomic_load(&Q.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+      if (ld_err(Q)) return;
       if (wall_clock64() - t0 > Q.timeout_ticks) {
-        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
     }
+    // the word was raised after the round's data landed (a host store after
+    // the last push, or a stream release behind the copies); no workgroup of
+    // this launch has read those lines (keys do not share lines), so an
+    // agent-scope acquire for the tile's loads suffices — a system-scope one
+    // per waiting tile would invalidate the XCD's L2 each time
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
-  // the word was written after the round's data landed (host store after
-  // the last push, or a stream release behind the copies): acquire before
-  // the tile's loads
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const uint32_t perm = (uint32_t)(w >> 32);
   if (perm == kKeySkip) {
     keep_prefetch(pf);
     return;
   }
-  RecRegs rp = r;
-  permute_srcs(r.p, perm, rp.p);
+  // fast path: the 8 pointers permuted in registers (selects); element work
+  // and the NaN replay index the pointer arrays in memory through the order
+  // (no per-lane array, so no scratch)
+  const unsigned char* q[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const uint32_t wk = (perm >> (4 * m)) & 7u;
+    const unsigned char* v = r.p[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) v = wk == (uint32_t)k ? r.p[k] : v;
+    q[m] = v;
+  }
+  const PermSrcs xs{reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes), perm};
   if (r.kind == kTileElem) {
     const BatchEntry& e = Q.L.entries[r.b];
-    const unsigned char* es[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) es[m] = e.srcs[(perm >> (4 * m)) & 7u];
-    fold_elements<Op>(es, e.n, e.dst, e.g, e.aligned != 0,
-                      (uint64_t)r.a * kBlock + threadIdx.x, (uint64_t)r.c * kBlock);
+    fold_elements<Op, PermSrcs>(PermSrcs{e.srcs, perm}, e.n, e.dst, e.g, e.aligned != 0,
+                                (uint64_t)r.a * kBlock + threadIdx.x, (uint64_t)r.c * kBlock);
   } else if (r.kind == kTileFull) {
-    fold_tile_full_buf<Op, VPT, NT, -8>(rp.p, rp.p, (int)r.n, r.dst, 0, threadIdx.x);
+    fold_tile_full_buf<Op, VPT, NT, -8, NoMid, PermSrcs>(q, xs, (int)r.n, r.dst, 0,
+                                                         threadIdx.x);
   } else {
-    fold_tile_body<Op, VPT, NT, -8, true>(rp.p, rp.p, (int)r.n, r.dst, 0, 0, r.a, threadIdx.x);
+    fold_tile_body<Op, VPT, NT, -8, true, PermSrcs>(q, xs, (int)r.n, r.dst, 0, 0, r.a,
+                                                     threadIdx.x);
   }
   keep_prefetch(pf);
 }

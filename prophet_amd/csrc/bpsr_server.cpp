@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -403,8 +404,23 @@ void completer_main(byteps_server* s, Lane* Lp) {
     const Lane::Tracked t = L.cq.front();
     const uint64_t seq = t.seq;
     lk.unlock();
-    (void)hipEventSynchronize(t.ev);  // a failed launch failed its keys already
-    if (t.kq_epoch) kq_epoch_done(s, t.kq_epoch, t.seq);
+    if (t.kq_epoch) {
+      // a keyed consumer: every pull and view of its epoch waits for this,
+      // so poll its event (no other thread makes HIP calls on the device-
+      // release path) for up to 2 ms before a blocking wait — a blocking
+      // event wait wakes tens of microseconds late
+      const auto p0 = std::chrono::steady_clock::now();
+      while (hipEventQuery(t.ev) == hipErrorNotReady) {
+        if (std::chrono::steady_clock::now() - p0 > std::chrono::milliseconds(2)) {
+          (void)hipEventSynchronize(t.ev);
+          break;
+        }
+        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+      }
+      kq_epoch_done(s, t.kq_epoch, t.seq);
+    } else {
+      (void)hipEventSynchronize(t.ev);  // a failed launch failed its keys already
+    }
     lk.lock();
     L.cq.pop_front();
     L.done_seq = seq;
@@ -872,6 +888,8 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
   {
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (s->kq && keyq_failed(s->kq)) {
+      if (getenv("BPSR_SERVER_RELEASE_DEBUG"))
+        fprintf(stderr, "bpsr server: epoch %u timed out: %s\n", epoch, keyq_debug(s->kq).c_str());
       s->kq_off.store(true);
       for (KeyState* k : s->kq_keys)
         if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
@@ -911,7 +929,9 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
 // Blocking readers of a keyed round's store wait for its epoch to be
 // published (caller holds no lock); then the key's error, if it failed.
 void wait_published(byteps_server* s, KeyState* ks, uint64_t seq) {
+  (void)ks;
   Lane& K = *s->klane;
+  if (K.done_pub.load(std::memory_order_acquire) >= seq) return;
   std::unique_lock<std::mutex> dl(K.done_mu);
   K.done_cv.wait(dl, [&] { return K.done_seq >= seq; });
 }
@@ -2071,8 +2091,10 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   lk.unlock();
   if (need) {  // tracked by a completer (the lane's, or the keyed one): no HIP call here
     Lane& L = fl < 0 ? *s->klane : *s->lanes[fl];
-    std::unique_lock<std::mutex> dl(L.done_mu);
-    L.done_cv.wait(dl, [&] { return L.done_seq >= need; });
+    if (L.done_pub.load(std::memory_order_acquire) < need) {  // else: no lock at all
+      std::unique_lock<std::mutex> dl(L.done_mu);
+      L.done_cv.wait(dl, [&] { return L.done_seq >= need; });
+    }
   } else if (has) {
     hipError_t e = hipEventSynchronize(ev);
     if (e != hipSuccess) return hip_fail(e, "store fold sync");

@@ -1376,10 +1376,14 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
            for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
     torch.cuda.synchronize()
+    # the workers' device work goes on non-blocking streams: the legacy NULL
+    # stream would wait for the epoch's consumer, which waits for the workers
+    streams = [torch.cuda.Stream(device=dev) for _ in range(N)]
     bar = threading.Barrier(N + 1)
     errors, pulled = [], {}
 
     def worker(w):
+        torch.cuda.set_stream(streams[w])
         try:
             rng = random.Random(500 + w)
             for j, k in enumerate(keys):
@@ -1392,9 +1396,13 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
                     if r == 3:                                 # a round of copied pushes
                         srv.push(keys[j], w, src[(w, r, j)], dt)
                     else:                                      # the transport wrote the slot
+                        # (a stream sync, never a device-wide one: the epoch's
+                        # consumer is running and waits for this thread's releases)
                         ptr = srv.recv_slot(keys[j], w)
-                        _ptr_copy(ptr, src[(w, r, j)])
-                        torch.cuda.synchronize()
+                        st = torch.cuda.current_stream(dev)
+                        x = src[(w, r, j)]
+                        GpuReducer().copy(ptr, x, x.numel() * x.element_size(), stream=st)
+                        st.synchronize()
                         srv.push_ready(keys[j], w)
                 outs = []
                 for j, k in enumerate(keys):
@@ -1404,7 +1412,7 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
                         assert ln == n
                         o = torch.empty(n, dtype=torch.uint8, device=dev)
                         GpuReducer().copy(o, p, n)
-                        torch.cuda.synchronize()
+                        torch.cuda.current_stream(dev).synchronize()
                         outs.append(o.cpu().numpy())
                     elif w % 3 == 1:
                         o = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -1427,7 +1435,10 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     st0 = None
     try:
         for r in range(1, R + 1):
-            bar.wait(timeout=240)
+            try:
+                bar.wait(timeout=240)
+            except threading.BrokenBarrierError:
+                raise AssertionError(f"a worker failed: {errors}")
             assert not errors, errors
             for j, k in enumerate(keys):
                 rounds, _, order = srv.key_info(k)
