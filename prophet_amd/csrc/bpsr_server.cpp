@@ -137,6 +137,7 @@ struct PullJob {
   size_t len = 0;
   Response resp;
   SyncWait* direct = nullptr;
+  uint64_t kseq = 0;  // parked on a keyed epoch: the keyed completer's seq it waits for
 };
 
 // A non-blocking push of device data whose copy into its slot waits for the
@@ -670,6 +671,7 @@ void queue_pull_copies(byteps_server* s, KeyState* ks, const KeyState::WaitingCo
     j.resp.ctx = wc.ctx;
     j.resp.view = static_cast<const char*>(wc.view);
     j.resp.len = wc.len;
+    j.kseq = park ? ks->fold_seq : 0;
     if (park) s->kq_parked.push_back(j);
     else L.pulls.push_back(j);
   }
@@ -895,7 +897,7 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
         if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
     }
     s->kq_done_seq = seq;
-    for (PullJob& j : s->kq_parked) (j.ks->fold_seq <= seq ? go : keep).push_back(j);
+    for (PullJob& j : s->kq_parked) (j.kseq <= seq ? go : keep).push_back(j);
     s->kq_parked.swap(keep);
   }
   for (KeyState* k : failed) {

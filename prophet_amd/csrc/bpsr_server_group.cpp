@@ -231,12 +231,23 @@ struct PushPiece {
   uint64_t key;
   const void* data;
   size_t len;
+  bool split;  // one piece of a range-split key (stamped)
   int pos;
 };
-int scatter_pushes(byteps_server_group* g, const std::vector<PushPiece>& pcs, int worker,
-                   int dtype, int location) {
+int scatter_pushes(byteps_server_group* g, std::vector<PushPiece>& pcs, int worker, int dtype,
+                   int location) {
   for (const PushPiece& p : pcs)
     if (int rc = bpsr::server_check_key(p.s, p.key, p.len, dtype)) return rc;
+  // stamped only once every piece passed (a refused push takes no position):
+  // one position per split key, shared by its consecutive pieces
+  for (size_t i = 0; i < pcs.size(); ++i) {
+    if (!pcs[i].split) continue;
+    if (i > 0 && pcs[i - 1].split && pcs[i - 1].key == pcs[i].key) {
+      pcs[i].pos = pcs[i - 1].pos;
+      continue;
+    }
+    pcs[i].pos = stamp(g, pcs[i].key, worker);
+  }
   Acks acks;
   int rc = 0;
   size_t queued = 0;
@@ -460,9 +471,8 @@ int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, c
         return rc;
     return BYTEPS_REDUCE_OK;
   }
-  const int pos = stamp(g, key, worker);
   std::vector<PushPiece> pcs;
-  for (const Piece& p : ps) pcs.push_back({g->inst[p.server], key, d + p.off, p.len, pos});
+  for (const Piece& p : ps) pcs.push_back({g->inst[p.server], key, d + p.off, p.len, true, -1});
   return scatter_pushes(g, pcs, worker, dtype, location);
 }
 
@@ -527,10 +537,9 @@ int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
   std::vector<PushPiece> pcs;
   for (int i = 0; i < n; ++i) {
     route(g, keys[i], lens[i], &ps);
-    const int pos = ps.size() > 1 ? stamp(g, keys[i], worker) : -1;
     for (const Piece& p : ps)
       pcs.push_back({g->inst[p.server], keys[i], static_cast<const char*>(datas[i]) + p.off,
-                     p.len, pos});
+                     p.len, ps.size() > 1, -1});
   }
   return scatter_pushes(g, pcs, worker, dtype, location);
 }
