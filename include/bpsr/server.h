@@ -232,7 +232,9 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
  * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
  * push-copy launches, out[6] keyed consumer launches and out[7] rounds
- * released on the device (BPSR_SERVER_RELEASE=device); the first n (<= 8). */
+ * released on the device (BPSR_SERVER_RELEASE=device), out[8] blocking pulls
+ * served by the pull copy service and out[9] that service's kernel launches;
+ * the first n (<= 10). */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

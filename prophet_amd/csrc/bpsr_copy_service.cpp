@@ -1,0 +1,266 @@
+// The pull copy service's host side (kernel: bpsr_k_service.hip).
+//
+// A blocking pull into device memory used to ride a lane launch: the pull
+// thread handed its copy to the lane issuer, the issuer launched it, the
+// lane's completer saw the launch finish and woke the thread — two thread
+// hand-offs and a HIP launch per pull, about 50 us per pull at best, which a
+// worker pulling 160 keys one after another pays 160 times.
+// Here the pull thread writes one tagged 32-B job into a pinned ring and
+// spins on the job's done word: the persistent service kernel
+// picks the job up within a few microseconds, copies it, makes the bytes
+// visible device-wide and stores the done word.  No HIP call on that path.
+//
+// The kernel runs on a non-blocking high-priority stream: a hardware queue of
+// its own (the runtime shares only normal-priority queues between streams), so
+// it never holds back work queued on the process's shared queues, and no
+// implicit synchronisation with the legacy NULL stream, so PyTorch's default
+// stream does not wait for a running service (a CU-masked stream would have
+// its own queue but is a blocking stream: DESIGN.md §9).  It exits by
+// itself after kIdleUs without a job or kMaxMs of age, and is relaunched by
+// the next poster that finds it gone; a job stranded by an exit (posted just
+// as the leader decided to stop) is served by the relaunch, which starts at
+// the oldest job still pending and skips jobs already done.  A relaunch
+// happens only after the old launch has completed, so no job is copied by two
+// launches at once (a late second copy could overwrite a buffer its caller
+// already reuses).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "bpsr_error.h"
+#include "bpsr_internal.h"
+
+namespace bpsr {
+
+namespace {
+constexpr uint32_t kSvcWgs = 65;             // workgroups per launch: the fetcher + 64 copiers
+constexpr size_t kChunk = 64 << 10;          // one job's bytes at most (a large copy spreads)
+// A launch's idle exit (short: a device-wide synchronisation waits for a
+// running service; a pull burst keeps it alive) and its age limit.
+constexpr int kIdleUs = 500, kMaxMs = 2000;
+constexpr int kCheckUs = 200;                // a waiter's liveness check period
+constexpr int kTimeoutMs = 10000;            // a job's give-up (reported, not retried)
+}  // namespace
+
+struct CopyService {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev = nullptr;       // the current launch's completion
+  SvcJob* ring = nullptr;        // pinned host
+  uint64_t* done = nullptr;      // pinned host, one 64-B line per slot (kDoneStride words)
+  uint32_t* stop = nullptr;      // pinned host
+  SvcJob* ring_d = nullptr;      // their device views
+  uint64_t* done_d = nullptr;
+  uint32_t* stop_d = nullptr;
+  uint64_t* dev = nullptr;       // device words of the kernel
+  SvcJob* dring = nullptr;       // device ring
+  uint64_t* trace = nullptr;     // probes only
+  uint64_t idle_ticks = 0, max_ticks = 0;
+  // Posting is lock-free (a job index from `posted`, then the slot's words);
+  // `mu` serialises only launches and liveness checks.
+  std::atomic<uint64_t> posted{0};      // job indices handed out
+  std::atomic<int64_t> last_post_ns{0};
+  std::atomic<bool> running{false};     // written under mu
+  std::atomic<bool> broken{false};      // a job timed out: the service is off for good
+  std::mutex mu;
+  uint64_t scan_from = 0;               // under mu: every job below is done
+  std::atomic<uint64_t> launches{0};
+};
+
+namespace {
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// A slot's done word only grows (its next job is posted after this one is
+// done), so a later job's value also says this one is done.
+bool job_done(const CopyService* c, uint64_t j) {
+  return __atomic_load_n(&c->done[(j % kSvcRing) * kDoneStride], __ATOMIC_ACQUIRE) >= j + 1;
+}
+
+// With mu held: a launch is serving unless its event says it is gone.
+bool svc_alive(CopyService* c) {
+  if (!c->running.load()) return false;
+  if (hipEventQuery(c->ev) == hipSuccess) c->running.store(false);
+  return c->running.load();
+}
+
+// With mu held: start a launch at the oldest job not done (jobs handed out
+// but not yet written count as not done: the fetcher waits for them).
+int svc_launch(CopyService* c) {
+  if (c->running.load()) {  // let the old launch finish first (it is stopping)
+    hipError_t e = hipEventSynchronize(c->ev);
+    if (e != hipSuccess) return hip_fail(e, "copy service: old launch");
+    c->running.store(false);
+  }
+  const uint64_t posted = c->posted.load();
+  uint64_t start = c->scan_from;
+  while (start < posted && job_done(c, start)) ++start;
+  c->scan_from = start;
+  SvcArgs a{};
+  a.ring = c->ring_d;
+  a.done = c->done_d;
+  a.stop = c->stop_d;
+  a.dev = c->dev;
+  a.dring = c->dring;
+  a.trace = c->trace;
+  a.start = start;
+  a.check_below = posted;
+  a.idle_ticks = c->idle_ticks;
+  a.max_ticks = c->max_ticks;
+  a.wgs = kSvcWgs;
+  hipError_t e = hipMemsetAsync(c->dev, 0, 4 * sizeof(uint64_t), c->stream);
+  if (e == hipSuccess) e = launch_copy_service(a, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(c->ev, c->stream);
+  if (e != hipSuccess) return hip_fail(e, "copy service launch");
+  c->running.store(true);
+  c->launches.fetch_add(1, std::memory_order_relaxed);
+  return 0;
+}
+
+}  // namespace
+
+int copysvc_create(int device, CopyService** out) {
+  *out = nullptr;
+  CopyService* c = new CopyService();
+  c->device = device;
+  int khz = 0;
+  hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  if (e != hipSuccess || khz <= 0) {
+    delete c;
+    return e != hipSuccess ? hip_fail(e, "wall clock rate")
+                           : fail(BYTEPS_REDUCE_EHIP, "copy service: no wall clock rate");
+  }
+  c->idle_ticks = (uint64_t)khz * kIdleUs / 1000;
+  c->max_ticks = (uint64_t)khz * kMaxMs;
+  int prio_lo = 0, prio_hi = 0;
+  e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (e == hipSuccess && prio_lo == prio_hi) {
+    delete c;
+    return fail(BYTEPS_REDUCE_EHIP, "copy service: no stream priorities (no queue of its own)");
+  }
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev, hipEventDisableTiming);
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->ring), sizeof(SvcJob) * kSvcRing, fl);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&c->done), sizeof(uint64_t) * kSvcRing * kDoneStride, fl);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->stop), 64, fl);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dev), 256);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dring), sizeof(SvcJob) * kSvcRing);
+  if (e == hipSuccess) e = hipMemset(c->dring, 0, sizeof(SvcJob) * kSvcRing);
+  if (e == hipSuccess) {
+    std::memset(c->ring, 0, sizeof(SvcJob) * kSvcRing);
+    std::memset(c->done, 0, sizeof(uint64_t) * kSvcRing * kDoneStride);
+    *c->stop = 0;
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ring_d), c->ring, 0);
+  }
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->done_d), c->done, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->stop_d), c->stop, 0);
+  if (e != hipSuccess) {
+    const int rc = hip_fail(e, "copy service setup");
+    copysvc_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+void copysvc_destroy(CopyService* c) {
+  if (!c) return;
+  if (c->stop) __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
+  if (c->running.load()) (void)hipEventSynchronize(c->ev);  // exits within one poll
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->ev) (void)hipEventDestroy(c->ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->ring) (void)hipHostFree(c->ring);
+  if (c->done) (void)hipHostFree(c->done);
+  if (c->stop) (void)hipHostFree(c->stop);
+  if (c->dev) (void)hipFree(c->dev);
+  if (c->dring) (void)hipFree(c->dring);
+  delete c;
+}
+
+// Waits for job j's done word: spin, then yield; every kCheckUs without it,
+// make sure a launch is serving.  0, or an error (the service then stays off).
+int wait_job(CopyService* c, uint64_t j, int64_t t0) {
+  int64_t t_check = now_ns();
+  for (;;) {
+    if (job_done(c, j)) return 0;
+    for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+    const int64_t now = now_ns();
+    if (now - t0 > 50'000) std::this_thread::yield();
+    if (now - t_check > kCheckUs * 1000ll) {
+      t_check = now;
+      std::lock_guard<std::mutex> g(c->mu);
+      if (job_done(c, j)) return 0;
+      if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+      if (!svc_alive(c)) {
+        const int rc = svc_launch(c);
+        if (rc) {
+          c->broken.store(true);
+          return rc;
+        }
+      }
+      if (now - t0 > kTimeoutMs * 1000000ll) {
+        c->broken.store(true);
+        __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
+        return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
+                    (unsigned long long)j, kTimeoutMs);
+      }
+    }
+  }
+}
+
+int copysvc_copy(CopyService* c, void* dst, const void* src, size_t len) {
+  if (len == 0) return 0;
+  if (((reinterpret_cast<uint64_t>(dst) + len) | (reinterpret_cast<uint64_t>(src) + len)) > kSvcMask)
+    return fail(BYTEPS_REDUCE_EARGS, "copy service: address beyond 48 bits");
+  if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+  const uint64_t n = (len + kChunk - 1) / kChunk;
+  const uint64_t first = c->posted.fetch_add(n);
+  const int64_t t0 = now_ns();
+  int rc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t j = first + i;
+    // the slot's previous job first (a ring's worth of jobs behind)
+    if (j >= kSvcRing && (rc = wait_job(c, j - kSvcRing, t0))) return rc;
+    SvcJob& r = c->ring[j % kSvcRing];
+    const size_t off = (size_t)i * kChunk;
+    const uint64_t tag = svc_tag(j) << 48;
+    __atomic_store_n(&r.w[0], (reinterpret_cast<uint64_t>(dst) + off) | tag, __ATOMIC_RELAXED);
+    __atomic_store_n(&r.w[1], (reinterpret_cast<uint64_t>(src) + off) | tag, __ATOMIC_RELAXED);
+    __atomic_store_n(&r.w[2], (uint64_t)std::min(kChunk, len - off) | tag, __ATOMIC_RELEASE);
+  }
+  // a launch idle for most of kIdleUs may be exiting: look after posting
+  const int64_t prev = c->last_post_ns.exchange(t0);
+  if (!c->running.load() || t0 - prev > kIdleUs * 500ll) {
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!svc_alive(c) && (rc = svc_launch(c))) {
+      c->broken.store(true);
+      return rc;
+    }
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if ((rc = wait_job(c, first + i, t0))) return rc;
+  return 0;
+}
+
+uint64_t copysvc_launches(CopyService* c) { return c ? c->launches.load() : 0; }
+
+uint64_t copysvc_posted(CopyService* c) { return c->posted.load(); }
+
+void copysvc_set_trace(CopyService* c, uint64_t* dev_trace) {
+  std::lock_guard<std::mutex> g(c->mu);
+  c->trace = dev_trace;
+}
+
+}  // namespace bpsr

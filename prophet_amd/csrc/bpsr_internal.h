@@ -280,6 +280,53 @@ int fold_any_alias(void* dst, const void* const* srcs, int n, size_t len, int dt
 hipError_t launch_copy(void* dst, const void* src, size_t len, const Tuning& tu,
                        hipStream_t s);
 
+// Pull copy service (bpsr_copy_service.cpp, kernel in bpsr_k_service.hip):
+// a persistent kernel of a few workgroups serving copies that host threads
+// post into a pinned job ring — a blocking pull's copy with no HIP call and
+// no thread hand-off on the caller's side.  Job j sits in slot j % kSvcRing
+// of the host ring; the launch's fetcher (workgroup 0) moves posted jobs into
+// the same slot of a device ring, where copier g (workgroups 1..wgs-1) finds
+// jobs start + g - 1, start + g - 1 + (wgs - 1), ...  Every descriptor word
+// carries the job's 16-bit tag in its top bits (addresses and lengths fit in
+// 48), so a reader that sees the tag in all three words has the whole job:
+// no separate publish word, no ordering between the words' stores.
+constexpr uint32_t kSvcRing = 4096;
+constexpr uint32_t kDoneStride = 8;  // done words one 64-B line apart (spinning host threads)
+constexpr uint64_t kSvcMask = (1ull << 48) - 1;
+struct SvcJob {      // 32 B: dst, src, len, each | tag << 48; one pad word
+  uint64_t w[4];
+};
+// 1..65535, never 0 (zeroed slots); one slot's successive jobs differ
+// (4096 and 65535 are coprime)
+__host__ __device__ inline uint64_t svc_tag(uint64_t job) { return job % 0xFFFFull + 1; }
+struct SvcArgs {
+  const SvcJob* ring;      // host ring (device view)
+  SvcJob* dring;           // device ring
+  uint64_t* done;          // host words: done[slot * kDoneStride] = job + 1 once the copy is visible
+  const uint32_t* stop;    // host word: nonzero = exit now
+  uint64_t* dev;           // device words: [1] jobs completed, [2] exit flag
+  uint64_t start;          // first job index of this launch
+  uint64_t check_below;    // jobs below this may be done already (a relaunch): look first
+  uint64_t idle_ticks;     // exit after this long without a new job ...
+  uint64_t max_ticks;      // ... or once this launch is this old (a relaunch takes over)
+  uint32_t wgs;            // fetcher + copiers
+  uint64_t* trace;         // probes only (null in the product): per slot, wall clock at
+                           // [0] fetched, [1] picked up, [2] copied and drained
+};
+hipError_t launch_copy_service(const SvcArgs& a, hipStream_t s);
+
+struct CopyService;
+int copysvc_create(int device, CopyService** out);
+// Blocking copy of len bytes (device memory to device memory) through the
+// service; returns once the bytes are visible to later work on the device.
+int copysvc_copy(CopyService* svc, void* dst, const void* src, size_t len);
+void copysvc_destroy(CopyService* svc);
+uint64_t copysvc_launches(CopyService* svc);  // kernel launches so far (0 for null)
+// Probes (tools/dbg/copysvc_probe.cpp): jobs posted so far; a device trace
+// buffer (kSvcRing * 4 words) used from the next launch on.
+uint64_t copysvc_posted(CopyService* svc);
+void copysvc_set_trace(CopyService* svc, uint64_t* dev_trace);
+
 // Keyed block queue (bpsr_api.cpp): the PS server's device releases.  One
 // block per key (bucket k: dst = the key's store, srcs = its receive slots in
 // WORKER order, n <= kKeyedMaxSrcs); launch k folds every key once, each tile

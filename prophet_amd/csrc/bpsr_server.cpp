@@ -341,6 +341,21 @@ struct byteps_server {
   uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
   std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
   std::atomic<uint64_t> n_consumer_launches{0}, n_key_releases{0};
+  // Blocking pulls into this device's memory (combine path): served by the
+  // pull copy service, created on first use (BPSR_SERVER_PULL_SERVICE=0: the
+  // lane issuers' batched copies instead).
+  bool pull_service = true;
+  std::mutex svc_mu;
+  bpsr::CopyService* svc = nullptr;
+  bool svc_tried = false;
+  std::atomic<uint64_t> n_service_pulls{0};
+  // order_after's events for those pulls: the service copies on no stream of
+  // ours, so a caller event is also waited for on a gate stream whose event
+  // the next service pull synchronises on (a blocking call: it waits anyway)
+  std::mutex gate_mu;
+  hipStream_t gate_stream = nullptr;
+  hipEvent_t gate_ev = nullptr;
+  std::atomic<uint64_t> gate_seq{0}, gate_done{0};
 };
 
 namespace bpsr {
@@ -1590,6 +1605,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (s->schedule || s->blocking) s->combine = false;
   if (const char* fl = getenv("BPSR_SERVER_INFLIGHT")) s->inflight = std::max(1L, atol(fl));
   if (const char* r = getenv("BPSR_SERVER_RELEASE")) s->dev_release = std::string(r) == "device";
+  if (const char* ps = getenv("BPSR_SERVER_PULL_SERVICE")) s->pull_service = atoi(ps) != 0;
   if (const char* t = getenv("BPSR_SERVER_RELEASE_TIMEOUT_S"))
     if (atof(t) > 0) s->kq_timeout_s = atof(t);
   // device releases: the fused left fold of a sync round, through the lane
@@ -1726,6 +1742,9 @@ int byteps_server_destroy(byteps_server* s) {
     if (ks->arena) (void)hipFree(ks->arena);
   }
   if (s->kq) (void)byteps_reduce_blockq_destroy(s->kq);
+  copysvc_destroy(s->svc);
+  if (s->gate_ev) (void)hipEventDestroy(s->gate_ev);
+  if (s->gate_stream) (void)hipStreamDestroy(s->gate_stream);
   for (hipEvent_t e : s->kq_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& Lp : s->lanes) {
@@ -1763,6 +1782,72 @@ void wait_lane_done(Lane& L, uint64_t seq) {
   if (spin_until([&] { return L.done_pub.load(std::memory_order_acquire) >= seq; })) return;
   std::unique_lock<std::mutex> dl(L.done_mu);
   L.done_cv.wait(dl, [&] { return L.done_seq >= seq; });
+}
+// The pull copy service for a blocking pull of `len` bytes into `out`, when
+// `out` is this device's memory (the service's release covers this device
+// only) and the pull is small enough that a lane copy's launch cost matters.
+constexpr size_t kServiceMaxPull = 16u << 20;
+CopyService* service_for(byteps_server* s, void* out, size_t len) {
+  if (!s->pull_service || len == 0 || len > kServiceMaxPull) return nullptr;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, out) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeDevice || a.device != s->cfg.device) return nullptr;
+  std::lock_guard<std::mutex> g(s->svc_mu);
+  if (!s->svc && !s->svc_tried) {
+    s->svc_tried = true;
+    if (copysvc_create(s->cfg.device, &s->svc)) s->svc = nullptr;  // lane copies then
+  }
+  return s->svc;
+}
+// A blocking pull through the copy service: wait for the round's fold as a
+// device view does (its completer's published sequence, no HIP call), then
+// one service copy; count the pull after the copy, as the lane path does.
+// Sync mode keeps the store still meanwhile: the next round needs this
+// worker's next push, which follows this pull.
+int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, size_t len) {
+  std::unique_lock<std::mutex> lk(ks->mu);
+  if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
+  ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
+  if (ks->error) return key_error(ks);
+  const bool has = ks->has_done;
+  hipEvent_t ev = ks->fold_ev;
+  const uint64_t need = ks->fold_seq;
+  const int fl = ks->fold_lane;
+  const void* store = ks->store;
+  lk.unlock();
+  if (need) {
+    wait_lane_done(fl < 0 ? *s->klane : *s->lanes[fl], need);
+  } else if (has) {
+    hipError_t e = hipEventSynchronize(ev);
+    if (e != hipSuccess) return hip_fail(e, "store fold sync");
+  }
+  lk.lock();
+  if (ks->error) return key_error(ks);  // a keyed epoch that timed out
+  lk.unlock();
+  const uint64_t gseq = s->gate_seq.load(std::memory_order_acquire);
+  if (gseq > s->gate_done.load(std::memory_order_acquire)) {  // order_after's events first
+    hipEvent_t gev;
+    {
+      std::lock_guard<std::mutex> g(s->gate_mu);
+      gev = s->gate_ev;
+    }
+    // the event's latest record covers every gate recorded up to gseq
+    hipError_t e = hipEventSynchronize(gev);
+    if (e != hipSuccess) return hip_fail(e, "order_after gate sync");
+    uint64_t d = s->gate_done.load(std::memory_order_relaxed);
+    while (d < gseq && !s->gate_done.compare_exchange_weak(d, gseq)) {
+    }
+  }
+  int rc = copysvc_copy(svc, out, store, len);
+  if (rc) return rc;
+  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
+  s->n_service_pulls.fetch_add(1, std::memory_order_relaxed);
+  lk.lock();
+  count_pull(s, ks);
+  return BYTEPS_REDUCE_OK;
 }
 void sync_push_cb(void* ctx, uint64_t, int, int status) {
   static_cast<SyncWait*>(ctx)->finish(status);
@@ -1962,6 +2047,7 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
     if (rc) return rc;
     KeyState* ks = key_for_pull(s, key);
     if (!ks) return BYTEPS_REDUCE_EARGS;
+    if (CopyService* svc = service_for(s, out, len)) return service_pull(s, svc, ks, out, len);
     std::unique_lock<std::mutex> lk(ks->mu);
     if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
     if (ks->error) return key_error(ks);
@@ -2458,16 +2544,31 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
       if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(caller event)");
     }
   }
+  if (s->pull_service && s->combine && !s->cfg.async_mode) {  // the copy service's gate
+    std::lock_guard<std::mutex> g(s->gate_mu);
+    hipError_t e = hipSuccess;
+    if (!s->gate_stream) e = hipStreamCreateWithFlags(&s->gate_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && !s->gate_ev) e = hipEventCreateWithFlags(&s->gate_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->gate_stream, ev, 0);
+    if (e == hipSuccess) e = hipEventRecord(s->gate_ev, s->gate_stream);
+    if (e != hipSuccess) return hip_fail(e, "order_after gate");
+    s->gate_seq.fetch_add(1, std::memory_order_release);
+  }
   return BYTEPS_REDUCE_OK;
 }
 
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
   if (!s || (n > 0 && !out) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  const uint64_t v[8] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
-                         s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
-                         s->n_copy_launches.load(), s->n_consumer_launches.load(),
-                         s->n_key_releases.load()};
-  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  uint64_t svc_launches = 0;
+  {
+    std::lock_guard<std::mutex> g(s->svc_mu);
+    svc_launches = bpsr::copysvc_launches(s->svc);
+  }
+  const uint64_t v[10] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+                          s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
+                          s->n_copy_launches.load(), s->n_consumer_launches.load(),
+                          s->n_key_releases.load(), s->n_service_pulls.load(), svc_launches};
+  for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

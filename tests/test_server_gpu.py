@@ -1349,6 +1349,103 @@ def test_order_after_orders_running_producer_without_host_wait():
     srv.close()
 
 
+@pytest.mark.parametrize("service", ["1", "0"], ids=["copy_service", "lane_copies"])
+def test_blocking_device_pulls_through_copy_service(port, service, monkeypatch):
+    """Blocking pulls into this device's memory (combining mode) are served by
+    the pull copy service (a persistent kernel fed through a pinned job ring):
+    bit-exact at every size, from one element to a key of many 256 KiB jobs,
+    into destinations at byte offsets 0..2 (vector, word and byte copies);
+    across the service's idle exit and relaunch (a pause between rounds); and
+    behind order_after — the destination's previous writer (a long spin, then
+    a fill on the caller's stream) lands before the copy.  PyTorch's default
+    stream does not wait for a running service.  BPSR_SERVER_PULL_SERVICE=0
+    serves the same pulls with lane copies."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_PULL_SERVICE", service)
+    dt, N, R = DType.FLOAT16, 3, 3
+    sizes = [1, 8, 1001, 131_072 + 5, 1_500_007]                # elements per key
+    keys = list(range(70, 70 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    bufs = {(w, j): torch.zeros(n * es + 8, dtype=torch.uint8, device=dev)
+            for w in range(N) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    bar = threading.Barrier(N + 1)
+    errors, pulled, stream_s = [], {}, []
+
+    def worker(w):
+        try:
+            rng = random.Random(900 + w)
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)              # init round
+            for r in range(1, R + 1):
+                order = list(range(len(keys)))
+                rng.shuffle(order)
+                for j in order:
+                    srv.push(keys[j], w, src[(w, r, j)], dt)
+                bar.wait(timeout=120)                           # main reads the orders
+                for j in order:
+                    off = (w + j + r) % 3
+                    n = sizes[j] * es
+                    dst = bufs[(w, j)][off:off + n]
+                    if j == len(sizes) - 1 and w == 0:
+                        torch.cuda._sleep(50_000_000)           # the previous writer, still running
+                    dst.fill_(0xAB)
+                    srv.pull(keys[j], dst)
+                    if r == R and w == 0:   # right after a pull: the service is running
+                        t0 = time.perf_counter()
+                        x = torch.ones(1024, device=dev)
+                        x.add_(1)
+                        torch.cuda.current_stream(dev).synchronize()
+                        stream_s.append(time.perf_counter() - t0)
+                    pulled[(w, r, j)] = dst.cpu().numpy().copy()
+                bar.wait(timeout=120)
+                if r == 1:
+                    time.sleep(0.05)                            # the service exits idle
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    orders = {}
+    try:
+        for r in range(1, R + 1):
+            bar.wait(timeout=120)
+            for j, k in enumerate(keys):
+                rounds, _, order = srv.key_info(k)
+                assert rounds == r and sorted(order) == list(range(N))
+                orders[(r, j)] = order
+            bar.wait(timeout=120)
+    except threading.BrokenBarrierError:
+        raise AssertionError(f"worker failed: {errors}")
+    finally:
+        for t in ts:
+            t.join(timeout=60)
+    assert not errors, errors
+    st = srv.stats()
+    srv.close()
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, j) for w in orders[(r, j)]], n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, pulled[(w, r, j)], want, nan_class_f32_f64=False,
+                                   what=f"r{r} key {j} w{w}")
+    total = N * R * len(keys)
+    if service == "1":
+        assert st["service_pulls"] == total
+        assert st["service_launches"] >= 2                      # the idle exit, then a relaunch
+    else:
+        assert st["service_pulls"] == 0 and st["service_launches"] == 0
+    # the default stream's work did not wait for the running service
+    assert len(stream_s) == len(keys) and sorted(stream_s)[len(keys) // 2] < 0.05, stream_s
+
+
 def _ptr_copy(ptr, src):
     from prophet_amd.reducer import GpuReducer
     GpuReducer().copy(ptr, src, src.numel() * src.element_size())

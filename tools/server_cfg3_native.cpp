@@ -141,8 +141,8 @@ int main(int argc, char** argv) {
                        hipMemcpyDeviceToDevice));
         }
     }
-    uint64_t st0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st0, 8));
+    uint64_t st0[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st0, 10));
     // persistent worker threads (a transport's receive threads), released per
     // round by the driver and joined by a countdown
     std::vector<double> ts;
@@ -299,9 +299,9 @@ int main(int argc, char** argv) {
     const double med = ts[ts.size() / 2];
     std::sort(push_ts.begin(), push_ts.end());
     const double push_med = push_ts[push_ts.size() / 2];
-    uint64_t st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st, 8));
-    for (int i = 0; i < 8; ++i) st[i] -= st0[i];
+    uint64_t st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    CKR(byteps_server_stats(srv, st, 10));
+    for (int i = 0; i < 10; ++i) st[i] -= st0[i];
     const char* rel = getenv("BPSR_SERVER_RELEASE");
     printf("{\"config\": \"cfg3_via_server\", \"driver\": \"native C++ threads "
            "(tools/server_cfg3_native.cpp)\", \"variant\": \"%s\", \"n_workers\": %d, "
@@ -311,13 +311,15 @@ int main(int argc, char** argv) {
            "\"rounds_folded_per_round\": %.1f, \"pull_launches_per_round\": %.1f, "
            "\"issuer_ms_per_round\": %.4f, \"push_copy_launches_per_round\": %.1f, "
            "\"release\": \"%s\", \"consumer_launches_per_round\": %.2f, "
-           "\"key_releases_per_round\": %.1f, \"pulls_agree\": %s}\n",
+           "\"key_releases_per_round\": %.1f, \"service_pulls_per_round\": %.1f, "
+           "\"service_launches\": %llu, \"pulls_agree\": %s}\n",
            names[variant], N, np, lanes, total, med * 1e3,
            ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, push_med * 1e3,
            (double)st[0] / total_rounds, (double)st[1] / total_rounds,
            (double)st[2] / total_rounds, (double)st[4] * 1e-6 / total_rounds,
            (double)st[5] / total_rounds, rel ? rel : "launch", (double)st[6] / total_rounds,
-           (double)st[7] / total_rounds, same ? "true" : "false");
+           (double)st[7] / total_rounds, (double)st[8] / total_rounds,
+           (unsigned long long)st[9], same ? "true" : "false");
     fflush(stdout);
     CKR(byteps_server_destroy(srv));
   }
