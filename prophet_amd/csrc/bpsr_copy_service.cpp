@@ -156,7 +156,11 @@ int copysvc_create(int device, CopyService** out) {
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->stop), 64, fl);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dev), 256);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dring), sizeof(SvcJob) * kSvcRing);
-  if (e == hipSuccess) e = hipMemset(c->dring, 0, sizeof(SvcJob) * kSvcRing);
+  // on the service's own (non-blocking) stream: a NULL-stream memset would
+  // wait for every blocking stream, a running keyed consumer's included —
+  // which can be waiting for this very thread's next push
+  if (e == hipSuccess) e = hipMemsetAsync(c->dring, 0, sizeof(SvcJob) * kSvcRing, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) {
     std::memset(c->ring, 0, sizeof(SvcJob) * kSvcRing);
     std::memset(c->done, 0, sizeof(uint64_t) * kSvcRing * kDoneStride);
