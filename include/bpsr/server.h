@@ -143,15 +143,26 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
 int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
 
 /* A worker's pull: blocks until the key's current round is finished (sync mode),
- * then copies the store (len bytes) to `out`.  Into device memory with the
- * default engine in sync mode, the copy is one of the lane issuer's batched
- * pull copies: the issuer tells the caller which of its launches carries the
- * copy, and the caller waits for the lane's completer to see that launch
- * complete (no HIP call on the caller's thread, no responder hop), then counts
- * the pull.  Pulls parked before the round finishes are queued together when
- * it does, so the pulls one round completion answers ride in one launch.  A
- * call made from inside a callback (on the responder thread) copies directly.
- * The same holds for blocking pushes of device data (byteps_server_push).
+ * then copies the store (len bytes) to `out`.  Into THIS device's memory with
+ * the default engine in sync mode (up to 16 MiB), the pull copy service does
+ * the copy: the caller waits for the round's fold as a device view does (its
+ * completer's published sequence), writes one tagged job per 64 KiB into a
+ * pinned ring and spins on the jobs' done words, which a persistent service
+ * kernel (fetcher + 64 copier workgroups, on a non-blocking high-priority
+ * stream of its own) stores once the bytes are visible device-wide — no HIP
+ * call and no thread hand-off per pull (≈5–6 µs per small pull from 1 or 8
+ * threads).  The kernel exits after 0.5 ms without a job (or
+ * after 2 s; the next pull relaunches it), so a device-wide synchronisation
+ * waits at most that long for it.  Events given to byteps_server_order_after
+ * are waited for (on the host) before such a copy.  BPSR_SERVER_PULL_SERVICE=0
+ * or other destinations: the copy is one of the lane issuer's batched pull
+ * copies: the issuer tells the caller which of its launches carries the copy,
+ * and the caller waits for the lane's completer to see that launch complete
+ * (no HIP call on the caller's thread, no responder hop), then counts the
+ * pull.  Pulls parked before the round finishes are queued together when it
+ * does, so the pulls one round completion answers ride in one launch.  A call
+ * made from inside a callback (on the responder thread) copies directly.  The
+ * same holds for blocking pushes of device data (byteps_server_push).
  * BPSR_SERVER_SPIN_US=n: such a waiter polls the lane's completion for up to
  * n µs before it sleeps (default 0: it sleeps at once). */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
