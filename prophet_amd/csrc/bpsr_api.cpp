@@ -1152,6 +1152,12 @@ uint32_t keyq_launched(byteps_reduce_blockq* q) {
   return q->launch_epoch;
 }
 
+void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched) {
+  std::lock_guard<std::mutex> g(q->mu);
+  *next_epoch = q->rel_epoch[(size_t)key] + 1;
+  *launched = q->launch_epoch;
+}
+
 int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s) {
   std::lock_guard<std::mutex> g(q->mu);
   const uint32_t ep = q->rel_epoch[(size_t)key] + 1;

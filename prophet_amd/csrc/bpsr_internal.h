@@ -342,6 +342,8 @@ int keyq_launch(struct byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* st
                 uint32_t* epoch);
 uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
 uint32_t keyq_launched(struct byteps_reduce_blockq* q);
+// Both of the above under one lock.
+void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched);
 int keyq_release(struct byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s);
 bool keyq_failed(struct byteps_reduce_blockq* q);
 std::string keyq_debug(struct byteps_reduce_blockq* q);  // state summary (synchronous copy)

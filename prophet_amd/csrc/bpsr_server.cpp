@@ -245,6 +245,7 @@ struct KeyState {
   hipEvent_t fold_ev = nullptr;
   uint64_t fold_seq = 0;      // lane completion seq of the last issued round (0: untracked)
   int fold_lane = 0;          // the lane whose completer tracks fold_seq
+  std::vector<int> order_tmp; // a keyed round's order on its way out (arrive)
   // device releases: the key's block in the server's keyed queue (-1: none),
   // whether this round's last fold is a keyed consumer's, and whether a push
   // of the current round was copied into its slot (released behind the copy)
@@ -300,6 +301,14 @@ struct byteps_server {
   // every call looks its key up; keys are added once: lookups share the lock
   std::shared_mutex map_mu;
   std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
+  // ... and first probe a lock-free index of the same keys (open addressing,
+  // entries never removed before destroy; filled to half at most, later keys
+  // only in the map): a shared lock is an atomic add on one line that every
+  // calling thread bounces
+  static constexpr size_t kKeyIndex = 1u << 14;
+  std::unique_ptr<std::atomic<bpsr::KeyState*>[]> key_index{
+      new std::atomic<bpsr::KeyState*>[kKeyIndex]()};
+  size_t key_index_n = 0;  // under map_mu
   std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
   // responder thread: SendPullResponse of queued pulls (server.cc:100-114)
   // and SendPushResponse of non-blocking pushes (server.cc:255)
@@ -361,9 +370,30 @@ struct byteps_server {
 namespace bpsr {
 namespace {
 
-int set_device(const byteps_server* s) {
+// The device a server call last bound on this thread.  Every entry point
+// binds the server's device (set_device), except the two per-key calls of a
+// combining server's receive thread — push_ready and pull_device_view — which
+// bind once per thread (bind_cached: hipSetDevice costs ≈ 30 ns, a third of a
+// keyed push_ready): what they do themselves touches only the server's own
+// streams and events, their launches go through the lane issuers, and
+// whatever they create or allocate binds again first (force_device), since
+// the caller may have switched devices in between.
+thread_local int t_bound_device = -1;
+
+int force_device(const byteps_server* s) {
   hipError_t e = hipSetDevice(s->cfg.device);
-  return e == hipSuccess ? 0 : hip_fail(e, "hipSetDevice");
+  if (e != hipSuccess) {
+    t_bound_device = -1;
+    return hip_fail(e, "hipSetDevice");
+  }
+  t_bound_device = s->cfg.device;
+  return 0;
+}
+
+int set_device(const byteps_server* s) { return force_device(s); }
+
+int bind_cached(const byteps_server* s) {
+  return s->combine && t_bound_device == s->cfg.device ? 0 : force_device(s);
 }
 
 // Make the lane's fold stream wait for its copies, unless it already waits
@@ -459,7 +489,17 @@ int pick_lane(byteps_server* s, size_t len) {
   return best;
 }
 
+size_t key_slot(uint64_t key) {
+  return (size_t)((key * 0x9E3779B97F4A7C15ull) >> 50) & (byteps_server::kKeyIndex - 1);
+}
+
 KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
+  for (size_t i = key_slot(key), probes = 0; probes < 32; ++probes) {
+    KeyState* p = s->key_index[i].load(std::memory_order_acquire);
+    if (!p) break;
+    if (p->key == key) return p;
+    i = (i + 1) & (byteps_server::kKeyIndex - 1);
+  }
   {
     std::shared_lock<std::shared_mutex> g(s->map_mu);
     auto it = s->keys.find(key);
@@ -473,6 +513,16 @@ KeyState* get_key(byteps_server* s, uint64_t key, bool create) {
   ks->key = key;
   KeyState* p = ks.get();
   s->keys.emplace(key, std::move(ks));
+  if (s->key_index_n < byteps_server::kKeyIndex / 2) {
+    for (size_t i = key_slot(key), probes = 0; probes < 32; ++probes) {
+      if (!s->key_index[i].load(std::memory_order_relaxed)) {
+        s->key_index[i].store(p, std::memory_order_release);
+        ++s->key_index_n;
+        break;
+      }
+      i = (i + 1) & (byteps_server::kKeyIndex - 1);
+    }
+  }
   return p;
 }
 
@@ -497,6 +547,7 @@ int allocate(byteps_server* s, KeyState* ks, size_t len, int dtype) {
   // are latency-bound, and many of them should not cost 80 KiB a slot)
   const size_t align = len >= (1u << 20) ? kSlotAlign : 4096;
   ks->stride = (len + align - 1) / align * align + kSlotSkew;
+  if (int rc = force_device(s)) return rc;
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, ks->stride * (size_t)(N + 1));
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(key arena)");
@@ -577,6 +628,7 @@ size_t next_async_mirror(KeyState* ks) { return (size_t)(ks->mirror_next++ % ks-
 // with queue_now, also mirror the finished current round.  Caller holds ks->mu.
 int ensure_mirror(byteps_server* s, KeyState* ks, bool queue_now) {
   if (!ks->mirror.empty()) return 0;
+  if (int rc = force_device(s)) return rc;
   const int nm = s->cfg.async_mode ? s->cfg.num_workers + 1 : 2;
   hipError_t e;
   for (int i = 0; i < nm; ++i) {
@@ -824,7 +876,7 @@ void build_kq(byteps_server* s, int dtype) {
     d[i].len = keys[i]->len;
     d[i].n = N;
   }
-  if (keyq_create(d.data(), (int)d.size(), dtype, s->kq_timeout_s, &s->kq)) {
+  if (force_device(s) || keyq_create(d.data(), (int)d.size(), dtype, s->kq_timeout_s, &s->kq)) {
     s->kq = nullptr;  // no queue: every round keeps the lane launches
     return;
   }
@@ -858,15 +910,17 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
   {
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (s->kq_off.load()) return 1;
-    const uint32_t need = keyq_next_epoch(s->kq, ks->kq_key.load());
-    while (keyq_launched(s->kq) < need) {
-      const uint32_t next = keyq_launched(s->kq) + 1;
+    uint32_t need = 0, launched = 0;
+    keyq_state(s->kq, ks->kq_key.load(), &need, &launched);
+    for (; launched < need; launched = keyq_launched(s->kq)) {
+      const uint32_t next = launched + 1;
       const int slot = (int)(next % byteps_server::kKqRing);
       if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
         return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
                     byteps_server::kKqRing);
       hipEvent_t& e = s->kq_ev[slot];
       if (!e) {
+        if (int rc = force_device(s)) return rc;
         const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
         if (he != hipSuccess) {
           e = nullptr;
@@ -1159,9 +1213,11 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
   }
   if (ks->arrived < N) return 0;
   if (!q && keyed_member(s, ks)) {
-    // device release: no launch for this round
-    std::vector<int> order;
-    order.swap(ks->order);
+    // device release: no launch for this round (the order moves through a
+    // scratch vector that keeps its capacity: no allocation per round)
+    std::vector<int>& order = ks->order_tmp;
+    order.assign(ks->order.begin(), ks->order.end());
+    ks->order.clear();
     ks->arrived = 0;
     if (!ks->round_copied) {  // the pushes are in their slots already (push_ready)
       const int rc = key_release(s, ks, order, nullptr);
@@ -1613,7 +1669,7 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (!s->combine || cfg->async_mode || cfg->policy != BYTEPS_SERVER_FUSED ||
       cfg->num_workers > kKeyedMaxSrcs)
     s->dev_release = false;
-  int rc = set_device(s.get());
+  int rc = force_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
   int prio_lo = 0, prio_hi = 0;
@@ -1798,7 +1854,7 @@ CopyService* service_for(byteps_server* s, void* out, size_t len) {
   std::lock_guard<std::mutex> g(s->svc_mu);
   if (!s->svc && !s->svc_tried) {
     s->svc_tried = true;
-    if (copysvc_create(s->cfg.device, &s->svc)) s->svc = nullptr;  // lane copies then
+    if (force_device(s) || copysvc_create(s->cfg.device, &s->svc)) s->svc = nullptr;  // lane copies then
   }
   return s->svc;
 }
@@ -2021,7 +2077,7 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   if (!s) return fail(BYTEPS_REDUCE_EARGS, "null server");
   if (worker < 0 || worker >= s->cfg.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
-  int rc = set_device(s);
+  int rc = bind_cached(s);
   if (rc) return rc;
   KeyState* ks = get_key(s, key, false);
   if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
@@ -2162,7 +2218,7 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   if (len) *len = 0;
   if (s->cfg.async_mode)
     return fail(BYTEPS_REDUCE_EARGS, "device views need sync mode (async pushes rewrite the store)");
-  int rc = set_device(s);
+  int rc = bind_cached(s);
   if (rc) return rc;
   KeyState* ks = key_for_pull(s, key);
   if (!ks) return BYTEPS_REDUCE_EARGS;
@@ -2176,18 +2232,19 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   const uint64_t need = ks->fold_seq;
   const int fl = ks->fold_lane;
   const void* view = ks->store;
-  lk.unlock();
-  if (need) {  // tracked by a completer (the lane's, or the keyed one): no HIP call here
-    Lane& L = fl < 0 ? *s->klane : *s->lanes[fl];
-    if (L.done_pub.load(std::memory_order_acquire) < need) {  // else: no lock at all
-      std::unique_lock<std::mutex> dl(L.done_mu);
-      L.done_cv.wait(dl, [&] { return L.done_seq >= need; });
+  Lane* FL = need ? (fl < 0 ? s->klane.get() : s->lanes[fl].get()) : nullptr;
+  // the fold completed already (published without a lock): answer at once
+  if (!(FL && FL->done_pub.load(std::memory_order_acquire) >= need)) {
+    lk.unlock();
+    if (FL) {  // tracked by a completer (the lane's, or the keyed one): no HIP call here
+      std::unique_lock<std::mutex> dl(FL->done_mu);
+      FL->done_cv.wait(dl, [&] { return FL->done_seq >= need; });
+    } else if (has) {
+      hipError_t e = hipEventSynchronize(ev);
+      if (e != hipSuccess) return hip_fail(e, "store fold sync");
     }
-  } else if (has) {
-    hipError_t e = hipEventSynchronize(ev);
-    if (e != hipSuccess) return hip_fail(e, "store fold sync");
+    lk.lock();
   }
-  lk.lock();
   if (ks->error) return key_error(ks);  // a keyed epoch that timed out
   s->n_pulls.fetch_add(1, std::memory_order_relaxed);
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
@@ -2546,6 +2603,7 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
   }
   if (s->pull_service && s->combine && !s->cfg.async_mode) {  // the copy service's gate
     std::lock_guard<std::mutex> g(s->gate_mu);
+    if (!s->gate_stream && (rc = force_device(s))) return rc;
     hipError_t e = hipSuccess;
     if (!s->gate_stream) e = hipStreamCreateWithFlags(&s->gate_stream, hipStreamNonBlocking);
     if (e == hipSuccess && !s->gate_ev) e = hipEventCreateWithFlags(&s->gate_ev, hipEventDisableTiming);
