@@ -677,6 +677,9 @@ struct byteps_reduce_blockq {
   uint64_t* khwords_dev = nullptr;
   BlockqCtl* hctl = nullptr;        // pinned host
   BlockqCtl* hctl_dev = nullptr;
+  uint32_t* kcnt = nullptr;         // device, one tile counter per block
+  uint32_t* khdone = nullptr;       // pinned host, one completion word per block
+  uint32_t* khdone_dev = nullptr;
 };
 
 // One consumer stream per device, created on first use, never destroyed:
@@ -716,6 +719,8 @@ static void blockq_free(byteps_reduce_blockq* q) {
   if (q->kwords) (void)hipFree(q->kwords);
   if (q->khwords) (void)hipHostFree(q->khwords);
   if (q->hctl) (void)hipHostFree(q->hctl);
+  if (q->kcnt) (void)hipFree(q->kcnt);
+  if (q->khdone) (void)hipHostFree(q->khdone);
   if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
   if (q->join_ev) (void)hipEventDestroy(q->join_ev);
   if (q->dev_table) (void)hipFree(q->dev_table);
@@ -847,6 +852,8 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.keyed = 0;
   Q.kwords = nullptr;
   Q.khwords = nullptr;
+  Q.kcnt = nullptr;
+  Q.khdone = nullptr;
   Q.herr = nullptr;
   const Tuning tu = tuning_for_n(q->ti.nmax);
   const bool gated = q->occ == 0;
@@ -1088,6 +1095,16 @@ int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double 
     e = hipHostGetDevicePointer(&d, p, 0);
     q->khwords_dev = static_cast<uint64_t*>(d);
   }
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->kcnt), sizeof(uint32_t) * (size_t)nkeys);
+  if (e == hipSuccess) e = hipMemset(q->kcnt, 0, sizeof(uint32_t) * (size_t)nkeys);
+  if (e == hipSuccess)
+    e = hipHostMalloc(&p, sizeof(uint32_t) * (size_t)nkeys, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e == hipSuccess) {
+    q->khdone = static_cast<uint32_t*>(p);
+    for (int i = 0; i < nkeys; ++i) __atomic_store_n(q->khdone + i, 0u, __ATOMIC_RELEASE);
+    e = hipHostGetDevicePointer(&d, p, 0);
+    q->khdone_dev = static_cast<uint32_t*>(d);
+  }
   if (e == hipSuccess)
     e = hipHostMalloc(&p, 256, hipHostMallocCoherent | hipHostMallocMapped);
   if (e == hipSuccess) {
@@ -1126,6 +1143,8 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   Q.keyed = 1;
   Q.kwords = q->kwords;
   Q.khwords = q->khwords_dev;
+  Q.kcnt = q->kcnt;
+  Q.khdone = q->khdone_dev;
   Q.grid = q->ti.tiles + 1;
   // Residency: at most 2 consumer workgroups per CU, and room left beside
   // them for the work a missing release may still need — a push copy into a
@@ -1170,6 +1189,10 @@ int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s)
   }
   q->rel_epoch[(size_t)key] = ep;
   return BYTEPS_REDUCE_OK;
+}
+
+bool keyq_key_done(const byteps_reduce_blockq* q, int key, uint32_t epoch) {
+  return epoch_reached(__atomic_load_n(q->khdone + key, __ATOMIC_ACQUIRE), epoch);
 }
 
 bool keyq_failed(byteps_reduce_blockq* q) {

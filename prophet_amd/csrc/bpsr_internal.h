@@ -123,6 +123,12 @@ struct BlockqLaunch {
   uint64_t* kwords;          // device words, one per block (helper / stream releases write them)
   const uint64_t* khwords;   // host words (device view), two per block by epoch parity
   uint32_t* herr;            // host word (device view): the helper mirrors ctl->err there
+  // Per-key completion: each finished tile adds to its block's counter (device,
+  // monotonic across epochs); the block's last tile of an epoch stores the
+  // epoch into the block's host word, once every tile's bytes are visible
+  // device-wide — a key's store can be read before the whole epoch ends.
+  uint32_t* kcnt;
+  uint32_t* khdone;          // host words (device view), one per block
 };
 // Arrival order of a keyed block: position m's source is worker
 // (perm >> 4m) & 7 (at most 8 sources); kKeySkip: the round is folded
@@ -346,6 +352,9 @@ uint32_t keyq_launched(struct byteps_reduce_blockq* q);
 void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched);
 int keyq_release(struct byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s);
 bool keyq_failed(struct byteps_reduce_blockq* q);
+// The key's fold for `epoch` is complete and visible device-wide (its block's
+// last tile stored the completion word): a lock-free host read.
+bool keyq_key_done(const struct byteps_reduce_blockq* q, int key, uint32_t epoch);
 std::string keyq_debug(struct byteps_reduce_blockq* q);  // state summary (synchronous copy)
 
 }  // namespace bpsr

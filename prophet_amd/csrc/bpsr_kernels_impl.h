@@ -711,6 +711,28 @@ struct PermSrcs {
   }
 };
 
+// A keyed tile is done: once every wave's stores have drained (write-through
+// for full tiles of a write-through launch; any other tile also writes back
+// its XCD's L2 first), one lane counts the tile for its block, and the
+// block's last tile of the epoch stores the epoch into the block's host word.
+template <int NT>
+__device__ __forceinline__ void key_tile_done(const BlockqLaunch& Q, uint32_t blk,
+                                              bool written_through) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (!written_through) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t nt = Q.block_first[blk + 1] - Q.block_first[blk];
+    const uint32_t old =
+        __hip_atomic_fetch_add(Q.kcnt + blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((old + 1) % nt == 0)
+      __hip_atomic_store(Q.khdone + blk, Q.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
   if (Q.helper && blockIdx.x == 0) {  // dispatched first: resident for the whole launch
@@ -745,6 +767,7 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
   const uint32_t perm = (uint32_t)(w >> 32);
   if (perm == kKeySkip) {
     keep_prefetch(pf);
+    key_tile_done<NT>(Q, blk, true);  // nothing stored: the count stays per epoch
     return;
   }
   // fast path: the 8 pointers permuted in registers (selects); element work
@@ -772,6 +795,7 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
                                                      threadIdx.x);
   }
   keep_prefetch(pf);
+  key_tile_done<NT>(Q, blk, r.kind == kTileFull && NT == kPolWt);
 }
 
 // ------------------------------------------------------------- launchers ----

@@ -246,6 +246,7 @@ struct KeyState {
   uint64_t fold_seq = 0;      // lane completion seq of the last issued round (0: untracked)
   int fold_lane = 0;          // the lane whose completer tracks fold_seq
   std::vector<int> order_tmp; // a keyed round's order on its way out (arrive)
+  uint32_t kq_round_epoch = 0; // a keyed round: the consumer epoch that folds it
   // device releases: the key's block in the server's keyed queue (-1: none),
   // whether this round's last fold is a keyed consumer's, and whether a push
   // of the current round was copied into its slot (released behind the copy)
@@ -907,10 +908,11 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
   for (size_t m = 0; m < order.size(); ++m) perm |= (uint32_t)order[m] << (4 * m);
   hipEvent_t ev = nullptr;
   uint64_t seq = 0;
+  uint32_t need = 0;
   {
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (s->kq_off.load()) return 1;
-    uint32_t need = 0, launched = 0;
+    uint32_t launched = 0;
     keyq_state(s->kq, ks->kq_key.load(), &need, &launched);
     for (; launched < need; launched = keyq_launched(s->kq)) {
       const uint32_t next = launched + 1;
@@ -945,6 +947,7 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
     seq = s->kq_ev_seq[slot];
   }
   s->n_key_releases.fetch_add(1, std::memory_order_relaxed);
+  ks->kq_round_epoch = need;
   return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
 }
 
@@ -1839,6 +1842,28 @@ void wait_lane_done(Lane& L, uint64_t seq) {
   std::unique_lock<std::mutex> dl(L.done_mu);
   L.done_cv.wait(dl, [&] { return L.done_seq >= seq; });
 }
+// Wait for a round's fold, read from the key's state under its lock (fold_seq
+// / fold_lane / kq_round_epoch).  A keyed round is readable as soon as its
+// key's completion word says so (the consumer may still be folding other
+// keys): poll that word and the keyed completer's progress for up to
+// kKeyedSpinUs, then sleep until the completer publishes the epoch (which
+// also settles a consumer that gave up).
+constexpr int kKeyedSpinUs = 200;
+void wait_round_fold(byteps_server* s, Lane& FL, uint64_t need, int kq_key, uint32_t kq_epoch) {
+  if (FL.done_pub.load(std::memory_order_acquire) >= need) return;
+  if (kq_key >= 0 && kq_epoch) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      for (int i = 0; i < 32; ++i) {
+        if (keyq_key_done(s->kq, kq_key, kq_epoch)) return;
+        if (FL.done_pub.load(std::memory_order_acquire) >= need) return;
+        __builtin_ia32_pause();
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kKeyedSpinUs)) break;
+    }
+  }
+  wait_lane_done(FL, need);
+}
 // The pull copy service for a blocking pull of `len` bytes into `out`, when
 // `out` is this device's memory (the service's release covers this device
 // only) and the pull is small enough that a lane copy's launch cost matters.
@@ -1873,9 +1898,11 @@ int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, si
   const uint64_t need = ks->fold_seq;
   const int fl = ks->fold_lane;
   const void* store = ks->store;
+  const int kq_key = fl < 0 ? ks->kq_key.load() : -1;
+  const uint32_t kq_epoch = ks->kq_round_epoch;
   lk.unlock();
   if (need) {
-    wait_lane_done(fl < 0 ? *s->klane : *s->lanes[fl], need);
+    wait_round_fold(s, fl < 0 ? *s->klane : *s->lanes[fl], need, kq_key, kq_epoch);
   } else if (has) {
     hipError_t e = hipEventSynchronize(ev);
     if (e != hipSuccess) return hip_fail(e, "store fold sync");
@@ -2233,12 +2260,15 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
   const int fl = ks->fold_lane;
   const void* view = ks->store;
   Lane* FL = need ? (fl < 0 ? s->klane.get() : s->lanes[fl].get()) : nullptr;
-  // the fold completed already (published without a lock): answer at once
-  if (!(FL && FL->done_pub.load(std::memory_order_acquire) >= need)) {
+  const int kq_key = fl < 0 ? ks->kq_key.load() : -1;
+  const uint32_t kq_epoch = ks->kq_round_epoch;
+  // the fold completed already (published without a lock, or the key's own
+  // completion word): answer at once
+  if (!(FL && (FL->done_pub.load(std::memory_order_acquire) >= need ||
+               (kq_key >= 0 && keyq_key_done(s->kq, kq_key, kq_epoch))))) {
     lk.unlock();
     if (FL) {  // tracked by a completer (the lane's, or the keyed one): no HIP call here
-      std::unique_lock<std::mutex> dl(FL->done_mu);
-      FL->done_cv.wait(dl, [&] { return FL->done_seq >= need; });
+      wait_round_fold(s, *FL, need, kq_key, kq_epoch);
     } else if (has) {
       hipError_t e = hipEventSynchronize(ev);
       if (e != hipSuccess) return hip_fail(e, "store fold sync");

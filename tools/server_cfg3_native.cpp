@@ -28,6 +28,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -245,32 +246,54 @@ int main(int argc, char** argv) {
             CKR(byteps_server_pull(srv, (uint64_t)i, out[k] + parts[i].first, parts[i].second,
                                    BYTEPS_SERVER_DEVICE));
     };
+    // Round hand-off between the driver and the worker threads.  The
+    // one-receive-thread variants (6, 7: ps-lite's shape, a receive thread
+    // that is always running) spin on atomics: a condition variable adds two
+    // thread wake-ups, 20-40 us, to every round (r04s28: 0.133-0.144 vs
+    // 0.114-0.117 ms for variant 6 with device releases).  The 8-thread
+    // variants keep the condition variable of rounds 2-3: with 8 busy
+    // workers and the server's own threads, spinning idle threads take CPU
+    // from them (r04s28: variant 4 0.21 vs 0.29-0.31 ms, variant 0 1.39-1.43
+    // vs 1.68-1.76).  CFG3_HANDOFF=spin|cv overrides.
+    const char* ho = getenv("CFG3_HANDOFF");
+    const bool cv_handoff = ho ? std::string(ho) == "cv" : !(variant == 6 || variant == 7);
+    std::atomic<int> go_a{-1}, left_a{0};
     std::vector<std::thread> th;
     for (int k = 0; k < N; ++k)
       th.emplace_back([&, k] {
         for (int r = 0; r < total_rounds; ++r) {
-          {
+          if (cv_handoff) {
             std::unique_lock<std::mutex> lk(m);
             cv.wait(lk, [&] { return go >= r; });
+          } else {
+            while (go_a.load(std::memory_order_acquire) < r) __builtin_ia32_pause();
           }
           one_round(k, r);
-          std::lock_guard<std::mutex> lk(m);
-          if (--left == 0) cv.notify_all();
+          if (cv_handoff) {
+            std::lock_guard<std::mutex> lk(m);
+            if (--left == 0) cv.notify_all();
+          } else {
+            left_a.fetch_sub(1, std::memory_order_acq_rel);
+          }
         }
       });
     for (int r = 0; r < total_rounds; ++r) {
       acks = 0;
       pulled = 0;
       auto t0 = std::chrono::steady_clock::now();
-      {
-        std::lock_guard<std::mutex> lk(m);
-        left = N;
-        go = r;
-      }
-      cv.notify_all();
-      {
+      if (cv_handoff) {
+        {
+          std::lock_guard<std::mutex> lk(m);
+          left = N;
+          go = r;
+        }
+        cv.notify_all();
         std::unique_lock<std::mutex> lk(m);
         cv.wait(lk, [&] { return left == 0; });
+      } else {
+        left_a.store(N, std::memory_order_release);
+        go_a.store(r, std::memory_order_release);
+        while (left_a.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
       }
       if (variant == 1 || variant >= 7)
         while (acks.load() < (long)N * np) std::this_thread::yield();
@@ -312,14 +335,14 @@ int main(int argc, char** argv) {
            "\"issuer_ms_per_round\": %.4f, \"push_copy_launches_per_round\": %.1f, "
            "\"release\": \"%s\", \"consumer_launches_per_round\": %.2f, "
            "\"key_releases_per_round\": %.1f, \"service_pulls_per_round\": %.1f, "
-           "\"service_launches\": %llu, \"pulls_agree\": %s}\n",
+           "\"service_launches\": %llu, \"handoff\": \"%s\", \"pulls_agree\": %s}\n",
            names[variant], N, np, lanes, total, med * 1e3,
            ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, push_med * 1e3,
            (double)st[0] / total_rounds, (double)st[1] / total_rounds,
            (double)st[2] / total_rounds, (double)st[4] * 1e-6 / total_rounds,
            (double)st[5] / total_rounds, rel ? rel : "launch", (double)st[6] / total_rounds,
            (double)st[7] / total_rounds, (double)st[8] / total_rounds,
-           (unsigned long long)st[9], same ? "true" : "false");
+           (unsigned long long)st[9], cv_handoff ? "condvar" : "spin", same ? "true" : "false");
     fflush(stdout);
     CKR(byteps_server_destroy(srv));
   }
