@@ -82,8 +82,13 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * kernel behind the round's copies — and one consumer launch per epoch (the
  * epoch's first release launches it) folds every key of the queue, each key's
  * tiles as soon as that key is released, in its arrival order (the same bits
- * as the launch path).  Pulls and views of a released round are answered once
- * that epoch's consumer has completed.  Contract: every key of the queue
+ * as the launch path).  Each key's last tile stores the epoch into the key's
+ * completion word once the key's bytes are visible device-wide, so device
+ * views and blocking device pulls (the copy service) of a released round are
+ * answered as soon as THAT key is folded, while the consumer still folds
+ * others; other pulls wait for the epoch's consumer to complete.  A key whose
+ * fold completed stays readable even if the epoch later gives up on another
+ * key (see below); the keys then fail on their next call.  Contract: every key of the queue
  * completes one round per epoch (BytePS pushes every key once per
  * iteration); a key that is not pushed within BPSR_SERVER_RELEASE_TIMEOUT_S
  * (default 5) seconds makes that epoch's consumer give up: the keys released
