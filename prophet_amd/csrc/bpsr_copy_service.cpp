@@ -262,6 +262,8 @@ uint64_t copysvc_launches(CopyService* c) { return c ? c->launches.load() : 0; }
 
 uint64_t copysvc_posted(CopyService* c) { return c->posted.load(); }
 
+bool copysvc_broken(const CopyService* c) { return c->broken.load(); }
+
 void copysvc_set_trace(CopyService* c, uint64_t* dev_trace) {
   std::lock_guard<std::mutex> g(c->mu);
   c->trace = dev_trace;

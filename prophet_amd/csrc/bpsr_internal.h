@@ -328,6 +328,9 @@ int copysvc_create(int device, CopyService** out);
 int copysvc_copy(CopyService* svc, void* dst, const void* src, size_t len);
 void copysvc_destroy(CopyService* svc);
 uint64_t copysvc_launches(CopyService* svc);  // kernel launches so far (0 for null)
+// A job timed out or a launch failed: the service takes no more jobs (its
+// callers use another copy path from then on).
+bool copysvc_broken(const CopyService* svc);
 // Probes (tools/dbg/copysvc_probe.cpp): jobs posted so far; a device trace
 // buffer (kSvcRing * 4 words) used from the next launch on.
 uint64_t copysvc_posted(CopyService* svc);

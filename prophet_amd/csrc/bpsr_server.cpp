@@ -1881,7 +1881,9 @@ CopyService* service_for(byteps_server* s, void* out, size_t len) {
     s->svc_tried = true;
     if (force_device(s) || copysvc_create(s->cfg.device, &s->svc)) s->svc = nullptr;  // lane copies then
   }
-  return s->svc;
+  // a service that gave up (a job not served in time) takes no more pulls:
+  // they ride lane copies, as with BPSR_SERVER_PULL_SERVICE=0
+  return s->svc && !copysvc_broken(s->svc) ? s->svc : nullptr;
 }
 // A blocking pull through the copy service: wait for the round's fold as a
 // device view does (its completer's published sequence, no HIP call), then
