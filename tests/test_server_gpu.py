@@ -1446,6 +1446,80 @@ def test_blocking_device_pulls_through_copy_service(port, service, monkeypatch):
     assert len(stream_s) == len(keys) and sorted(stream_s)[len(keys) // 2] < 0.05, stream_s
 
 
+def test_copy_service_many_rounds_racing_pullers(port):
+    """The pull copy service under load: 4 worker threads, 24 keys of random
+    sizes (1 element … 700 K fp32, so jobs of 1 … 11 chunks), 12 rounds; each
+    worker pushes every key, then pulls every key into its own device buffer
+    in its own random order, sometimes pausing past the service's idle exit —
+    thousands of jobs from racing posters, relaunches included.  Every pulled
+    byte equals the oracle's left fold in the recorded arrival order."""
+    from prophet_amd.server import PSServer
+    dt, N, R = DType.FLOAT32, 4, 12
+    rng0 = random.Random(77)
+    sizes = [rng0.choice([1, 3, 1000, 16_384, 70_001, 300_000, 700_000]) for _ in range(24)]
+    keys = list(range(200, 200 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=4)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    outs = {(w, j): torch.empty(n * es, dtype=torch.uint8, device=dev)
+            for w in range(N) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    bar = threading.Barrier(N + 1)
+    errors, pulled = [], {}
+
+    def worker(w):
+        try:
+            rng = random.Random(300 + w)
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)
+            for r in range(1, R + 1):
+                order = list(range(len(keys)))
+                rng.shuffle(order)
+                for j in order:
+                    srv.push(keys[j], w, src[(w, r, j)], dt)
+                bar.wait(timeout=120)
+                rng.shuffle(order)
+                for j in order:
+                    if rng.random() < 0.02:
+                        time.sleep(0.002)                # past the idle exit
+                    srv.pull(keys[j], outs[(w, j)])
+                    pulled[(w, r, j)] = outs[(w, j)].cpu().numpy().copy()
+                bar.wait(timeout=120)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    orders = {}
+    try:
+        for r in range(1, R + 1):
+            bar.wait(timeout=120)
+            for j, k in enumerate(keys):
+                orders[(r, j)] = srv.key_info(k)[2]
+            bar.wait(timeout=120)
+    except threading.BrokenBarrierError:
+        raise AssertionError(f"worker failed: {errors}")
+    finally:
+        for t in ts:
+            t.join(timeout=60)
+    assert not errors, errors
+    st = srv.stats()
+    srv.close()
+    for r in range(1, R + 1):
+        for j, n in enumerate(sizes):
+            want = np.zeros(n * es, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, j) for w in orders[(r, j)]], n * es, dt)
+            for w in range(N):
+                assert_bytes_match(dt, pulled[(w, r, j)], want, nan_class_f32_f64=False,
+                                   what=f"r{r} key {j} w{w}")
+    assert st["service_pulls"] == N * R * len(keys)
+    assert st["service_launches"] >= 2
+
+
 def _ptr_copy(ptr, src):
     from prophet_amd.reducer import GpuReducer
     GpuReducer().copy(ptr, src, src.numel() * src.element_size())
