@@ -359,6 +359,11 @@ int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, c
                              size_t len, int dtype, int location);
 int byteps_server_group_pull(byteps_server_group* g, uint64_t key, void* out, size_t len,
                              int location);
+/* byteps_server_pull_host_view on the instance holding a whole (unsplit) key:
+ * the zero-copy pull response of server.cc:42-70 (EARGS for a key split over
+ * several instances: view each piece through byteps_server_group_instance). */
+int byteps_server_group_pull_host_view(byteps_server_group* g, uint64_t key, const void** data,
+                                       size_t* len);
 /* byteps_server_push_many / _pull_many: keys routed, one batched call per instance. */
 int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
                                   const void* const* datas, const size_t* lens, int n, int worker,

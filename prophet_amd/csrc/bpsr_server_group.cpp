@@ -496,6 +496,23 @@ int byteps_server_group_pull(byteps_server_group* g, uint64_t key, void* out, si
   return BYTEPS_REDUCE_OK;
 }
 
+int byteps_server_group_pull_host_view(byteps_server_group* g, uint64_t key, const void** data,
+                                       size_t* len) {
+  if (!data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  *data = nullptr;
+  if (len) *len = 0;
+  int rc = check_group(g);
+  if (rc) return rc;
+  const size_t klen = declared_len(g, key);
+  std::vector<Piece> ps;
+  route(g, key, klen ? klen : 1, &ps);
+  if (ps.size() != 1)
+    return fail(BYTEPS_REDUCE_EARGS,
+                "key %llu is split over %zu instances: no single view (pull it, or view each "
+                "piece through byteps_server_group_instance)", (unsigned long long)key, ps.size());
+  return byteps_server_pull_host_view(g->inst[ps[0].server], key, data, len);
+}
+
 int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
                                   const void* const* datas, const size_t* lens, int n, int worker,
                                   int dtype, int location) {

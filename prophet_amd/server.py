@@ -30,6 +30,7 @@ SERVER_EXPORTS = (
     "byteps_server_group_instance", "byteps_server_group_init_key", "byteps_server_group_push",
     "byteps_server_group_pull", "byteps_server_group_push_many", "byteps_server_group_pull_many",
     "byteps_server_order_after", "byteps_server_group_order_after",
+    "byteps_server_group_pull_host_view",
 )
 SPLIT_HASH, SPLIT_RANGE = 0, 1
 HASH_FNS = {"djb2": 0, "naive": 1, "sdbm": 2, "built_in": 3}
@@ -71,6 +72,8 @@ def _lib():
         L.byteps_server_group_init_key.argtypes = [_vp, _u64, _sz, _int]
         L.byteps_server_group_push.argtypes = [_vp, _u64, _int, _vp, _sz, _int, _int]
         L.byteps_server_group_pull.argtypes = [_vp, _u64, _vp, _sz, _int]
+        L.byteps_server_group_pull_host_view.argtypes = [_vp, _u64, ctypes.POINTER(_vp),
+                                                         ctypes.POINTER(_sz)]
         L.byteps_server_group_push_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int, _int,
                                                     _int]
         L.byteps_server_group_pull_many.argtypes = [_vp, P(_u64), P(_vp), P(_sz), _int, _int]
@@ -458,6 +461,16 @@ class PSServerGroup:
         self._order([key], [out])
         _check(self.lib.byteps_server_group_pull(self.handle, key, p,
                                                  n if nbytes is None else nbytes, loc))
+
+    def pull_view(self, key: int) -> memoryview:
+        """Zero-copy pull response of a whole (unsplit) key from the instance
+        holding it (byteps_server_group_pull_host_view; PSServer.pull_view's
+        validity rules)."""
+        p, n = _vp(), _sz()
+        _check(self.lib.byteps_server_group_pull_host_view(self.handle, key, ctypes.byref(p),
+                                                           ctypes.byref(n)))
+        buf = (ctypes.c_char * n.value).from_address(p.value)
+        return memoryview(buf).cast("B").toreadonly()
 
     def push_many(self, keys, worker: int, datas, dtype: int) -> None:
         bufs = [_buf(d) for d in datas]

@@ -81,6 +81,7 @@ def test_bench_one_gpu_line_has_every_object():
     srv = line["server_cfg1"]
     assert "error" not in srv, srv
     assert srv["exact_vs_torch_sum"] is True and srv["node_GiBps"] > 0
+    assert srv["pull"].startswith("host_view") and srv["copying_pulls"]["node_GiBps"] > 0
 
 
 def test_server_group_leg_matches_oracle():

@@ -251,3 +251,52 @@ def test_group_push_validation_and_partial_failure():
     PortReducer(nthreads=4).sum_n(want, r1, n * 4, dt)
     assert np.array_equal(out, want)
     grp.close()
+
+
+def test_group_host_view_of_whole_keys():
+    """byteps_server_group_pull_host_view: a key held whole by one instance is
+    answered with that instance's pinned mirror (the zero-copy pull response
+    of server.cc:42-70), bit-exact with the oracle's fold in the recorded
+    arrival order; a key split over several instances has no single view
+    (EARGS), and its pull still works."""
+    from prophet_amd.reducer import EARGS, ReduceError
+    from prophet_amd.server import PSServerGroup
+    dt, N, n = DType.FLOAT32, 2, 300_001
+    grp = PSServerGroup(N, devices=[0, 0], split="range", split_min_bytes=1 << 30)
+    whole, split = 5, 6
+    grp.init_key(whole, n * 4, dt)
+    for r in range(3):                                   # init round + 2 rounds
+        ts = [threading.Thread(target=grp.push, args=(whole, w, data(dt, n, w, r, 5), dt))
+              for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        if r == 0:
+            continue
+        views = [bytes(grp.pull_view(whole)) for _ in range(N)]
+        # two fp32 operands: IEEE addition commutes, either arrival order folds
+        # to the same bits
+        want = np.zeros(n * 4, np.uint8)
+        PortReducer(nthreads=4).sum_n(want, [data(dt, n, w, r, 5) for w in range(N)], n * 4, dt)
+        for v in views:
+            assert np.array_equal(np.frombuffer(v, np.uint8), want)
+    grp.close()
+    grp = PSServerGroup(N, devices=[0, 0], split="range", split_min_bytes=4096)
+    grp.init_key(split, n * 4, dt)
+    for r in range(2):
+        ts = [threading.Thread(target=grp.push, args=(split, w, data(dt, n, w, r, 6), dt))
+              for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+    with pytest.raises(ReduceError) as e:
+        grp.pull_view(split)
+    assert e.value.code == EARGS
+    out = np.zeros(n * 4, np.uint8)
+    grp.pull(split, out)
+    want = np.zeros(n * 4, np.uint8)
+    PortReducer(nthreads=4).sum_n(want, [data(dt, n, w, 1, 6) for w in range(N)], n * 4, dt)
+    assert np.array_equal(out, want)
+    grp.close()
