@@ -169,7 +169,12 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
  * made from inside a callback (on the responder thread) copies directly.  The
  * same holds for blocking pushes of device data (byteps_server_push).
  * BPSR_SERVER_SPIN_US=n: such a waiter polls the lane's completion for up to
- * n µs before it sleeps (default 0: it sleeps at once). */
+ * n µs before it sleeps (default 0: it sleeps at once).  Blocking pushes FROM
+ * this device's memory (up to 16 MiB) take the copy service the same way:
+ * once the key's previous fold has completed, the service copies the data
+ * into the worker's slot with no key lock held, then the push arrives as a
+ * push_ready would (config 3's keys pushed and pulled one by one by 8
+ * threads: 20–21 → 3.0 ms per round).  Host sources keep the lanes' copies. */
 int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, int location);
 
 /* Zero-copy pull response for a host transport (server.cc:42-70 answers a pull
@@ -249,8 +254,8 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
  * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
  * push-copy launches, out[6] keyed consumer launches and out[7] rounds
  * released on the device (BPSR_SERVER_RELEASE=device), out[8] blocking pulls
- * served by the pull copy service and out[9] that service's kernel launches;
- * the first n (<= 10). */
+ * served by the pull copy service, out[9] that service's kernel launches and
+ * out[10] blocking pushes it served; the first n (<= 11). */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

@@ -358,7 +358,7 @@ struct byteps_server {
   std::mutex svc_mu;
   bpsr::CopyService* svc = nullptr;
   bool svc_tried = false;
-  std::atomic<uint64_t> n_service_pulls{0};
+  std::atomic<uint64_t> n_service_pulls{0}, n_service_pushes{0};
   // order_after's events for those pulls: the service copies on no stream of
   // ours, so a caller event is also waited for on a gate stream whose event
   // the next service pull synchronises on (a blocking call: it waits anyway)
@@ -1868,14 +1868,7 @@ void wait_round_fold(byteps_server* s, Lane& FL, uint64_t need, int kq_key, uint
 // `out` is this device's memory (the service's release covers this device
 // only) and the pull is small enough that a lane copy's launch cost matters.
 constexpr size_t kServiceMaxPull = 16u << 20;
-CopyService* service_for(byteps_server* s, void* out, size_t len) {
-  if (!s->pull_service || len == 0 || len > kServiceMaxPull) return nullptr;
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, out) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (a.type != hipMemoryTypeDevice || a.device != s->cfg.device) return nullptr;
+CopyService* service_get(byteps_server* s) {
   std::lock_guard<std::mutex> g(s->svc_mu);
   if (!s->svc && !s->svc_tried) {
     s->svc_tried = true;
@@ -1884,6 +1877,48 @@ CopyService* service_for(byteps_server* s, void* out, size_t len) {
   // a service that gave up (a job not served in time) takes no more pulls:
   // they ride lane copies, as with BPSR_SERVER_PULL_SERVICE=0
   return s->svc && !copysvc_broken(s->svc) ? s->svc : nullptr;
+}
+bool on_this_device(const byteps_server* s, const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeDevice && a.device == s->cfg.device;
+}
+CopyService* service_for(byteps_server* s, void* out, size_t len) {
+  if (!s->pull_service || len == 0 || len > kServiceMaxPull) return nullptr;
+  if (!on_this_device(s, out)) return nullptr;
+  return service_get(s);
+}
+// A blocking push's source for the service's copiers: this device's memory;
+// nullptr when the push takes the lane path.  Host sources stay on the lane
+// path: the copiers reading pinned host memory over PCIe made config 1's
+// host-resident rounds slower than the lanes' SDMA copies (r04s35: 28 vs 31.6
+// GiB/s with views, 23 vs 30.6 with copying pulls).
+const void* service_src(byteps_server* s, const void* data, size_t len, int location) {
+  if (!s->pull_service || !s->combine || s->cfg.async_mode || t_responder || len == 0 ||
+      len > kServiceMaxPull || location != BYTEPS_SERVER_DEVICE)
+    return nullptr;
+  return on_this_device(s, data) ? data : nullptr;
+}
+// The events given to byteps_server_order_after so far, waited for on the
+// host before a service copy (the service copies on no stream of ours).
+int wait_order_gate(byteps_server* s) {
+  const uint64_t gseq = s->gate_seq.load(std::memory_order_acquire);
+  if (gseq <= s->gate_done.load(std::memory_order_acquire)) return 0;
+  hipEvent_t gev;
+  {
+    std::lock_guard<std::mutex> g(s->gate_mu);
+    gev = s->gate_ev;
+  }
+  // the event's latest record covers every gate recorded up to gseq
+  hipError_t e = hipEventSynchronize(gev);
+  if (e != hipSuccess) return hip_fail(e, "order_after gate sync");
+  uint64_t d = s->gate_done.load(std::memory_order_relaxed);
+  while (d < gseq && !s->gate_done.compare_exchange_weak(d, gseq)) {
+  }
+  return 0;
 }
 // A blocking pull through the copy service: wait for the round's fold as a
 // device view does (its completer's published sequence, no HIP call), then
@@ -1912,20 +1947,7 @@ int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, si
   lk.lock();
   if (ks->error) return key_error(ks);  // a keyed epoch that timed out
   lk.unlock();
-  const uint64_t gseq = s->gate_seq.load(std::memory_order_acquire);
-  if (gseq > s->gate_done.load(std::memory_order_acquire)) {  // order_after's events first
-    hipEvent_t gev;
-    {
-      std::lock_guard<std::mutex> g(s->gate_mu);
-      gev = s->gate_ev;
-    }
-    // the event's latest record covers every gate recorded up to gseq
-    hipError_t e = hipEventSynchronize(gev);
-    if (e != hipSuccess) return hip_fail(e, "order_after gate sync");
-    uint64_t d = s->gate_done.load(std::memory_order_relaxed);
-    while (d < gseq && !s->gate_done.compare_exchange_weak(d, gseq)) {
-    }
-  }
+  if (int rc = wait_order_gate(s)) return rc;
   int rc = copysvc_copy(svc, out, store, len);
   if (rc) return rc;
   s->n_pulls.fetch_add(1, std::memory_order_relaxed);
@@ -1933,6 +1955,52 @@ int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, si
   lk.lock();
   count_pull(s, ks);
   return BYTEPS_REDUCE_OK;
+}
+// A blocking push through the copy service: once the slot is free (the key's
+// previous fold has completed — the same rule as the lane copy's stream wait),
+// the service copies the data into the worker's slot with no key lock held
+// and no HIP call; then the push arrives as if the transport had written the
+// slot itself (a push_ready: the round needs no copy ordering, and a device
+// release can be a host store).
+int service_push(byteps_server* s, CopyService* svc, uint64_t key, int worker, const void* src,
+                 size_t len, int dtype) {
+  KeyState* ks = get_key(s, key, true);
+  std::unique_lock<std::mutex> lk(ks->mu);
+  int rc = allocate(s, ks, len, dtype);
+  if (rc) return rc;
+  ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
+  if (ks->error) return key_error(ks);
+  if (ks->has_done) {
+    const bool keyed = ks->fold_lane < 0;
+    const uint64_t need = ks->fold_seq;
+    const int fl = ks->fold_lane;
+    const int kq_key = keyed ? ks->kq_key.load() : -1;
+    const uint32_t kq_epoch = ks->kq_round_epoch;
+    hipEvent_t ev = ks->fold_ev;
+    lk.unlock();
+    if (need) {
+      wait_round_fold(s, keyed ? *s->klane : *s->lanes[fl], need, kq_key, kq_epoch);
+    } else {
+      const hipError_t e = hipEventSynchronize(ev);
+      if (e != hipSuccess) return hip_fail(e, "slot's last fold");
+    }
+    lk.lock();
+    if (ks->error) return key_error(ks);
+  }
+  lk.unlock();
+  if ((rc = wait_order_gate(s))) return rc;  // the data's producer on the caller's stream
+  if ((rc = copysvc_copy(svc, ks->slot[worker], src, len))) return rc;
+  s->n_service_pushes.fetch_add(1, std::memory_order_relaxed);
+  lk.lock();
+  if (ks->error) return key_error(ks);
+  std::vector<FoldJob> defer;
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk, &defer))) return rc;
+  if (!defer.empty()) {
+    lk.unlock();
+    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return rc;
+    lk.lock();
+  }
+  return 0;
 }
 void sync_push_cb(void* ctx, uint64_t, int, int status) {
   static_cast<SyncWait*>(ctx)->finish(status);
@@ -1958,6 +2026,11 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   if (!s || !data) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   if (worker < 0 || worker >= s->cfg.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
+  if (const void* src = service_src(s, data, len, location)) {
+    int rc = set_device(s);
+    if (rc) return rc;
+    if (CopyService* svc = service_get(s)) return service_push(s, svc, key, worker, src, len, dtype);
+  }
   if (location == BYTEPS_SERVER_DEVICE && s->combine && !t_responder) {
     // device data: the copy goes through the lane issuer (batched with the
     // other pushes that piled up) and the push returns once it has landed;
@@ -2654,11 +2727,12 @@ int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
     std::lock_guard<std::mutex> g(s->svc_mu);
     svc_launches = bpsr::copysvc_launches(s->svc);
   }
-  const uint64_t v[10] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+  const uint64_t v[11] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
                           s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
                           s->n_copy_launches.load(), s->n_consumer_launches.load(),
-                          s->n_key_releases.load(), s->n_service_pulls.load(), svc_launches};
-  for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
+                          s->n_key_releases.load(), s->n_service_pulls.load(), svc_launches,
+                          s->n_service_pushes.load()};
+  for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

@@ -1517,6 +1517,7 @@ def test_copy_service_many_rounds_racing_pullers(port):
                 assert_bytes_match(dt, pulled[(w, r, j)], want, nan_class_f32_f64=False,
                                    what=f"r{r} key {j} w{w}")
     assert st["service_pulls"] == N * R * len(keys)
+    assert st["service_pushes"] == N * (R + 1) * len(keys)     # device pushes too
     assert st["service_launches"] >= 2
 
 

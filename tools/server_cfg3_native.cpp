@@ -102,8 +102,8 @@ int main(int argc, char** argv) {
                          "push_many_d2d+pull_many", "push_ready+device_view",
                          "push_ready_many+device_view", "one_receive_thread:push_ready+device_view",
                          "one_receive_thread:push_async_d2d+pull_into_async",
-                         "push_async_d2d+pull_into_async"};
-  constexpr int kVariants = 9;
+                         "push_async_d2d+pull_into_async", "push_blocking_d2d"};
+  constexpr int kVariants = 10;
   std::vector<uint64_t> keys(np);
   std::vector<size_t> lens(np);
   for (int i = 0; i < np; ++i) {
@@ -142,8 +142,8 @@ int main(int argc, char** argv) {
                        hipMemcpyDeviceToDevice));
         }
     }
-    uint64_t st0[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st0, 10));
+    uint64_t st0[11] = {0};
+    CKR(byteps_server_stats(srv, st0, 11));
     // persistent worker threads (a transport's receive threads), released per
     // round by the driver and joined by a countdown
     std::vector<double> ts;
@@ -161,7 +161,7 @@ int main(int argc, char** argv) {
     };
     std::vector<double> push_ts;
     auto one_round = [&](int k, int r) {
-      if (variant >= 7) {  // non-blocking device pushes and pulls into device buffers
+      if (variant == 7 || variant == 8) {  // non-blocking device pushes and pulls into device buffers
         if (variant == 7 && k != 0) {
           stamp(k);
           return;
@@ -236,6 +236,9 @@ int main(int argc, char** argv) {
           for (int i = 0; i < np; ++i) {
             if (ready)
               CKR(byteps_server_push_ready(srv, (uint64_t)i, k));
+            else if (variant == 9)  // a per-key blocking transport: blocking device pushes
+              CKR(byteps_server_push(srv, (uint64_t)i, k, grad[k] + parts[i].first,
+                                     parts[i].second, BYTEPS_REDUCE_FLOAT16, BYTEPS_SERVER_DEVICE));
             else
               CKR(byteps_server_push_async(srv, (uint64_t)i, k, grad[k] + parts[i].first,
                                            parts[i].second, BYTEPS_REDUCE_FLOAT16,
@@ -295,9 +298,9 @@ int main(int argc, char** argv) {
         go_a.store(r, std::memory_order_release);
         while (left_a.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
       }
-      if (variant == 1 || variant >= 7)
+      if (variant == 1 || variant == 7 || variant == 8)
         while (acks.load() < (long)N * np) std::this_thread::yield();
-      if (variant >= 7)
+      if (variant == 7 || variant == 8)
         while (pulled.load() < (long)N * np) std::this_thread::yield();
       const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (r >= 2 && r < rounds + 2) {
@@ -322,9 +325,9 @@ int main(int argc, char** argv) {
     const double med = ts[ts.size() / 2];
     std::sort(push_ts.begin(), push_ts.end());
     const double push_med = push_ts[push_ts.size() / 2];
-    uint64_t st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    CKR(byteps_server_stats(srv, st, 10));
-    for (int i = 0; i < 10; ++i) st[i] -= st0[i];
+    uint64_t st[11] = {0};
+    CKR(byteps_server_stats(srv, st, 11));
+    for (int i = 0; i < 11; ++i) st[i] -= st0[i];
     const char* rel = getenv("BPSR_SERVER_RELEASE");
     printf("{\"config\": \"cfg3_via_server\", \"driver\": \"native C++ threads "
            "(tools/server_cfg3_native.cpp)\", \"variant\": \"%s\", \"n_workers\": %d, "
@@ -335,14 +338,16 @@ int main(int argc, char** argv) {
            "\"issuer_ms_per_round\": %.4f, \"push_copy_launches_per_round\": %.1f, "
            "\"release\": \"%s\", \"consumer_launches_per_round\": %.2f, "
            "\"key_releases_per_round\": %.1f, \"service_pulls_per_round\": %.1f, "
-           "\"service_launches\": %llu, \"handoff\": \"%s\", \"pulls_agree\": %s}\n",
+           "\"service_launches\": %llu, \"service_pushes_per_round\": %.1f, \"handoff\": \"%s\", "
+           "\"pulls_agree\": %s}\n",
            names[variant], N, np, lanes, total, med * 1e3,
            ts.front() * 1e3, med * 1e6 / np, alg / med / 8e12, push_med * 1e3,
            (double)st[0] / total_rounds, (double)st[1] / total_rounds,
            (double)st[2] / total_rounds, (double)st[4] * 1e-6 / total_rounds,
            (double)st[5] / total_rounds, rel ? rel : "launch", (double)st[6] / total_rounds,
            (double)st[7] / total_rounds, (double)st[8] / total_rounds,
-           (unsigned long long)st[9], cv_handoff ? "condvar" : "spin", same ? "true" : "false");
+           (unsigned long long)st[9], (double)st[10] / total_rounds, cv_handoff ? "condvar" : "spin",
+           same ? "true" : "false");
     fflush(stdout);
     CKR(byteps_server_destroy(srv));
   }
