@@ -77,9 +77,13 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * init round the server builds ONE keyed block queue over every declared key
  * of that key's dtype (each key's receive slots in worker order and its
  * store).  From then on a round's last arrival issues no launch: it stores
- * the key's arrival order and release word — from the host when the pushes
- * are in their slots already (byteps_server_push_ready), or by a one-lane
- * kernel behind the round's copies — and one consumer launch per epoch (the
+ * the key's arrival order and release word from the host when the pushes are
+ * in their slots already (byteps_server_push_ready, or blocking pushes of
+ * device data, which the copy service lands before they arrive).  A round
+ * with pushes still being copied by the lanes (non-blocking pushes, host
+ * data) folds with a lane launch behind its copies, and its key passes the
+ * epoch's consumer with a skip word: the consumer never waits for lane-stream
+ * work.  One consumer launch per epoch (the
  * epoch's first release launches it) folds every key of the queue, each key's
  * tiles as soon as that key is released, in its arrival order (the same bits
  * as the launch path).  Each key's last tile stores the epoch into the key's

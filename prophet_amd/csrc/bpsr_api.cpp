@@ -83,6 +83,8 @@ void make_geom(int dtype, size_t len, const void* dst, const void* const* srcs, 
 // and written by byteps_reduce_set_tuning: launches take a snapshot under the
 // lock, so a concurrent set_tuning never tears a launch's geometry.
 static std::mutex g_tuning_mu;
+thread_local int t_occ_floor = 0;
+thread_local std::atomic<const char*>* t_where = nullptr;
 
 static Tuning& tuning_storage() {
   static Tuning tu = [] {
@@ -189,6 +191,10 @@ struct StageRing {
   int next = 0;
   size_t zero_copy_max = kZeroCopyTable;
   std::vector<char> table;  // host copy of the table being built
+  // Buffers a slot outgrew: freed with the ring, never while it is in use —
+  // hipFree waits for the whole device, and a server lane's issuer must not
+  // wait for a running keyed consumer that waits for the releases it queues.
+  std::vector<void*> retired_host, retired_dev;
   ~StageRing() {
     for (auto& s : slots) {
       if (s.pending && s.done) (void)hipEventSynchronize(s.done);
@@ -196,6 +202,8 @@ struct StageRing {
       if (s.host) (void)hipHostFree(s.host);
       if (s.dev) (void)hipFree(s.dev);
     }
+    for (void* p : retired_host) (void)hipHostFree(p);
+    for (void* p : retired_dev) (void)hipFree(p);
   }
 };
 static thread_local StageRing g_ring;
@@ -214,16 +222,19 @@ static int stage_acquire(StageRing& ring, size_t bytes, StageSlot** out) {
   StageSlot& s = ring.slots[ring.next];
   ring.next = (ring.next + 1) % kRing;
   if (s.pending) {
+    note_where("ring: slot event sync");
     e = hipEventSynchronize(s.done);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize(stage)");
     s.pending = false;
   }
   if (s.device != dev || s.cap < bytes) {
-    if (s.host) (void)hipHostFree(s.host);
-    if (s.dev) (void)hipFree(s.dev);
+    // the outgrown buffers are retired, not freed (see StageRing)
+    if (s.host) ring.retired_host.push_back(s.host);
+    if (s.dev) ring.retired_dev.push_back(s.dev);
     if (s.done) (void)hipEventDestroy(s.done);
     s.host = s.host_dev = s.dev = nullptr;
     s.done = nullptr;
+    note_where("ring: grow");
     // grow geometrically: freeing pinned memory synchronises the device
     const size_t cap = std::max<size_t>({bytes, 2 * s.cap, kZeroCopyTable});
     s.cap = 0;
@@ -415,6 +426,7 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
   std::memcpy(slot->host, ring->table.data(), ti.bytes);
   hipError_t e = hipSuccess;
   const void* table = slot->host_dev;
+  note_where("ring: table copy");
   if (ti.bytes > ring->zero_copy_max) {  // large: one H2D copy, the kernel reads HBM
     e = hipMemcpyAsync(slot->dev, slot->host, ti.bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(batch table)");
@@ -424,8 +436,10 @@ int batched_with_ring(const byteps_bucket_desc* buckets, int nbuckets, int dtype
   // itself, like the block queue's join, made the server's lane issuers see
   // completions sooner and split config 3's rounds into more, smaller
   // launches — 33-43 instead of 23-31 per round at 4 lanes, r03s57.)
+  note_where("ring: kernel launch");
   e = launch_batched(batch_launch(table, ti, table == slot->dev), ti.vpt, dtype, mode,
                      tuning_for_n(ti.nmax), s);
+  note_where("ring: event record");
   if (e != hipSuccess) return hip_fail(e, "batched kernel launch");
   e = hipEventRecord(slot->done, s);
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(stage)");

@@ -171,10 +171,26 @@ inline size_t occ_lds_bytes(int occ) {
 // residency wins (profiles/r01_occ_sweep.jsonl, r01_thr_fold.jsonl: 8 MiB
 // 16.3 -> 14.6 us).  Batched launches (one Prophet block) likewise: the cap
 // measured 9 % slower on cfg3's 13-20 MB blocks (r01_thr_batch.jsonl).
+// Per calling thread: the fewest workgroups per CU a launch may be sized for
+// (0 = no floor).  A PS server lane issuer with device releases sets 4: while
+// a keyed consumer holds 2 × 58 KiB of every CU's LDS waiting for releases,
+// a launch asking for more than the 44 KiB left would never be placed, and
+// the release kernels queued behind it on the lane's stream — or on a stream
+// sharing its hardware queue — would never run (bpsr_server.cpp issuer_main).
+extern thread_local int t_occ_floor;
+// Debug: where a server lane issuer is inside the library's launch helpers
+// (its Lane::where, set by issuer_main; dumped with BPSR_SERVER_RELEASE_DEBUG).
+extern thread_local std::atomic<const char*>* t_where;
+inline void note_where(const char* w) {
+  if (t_where) t_where->store(w, std::memory_order_relaxed);
+}
 inline int launch_occ(const Tuning& tu, uint64_t tiles, bool batched) {
-  if (tu.occ != 1) return tu.occ;
-  if (tiles >= (batched ? tu.occ_min_tiles_batch : tu.occ_min_tiles)) return 1;
-  return batched ? tu.small_occ_batch : tu.small_occ;
+  int o;
+  if (tu.occ != 1) o = tu.occ;
+  else if (tiles >= (batched ? tu.occ_min_tiles_batch : tu.occ_min_tiles)) o = 1;
+  else o = batched ? tu.small_occ_batch : tu.small_occ;
+  if (t_occ_floor > 0 && o > 0 && o < t_occ_floor) o = t_occ_floor;
+  return o;
 }
 // Allow `kernel` to request up to `bytes` of dynamic LDS.  hipFuncSetAttribute
 // acts on the calling thread's current device, so it is applied once PER

@@ -869,10 +869,12 @@ static hipError_t launch_batched_vpt(const BatchLaunch& L, const Tuning& tu, hip
   const void* k[3] = {reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolPlain>),
                       reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolNt>),
                       reinterpret_cast<const void*>(&batched_kernel<Op, VPT, kPolWt>)};
+  note_where("batched: allow_lds");
   for (int i = 0; i < 3; ++i) {
     const hipError_t ok = allow_lds(attr[i], k[i]);
     if (ok != hipSuccess) return ok;
   }
+  note_where("batched: launch");
   if (L.tiles == 0) return hipSuccess;
   const size_t lds = occ_lds_bytes(launch_occ(tu, L.tiles, true));
   switch (cache_pol(tu, (uint64_t)L.tiles * VPT * kBlock * 16)) {

@@ -196,6 +196,7 @@ struct Lane {
   std::deque<Tracked> cq;
   uint64_t issued_seq = 0, done_seq = 0;
   std::atomic<uint64_t> done_pub{0};  // done_seq, readable without done_mu (spinning waiters)
+  std::atomic<const char*> where{"idle"};  // the issuer's step (BPSR_SERVER_RELEASE_DEBUG dumps)
   bool cq_stop = false;
   std::thread completer;
   // copies recorded into copy_mark so far / seen by a fold's wait on it (a
@@ -903,14 +904,19 @@ bool keyed_member(byteps_server* s, KeyState* ks) {
 // block's epoch has been launched (the first release of an epoch launches
 // it).  Then the round is published like an issued fold.  Returns 1 when
 // device releases were turned off meanwhile (the caller folds with a launch).
-int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream) {
+int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
+                bool skip = false) {
   uint32_t perm = 0;
   for (size_t m = 0; m < order.size(); ++m) perm |= (uint32_t)order[m] << (4 * m);
+  if (skip) perm = kKeySkip;
   hipEvent_t ev = nullptr;
   uint64_t seq = 0;
   uint32_t need = 0;
+  Lane& RL = *s->lanes[ks->lane];
+  if (stream) RL.where = "key_release: kq_mu";
   {
     std::lock_guard<std::mutex> g(s->kq_mu);
+    if (stream) RL.where = "key_release: launch";
     if (s->kq_off.load()) return 1;
     uint32_t launched = 0;
     keyq_state(s->kq, ks->kq_key.load(), &need, &launched);
@@ -937,15 +943,19 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
       s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
     }
     if (stream) {
+      RL.where = "key_release: wait d2h";
       // behind the lane's pull copies too (a store is rewritten by the fold)
       const hipError_t we = hipStreamWaitEvent(stream, s->lanes[ks->lane]->d2h_mark, 0);
       if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+      RL.where = "key_release: release kernel";
     }
     if (int rc = keyq_release(s->kq, ks->kq_key.load(), perm, stream)) return rc;
+    if (stream) RL.where = "key_release: publish";
     const int slot = (int)(need % byteps_server::kKqRing);
     ev = s->kq_ev[slot];
     seq = s->kq_ev_seq[slot];
   }
+  if (skip) return 0;  // the round is folded by a lane launch, which publishes it
   s->n_key_releases.fetch_add(1, std::memory_order_relaxed);
   ks->kq_round_epoch = need;
   return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
@@ -962,8 +972,36 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
   {
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (s->kq && keyq_failed(s->kq)) {
-      if (getenv("BPSR_SERVER_RELEASE_DEBUG"))
+      if (getenv("BPSR_SERVER_RELEASE_DEBUG")) {
         fprintf(stderr, "bpsr server: epoch %u timed out: %s\n", epoch, keyq_debug(s->kq).c_str());
+        for (size_t l = 0; l < s->lanes.size(); ++l) {
+          Lane& L = *s->lanes[l];
+          size_t nc = 0, ncp = 0, np = 0;
+          uint64_t iss = 0;
+          {
+            std::lock_guard<std::mutex> dg(L.done_mu);
+            iss = L.issued_seq;
+          }
+          {
+            std::lock_guard<std::mutex> cg(L.comb_mu);
+            nc = L.comb.size();
+            ncp = L.copies.size();
+            np = L.pulls.size();
+          }
+          fprintf(stderr,
+                  "  lane %zu: issued %llu done %llu, queued folds %zu copies %zu pulls %zu, "
+                  "issuer at %s\n",
+                  l, (unsigned long long)iss, (unsigned long long)L.done_pub.load(), nc, ncp, np,
+                  L.where.load());
+        }
+        int rounds_done = 0, pending = 0;
+        for (KeyState* k : s->kq_keys) {
+          if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) ++rounds_done;
+          pending += k->pending;
+        }
+        fprintf(stderr, "  keys released for this epoch %d of %zu, deferred jobs %d\n",
+                rounds_done, s->kq_keys.size(), pending);
+      }
       s->kq_off.store(true);
       for (KeyState* k : s->kq_keys)
         if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
@@ -1228,12 +1266,23 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
         if (rc) fail_key(s, ks, rc);
         return rc;
       }
+    } else {
+      // Copied pushes: the consumer passes this key at once (a SKIP word from
+      // the host) and the round folds with a lane launch behind its copies,
+      // which publishes it.  Releasing it behind the copies instead made the
+      // consumer wait on lane-stream work — which could sit behind launches
+      // the consumer's own residency kept off the chip: with non-blocking
+      // device pushes from 8 threads an epoch never completed (r04s38-s48).
+      const int rc = key_release(s, ks, order, nullptr, /*skip=*/true);
+      if (rc < 0) {
+        fail_key(s, ks, rc);
+        return rc;
+      }
     }
-    // copied pushes (released behind the copies, by the lane issuer), or
-    // device releases turned off meanwhile (an ordinary fold)
+    // copied pushes, or device releases turned off meanwhile: an ordinary fold
     FoldJob j;
     j.ks = ks;
-    j.kind = ks->round_copied ? kKeyRelease : kFinishFused;
+    j.kind = kFinishFused;
     j.acc = order[0];
     j.order = order;
     if (defer) {
@@ -1353,7 +1402,11 @@ int finish_blocking(byteps_server* s, KeyState* ks, std::unique_lock<std::mutex>
 // Issue one deferred round (no batching partner).
 int issue_one(byteps_server* s, FoldJob& j) {
   KeyState* ks = j.ks;
+  Lane& IL = *s->lanes[ks->lane];
+  const char* was = IL.where.load();
+  IL.where = "issue_one: key lock";
   std::lock_guard<std::mutex> g(ks->mu);
+  IL.where = was;
   ks->pending--;
   const int rc = ks->error ? 0 : execute(s, j);
   if (rc) fail_key(s, ks, rc);
@@ -1403,6 +1456,7 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
     hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
     if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
     hipEvent_t last = nullptr;
+    L.where = "copies: key locks";
     for (auto& j : jobs) {  // keyed folds run on the consumer's stream
       std::lock_guard<std::mutex> g(j.ks->mu);
       if (!rc && j.ks->keyed && j.ks->has_done && j.ks->fold_ev != last) {
@@ -1419,9 +1473,11 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
       d[k].n = 1;
     }
     hipEvent_t cev = nullptr;
+    L.where = "copies: launch";
     if (!rc)
       rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
                              BYTEPS_REDUCE_MODE_REFERENCE, L.copy, L.ring, &cev);
+    L.where = "copies: answers";
     if (!rc) {
       s->n_copy_launches.fetch_add(1, std::memory_order_relaxed);
       e = hipEventRecord(L.copy_mark, L.copy);
@@ -1505,6 +1561,10 @@ void issue_pull_copies(byteps_server* s, Lane& L, std::vector<PullJob>& jobs) {
 // up since the last issue.  Drains before it exits.
 void issuer_main(byteps_server* s, int lane) {
   (void)hipSetDevice(s->cfg.device);
+  // with device releases, every launch of this thread fits beside a running
+  // keyed consumer (2 × 58 KiB of each CU's LDS): 4 workgroups' worth per CU
+  if (s->dev_release) t_occ_floor = 4;
+  t_where = &s->lanes[lane]->where;
   Lane& L = *s->lanes[lane];
   std::vector<FoldJob> folds;
   std::vector<CopyJob> copies;
@@ -1519,6 +1579,7 @@ void issuer_main(byteps_server* s, int lane) {
     // device works through them, the rounds completing meanwhile pile up and
     // go out together in the next launch
     lk.unlock();
+    L.where = "window";
     {
       std::unique_lock<std::mutex> dl(L.done_mu);
       L.done_cv.wait(dl, [&] { return L.issued_seq - L.done_seq < s->inflight; });
@@ -1529,13 +1590,17 @@ void issuer_main(byteps_server* s, int lane) {
     pulls.swap(L.pulls);
     lk.unlock();
     const auto t0 = std::chrono::steady_clock::now();
+    L.where = "copies";
     if (!copies.empty()) issue_copies(s, L, copies);  // before the folds that read them
+    L.where = "pulls";
     if (!pulls.empty()) issue_pull_copies(s, L, pulls);  // before folds that rewrite stores
+    L.where = "folds";
     if (folds.size() == 1)
       (void)issue_one(s, folds[0]);
     else if (!folds.empty())
       (void)flush_folds(s, folds);  // a failed fold fails its keys (fail_key)
     folds.clear();
+    L.where = "idle";
     lk.lock();
     if (!L.pulls.empty()) {
       // the pulls parked on the rounds just published go out now, in one

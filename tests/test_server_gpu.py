@@ -1530,15 +1530,18 @@ def _ptr_copy(ptr, src):
 def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     """BPSR_SERVER_RELEASE=device: after the init round one keyed block queue
     folds every key, a round's last push_ready stores the release word (no
-    launch) and copied rounds are released behind their copies.  8 worker
-    threads, keys arriving in a different random order per worker and round
-    (never block order), 3 rounds from the slots (push_ready) and 1 of device
-    pushes; pulls as device views, blocking device copies and host copies.
-    Every pull equals the oracle's left fold in the recorded arrival order;
-    one consumer launch per round, every round released on the device."""
+    launch); blocking device pushes land through the copy service and are
+    released the same way; non-blocking device pushes (lane copies) pass the
+    consumer with a skip word and fold with a lane launch behind their copies.
+    8 worker threads, keys arriving in a different random order per worker and
+    round (never block order), 3 rounds from the slots (push_ready), 1 of
+    blocking device pushes and 1 of non-blocking ones; pulls as device views,
+    blocking device copies and host copies.  Every pull equals the oracle's
+    left fold in the recorded arrival order; one consumer launch per round;
+    lane folds only in the non-blocking round."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
-    N, R = 8, 4
+    N, R = 8, 5
     sizes = [1, 7, 1000, 4096 + 5, 65_536 + 3, 300_001]        # elements per key
     keys = list(range(40, 40 + len(sizes)))
     es = elem_size(dt)
@@ -1565,8 +1568,10 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
                 rng.shuffle(order)
                 for j in order:
                     time.sleep(rng.random() * 0.0005)
-                    if r == 3:                                 # a round of copied pushes
+                    if r == 3:                                 # blocking device pushes
                         srv.push(keys[j], w, src[(w, r, j)], dt)
+                    elif r == 4:                               # non-blocking: lane copies
+                        srv.push_async(keys[j], w, src[(w, r, j)], dt)
                     else:                                      # the transport wrote the slot
                         # (a stream sync, never a device-wide one: the epoch's
                         # consumer is running and waits for this thread's releases)
@@ -1630,9 +1635,9 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     assert not errors, errors
     st = srv.stats()
     srv.close()
-    assert st["key_releases"] == R * len(keys)                  # every round on the device
+    assert st["key_releases"] == (R - 1) * len(keys)   # all but the lane-copied round
     assert st["consumer_launches"] == R                          # one launch per epoch
-    assert st["fold_launches"] - st0["fold_launches"] == 0      # no lane fold launches
+    assert 1 <= st["fold_launches"] - st0["fold_launches"] <= len(keys)  # that round only
 
 
 def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
@@ -1640,7 +1645,9 @@ def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     round in which one key is never pushed makes that epoch's consumer give up
     after BPSR_SERVER_RELEASE_TIMEOUT_S: the key released in it fails with
     ETIMEOUT (no stale data), the server turns device releases off, and the
-    late key's round then folds with a launch, exactly."""
+    late key's round then folds with a launch, exactly.  Rounds 0-1 are
+    copied pushes (host data): they fold with lane launches while the
+    consumer passes their keys."""
     from prophet_amd.reducer import ETIMEOUT, ReduceError
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
@@ -1659,8 +1666,17 @@ def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     for k in (1, 2):
         for w in range(N):
             srv.pull(k, out)
-    for w in range(N):                                   # round 2: key 1 only
-        srv.push(1, w, data(dt, n, w, 2, 1), dt)
+    # round 2: key 1 only, written into its slots by the "transport" and
+    # released from the host (push_ready) — a device-released round; key 2
+    # never comes.  (Copied pushes would fold with a lane launch and pass the
+    # consumer with a skip word, so they could not show the timeout.)
+    dev = torch.device("cuda:0")
+    for w in range(N):
+        x = torch.from_numpy(data(dt, n, w, 2, 1)).to(dev)
+        _ptr_copy(srv.recv_slot(1, w), x)
+        torch.cuda.current_stream(dev).synchronize()   # before the epoch opens
+    for w in range(N):
+        srv.push_ready(1, w)
     with pytest.raises(ReduceError) as e:
         srv.pull(1, out)
     assert e.value.code == ETIMEOUT
