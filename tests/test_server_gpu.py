@@ -1635,9 +1635,13 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     assert not errors, errors
     st = srv.stats()
     srv.close()
-    assert st["key_releases"] == (R - 1) * len(keys)   # all but the lane-copied round
+    # lane-copied rounds fold with launches (the non-blocking round; also the
+    # blocking-push round when BPSR_SERVER_PULL_SERVICE=0 takes the service away)
+    import os
+    copied = 1 if os.environ.get("BPSR_SERVER_PULL_SERVICE", "1") != "0" else 2
+    assert st["key_releases"] == (R - copied) * len(keys)
     assert st["consumer_launches"] == R                          # one launch per epoch
-    assert 1 <= st["fold_launches"] - st0["fold_launches"] <= len(keys)  # that round only
+    assert 1 <= st["fold_launches"] - st0["fold_launches"] <= copied * len(keys)
 
 
 def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
