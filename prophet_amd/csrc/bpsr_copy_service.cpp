@@ -224,7 +224,10 @@ int wait_job(CopyService* c, uint64_t j, int64_t t0) {
   }
 }
 
-int copysvc_copy(CopyService* c, void* dst, const void* src, size_t len) {
+int copysvc_post(CopyService* c, void* dst, const void* src, size_t len, uint64_t* first_out,
+                 uint64_t* n_out) {
+  *first_out = 0;
+  *n_out = 0;
   if (len == 0) return 0;
   if (((reinterpret_cast<uint64_t>(dst) + len) | (reinterpret_cast<uint64_t>(src) + len)) > kSvcMask)
     return fail(BYTEPS_REDUCE_EARGS, "copy service: address beyond 48 bits");
@@ -253,6 +256,49 @@ int copysvc_copy(CopyService* c, void* dst, const void* src, size_t len) {
       return rc;
     }
   }
+  *first_out = first;
+  *n_out = n;
+  return 0;
+}
+
+int copysvc_test(CopyService* c, uint64_t first, uint64_t n, int64_t posted_ns, bool* done) {
+  *done = false;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t j = first + i;
+    if (job_done(c, j)) continue;
+    // not yet: past kCheckUs since posting, make sure a launch is serving
+    const int64_t now = now_ns();
+    if (now - posted_ns > kCheckUs * 1000ll) {
+      std::lock_guard<std::mutex> g(c->mu);
+      if (job_done(c, j)) continue;
+      if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+      if (!svc_alive(c)) {
+        const int rc = svc_launch(c);
+        if (rc) {
+          c->broken.store(true);
+          return rc;
+        }
+      }
+      if (now - posted_ns > kTimeoutMs * 1000000ll) {
+        c->broken.store(true);
+        __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
+        return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
+                    (unsigned long long)j, kTimeoutMs);
+      }
+    }
+    return 0;
+  }
+  *done = true;
+  return 0;
+}
+
+int64_t copysvc_now_ns() { return now_ns(); }
+
+int copysvc_copy(CopyService* c, void* dst, const void* src, size_t len) {
+  uint64_t first = 0, n = 0;
+  const int64_t t0 = now_ns();
+  int rc = copysvc_post(c, dst, src, len, &first, &n);
+  if (rc) return rc;
   for (uint64_t i = 0; i < n; ++i)
     if ((rc = wait_job(c, first + i, t0))) return rc;
   return 0;

@@ -343,6 +343,13 @@ int copysvc_create(int device, CopyService** out);
 // service; returns once the bytes are visible to later work on the device.
 int copysvc_copy(CopyService* svc, void* dst, const void* src, size_t len);
 void copysvc_destroy(CopyService* svc);
+// Non-blocking form: post the copy (jobs [*first, *first + *n)), then test
+// it; copysvc_test keeps the service serving (relaunch, timeout) like a
+// blocking copy's wait.  `posted_ns` = copysvc_now_ns() taken before posting.
+int copysvc_post(CopyService* svc, void* dst, const void* src, size_t len, uint64_t* first,
+                 uint64_t* n);
+int copysvc_test(CopyService* svc, uint64_t first, uint64_t n, int64_t posted_ns, bool* done);
+int64_t copysvc_now_ns();
 uint64_t copysvc_launches(CopyService* svc);  // kernel launches so far (0 for null)
 // A job timed out or a launch failed: the service takes no more jobs (its
 // callers use another copy path from then on).
