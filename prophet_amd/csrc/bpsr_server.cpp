@@ -287,6 +287,27 @@ struct KeyState {
 }  // namespace
 }  // namespace bpsr
 
+// A counter bumped by every per-key call: sharded over cache lines by
+// calling thread, so receive threads do not bounce one line per call.
+struct ShardedCount {
+  static constexpr int kShards = 16;
+  struct alignas(64) Slot {
+    std::atomic<uint64_t> v{0};
+  };
+  Slot slot[kShards];
+  static int shard() {
+    static std::atomic<int> next{0};
+    thread_local const int mine = next.fetch_add(1, std::memory_order_relaxed) % kShards;
+    return mine;
+  }
+  void add(uint64_t n = 1) { slot[shard()].v.fetch_add(n, std::memory_order_relaxed); }
+  uint64_t load() const {
+    uint64_t t = 0;
+    for (const Slot& x : slot) t += x.v.load(std::memory_order_relaxed);
+    return t;
+  }
+};
+
 struct byteps_server {
   byteps_server_config cfg;
   bool schedule = false;
@@ -297,8 +318,9 @@ struct byteps_server {
   bool combine = true;
   uint64_t inflight = 2;  // issuer: launches queued or running per lane (BPSR_SERVER_INFLIGHT)
   // telemetry (byteps_server_stats)
-  std::atomic<uint64_t> n_fold_launches{0}, n_rounds_folded{0}, n_pull_launches{0},
-      n_pulls{0}, issuer_ns{0}, n_copy_launches{0};
+  std::atomic<uint64_t> n_fold_launches{0}, n_pull_launches{0}, issuer_ns{0},
+      n_copy_launches{0};
+  ShardedCount n_rounds_folded, n_pulls;
   std::vector<std::unique_ptr<bpsr::Lane>> lanes;
   // every call looks its key up; keys are added once: lookups share the lock
   std::shared_mutex map_mu;
@@ -351,7 +373,8 @@ struct byteps_server {
   uint32_t kq_ev_epoch[kKqRing] = {};
   uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
   std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
-  std::atomic<uint64_t> n_consumer_launches{0}, n_key_releases{0};
+  std::atomic<uint64_t> n_consumer_launches{0};
+  ShardedCount n_key_releases;
   // Blocking pulls into this device's memory (combine path): served by the
   // pull copy service, created on first use (BPSR_SERVER_PULL_SERVICE=0: the
   // lane issuers' batched copies instead).
@@ -814,7 +837,7 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
                  bool mark = true, hipEvent_t batch = nullptr, uint64_t batch_seq = 0,
                  bool keyed = false) {
   Lane& L = *s->lanes[ks->lane];
-  s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
+  s->n_rounds_folded.add();
   ks->keyed = keyed;  // a keyed consumer's fold, tracked by the keyed completer
   ks->fold_lane = keyed ? -1 : ks->lane;
   ks->round_copied = false;
@@ -956,7 +979,7 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
     seq = s->kq_ev_seq[slot];
   }
   if (skip) return 0;  // the round is folded by a lane launch, which publishes it
-  s->n_key_releases.fetch_add(1, std::memory_order_relaxed);
+  s->n_key_releases.add();
   ks->kq_round_epoch = need;
   return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
 }
@@ -1079,7 +1102,7 @@ int execute(byteps_server* s, const FoldJob& j) {
     case kAsyncSum: {  // server.cc:220-230: every push is summed straight into the store
       rc = byteps_reduce_sum(ks->store, ks->slot[j.w], ks->len, ks->dtype, fs);
       if (rc) return rc;
-      s->n_rounds_folded.fetch_add(1, std::memory_order_relaxed);
+      s->n_rounds_folded.add();
       hipError_t e = hipEventRecord(ks->done, L.fold);
       if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
       if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -1538,7 +1561,7 @@ void issue_pull_copies(byteps_server* s, Lane& L, std::vector<PullJob>& jobs) {
       if (!rc && cev) seq = track(L, cev);
     }
   }
-  s->n_pulls.fetch_add(jobs.size(), std::memory_order_relaxed);
+  s->n_pulls.add(jobs.size());
   for (auto& j : jobs) {
     if (j.direct) {  // a blocking pull waits on the lane itself, then counts
       j.direct->lane = &L;
@@ -2015,7 +2038,7 @@ int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, si
   if (int rc = wait_order_gate(s)) return rc;
   int rc = copysvc_copy(svc, out, store, len);
   if (rc) return rc;
-  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
+  s->n_pulls.add();
   s->n_service_pulls.fetch_add(1, std::memory_order_relaxed);
   lk.lock();
   count_pull(s, ks);
@@ -2302,7 +2325,7 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
     lk.lock();
     if (ks->error) return key_error(ks);
   }
-  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
+  s->n_pulls.add();
   s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
   // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
@@ -2416,7 +2439,7 @@ int byteps_server_pull_device_view(byteps_server* s, uint64_t key, const void** 
     lk.lock();
   }
   if (ks->error) return key_error(ks);  // a keyed epoch that timed out
-  s->n_pulls.fetch_add(1, std::memory_order_relaxed);
+  s->n_pulls.add();
   count_pull(s, ks);  // server.cc:105-113: after NumWorkers pulls the key re-arms
   *data = view;
   if (len) *len = ks->len;
@@ -2741,7 +2764,7 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
     std::lock_guard<std::mutex> g(ks_of[i]->mu);
     count_pull(s, ks_of[i]);  // server.cc:105-113
   }
-  s->n_pulls.fetch_add((uint64_t)n, std::memory_order_relaxed);
+  s->n_pulls.add((uint64_t)n);
   return BYTEPS_REDUCE_OK;
 }
 
