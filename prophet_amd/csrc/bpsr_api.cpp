@@ -1169,30 +1169,30 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16),
                     kKeyedLds, true, q->dtype, q->mode, own);
   if (e != hipSuccess) return hip_fail(e, "keyed queue launch");
-  q->launch_epoch = ep;
+  __atomic_store_n(&q->launch_epoch, ep, __ATOMIC_RELEASE);
   if (stream) *stream = own;
   if (epoch) *epoch = ep;
   return BYTEPS_REDUCE_OK;
 }
 
+// A key's release epoch is written only by its releaser (the server
+// serialises a key's rounds) and the launch epoch only by keyq_launch (under
+// q->mu): both are read lock-free, so releases of different keys from many
+// receive threads share no lock.
 uint32_t keyq_next_epoch(byteps_reduce_blockq* q, int key) {
-  std::lock_guard<std::mutex> g(q->mu);
-  return q->rel_epoch[(size_t)key] + 1;
+  return __atomic_load_n(&q->rel_epoch[(size_t)key], __ATOMIC_ACQUIRE) + 1;
 }
 
 uint32_t keyq_launched(byteps_reduce_blockq* q) {
-  std::lock_guard<std::mutex> g(q->mu);
-  return q->launch_epoch;
+  return __atomic_load_n(&q->launch_epoch, __ATOMIC_ACQUIRE);
 }
 
 void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched) {
-  std::lock_guard<std::mutex> g(q->mu);
-  *next_epoch = q->rel_epoch[(size_t)key] + 1;
-  *launched = q->launch_epoch;
+  *next_epoch = keyq_next_epoch(q, key);
+  *launched = keyq_launched(q);
 }
 
 int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s) {
-  std::lock_guard<std::mutex> g(q->mu);
   const uint32_t ep = q->rel_epoch[(size_t)key] + 1;
   const uint64_t w = key_word(perm, ep);
   if (s) {
@@ -1201,7 +1201,7 @@ int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s)
   } else {
     __atomic_store_n(q->khwords + 2 * (size_t)key + (ep & 1u), w, __ATOMIC_RELEASE);
   }
-  q->rel_epoch[(size_t)key] = ep;
+  __atomic_store_n(&q->rel_epoch[(size_t)key], ep, __ATOMIC_RELEASE);
   return BYTEPS_REDUCE_OK;
 }
 

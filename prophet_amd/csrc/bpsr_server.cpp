@@ -372,6 +372,7 @@ struct byteps_server {
   uint64_t kq_ev_seq[kKqRing] = {};     // lane-0 seq of that launch
   uint32_t kq_ev_epoch[kKqRing] = {};
   uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
+  std::atomic<uint32_t> kq_pub_epoch{0};  // epochs launched with their kq_ev slot written
   std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
   std::atomic<uint64_t> n_consumer_launches{0};
   ShardedCount n_key_releases;
@@ -934,15 +935,30 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
   if (skip) perm = kKeySkip;
   hipEvent_t ev = nullptr;
   uint64_t seq = 0;
-  uint32_t need = 0;
+  const int kk = ks->kq_key.load();
+  uint32_t need = keyq_next_epoch(s->kq, kk);
   Lane& RL = *s->lanes[ks->lane];
-  if (stream) RL.where = "key_release: kq_mu";
-  {
+  if (!s->kq_off.load() && s->kq_pub_epoch.load(std::memory_order_acquire) >= need) {
+    // the epoch's consumer is launched and its slot published: no lock (the
+    // slot cannot be reused before this epoch completes, which needs this key)
+    const int slot = (int)(need % byteps_server::kKqRing);
+    ev = s->kq_ev[slot];
+    seq = s->kq_ev_seq[slot];
+    if (stream) {
+      RL.where = "key_release: wait d2h";
+      // behind the lane's pull copies too (a store is rewritten by the fold)
+      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
+      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+      RL.where = "key_release: release kernel";
+    }
+    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
+  } else {
+    if (stream) RL.where = "key_release: kq_mu";
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (stream) RL.where = "key_release: launch";
     if (s->kq_off.load()) return 1;
     uint32_t launched = 0;
-    keyq_state(s->kq, ks->kq_key.load(), &need, &launched);
+    keyq_state(s->kq, kk, &need, &launched);
     for (; launched < need; launched = keyq_launched(s->kq)) {
       const uint32_t next = launched + 1;
       const int slot = (int)(next % byteps_server::kKqRing);
@@ -964,20 +980,20 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
       s->kq_ev_epoch[slot] = got;
       s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
       s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
+      s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
     }
     if (stream) {
       RL.where = "key_release: wait d2h";
-      // behind the lane's pull copies too (a store is rewritten by the fold)
-      const hipError_t we = hipStreamWaitEvent(stream, s->lanes[ks->lane]->d2h_mark, 0);
+      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
       if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
       RL.where = "key_release: release kernel";
     }
-    if (int rc = keyq_release(s->kq, ks->kq_key.load(), perm, stream)) return rc;
-    if (stream) RL.where = "key_release: publish";
+    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
     const int slot = (int)(need % byteps_server::kKqRing);
     ev = s->kq_ev[slot];
     seq = s->kq_ev_seq[slot];
   }
+  if (stream) RL.where = "key_release: publish";
   if (skip) return 0;  // the round is folded by a lane launch, which publishes it
   s->n_key_releases.add();
   ks->kq_round_epoch = need;
