@@ -75,7 +75,9 @@ KERNEL_SIG = "prophet_amd/libbpsr.fold_f32_8.sig"
 KERNEL_SOURCES = ("prophet_amd/csrc/bpsr_kernels_impl.h", "prophet_amd/csrc/bpsr_ops.h",
                   "prophet_amd/csrc/bpsr_internal.h", "prophet_amd/csrc/bpsr_k_f32.hip")
 KERNEL_SOURCE_SPANS = (("prophet_amd/csrc/bpsr_api.cpp", "static Tuning& tuning_storage()",
-                        "static inline hipStream_t to_stream"),)
+                        "static inline hipStream_t to_stream"),
+                       ("prophet_amd/csrc/bpsr_internal.h", "inline size_t occ_lds_bytes",
+                        "// The 1-workgroup-per-CU cap pays"))
 
 
 def parse(argv=None):

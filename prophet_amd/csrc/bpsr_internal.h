@@ -163,8 +163,12 @@ struct Tuning {
 // CU.  Fewer bytes in flight per CU stream HBM better for the 9-stream fold
 // (tools/hbm_probe2.hip).
 constexpr size_t kLdsPerCU = 160 * 1024;
+// Dynamic LDS that caps a launch at `occ` workgroups per CU.  1 KiB short of
+// the even share: the same residency (occ + 1 workgroups never fit), and room
+// beside them for kernels with almost no LDS that must still get onto every
+// CU — the server's copy service and release kernels.
 inline size_t occ_lds_bytes(int occ) {
-  return occ > 0 ? (kLdsPerCU / (size_t)occ) & ~(size_t)255 : 0;
+  return occ > 0 ? ((kLdsPerCU / (size_t)occ) - 1024) & ~(size_t)255 : 0;
 }
 // The 1-workgroup-per-CU cap pays on long sweeps only: below occ_min_tiles
 // tiles (4096: 32 MiB per source at vpt 2) a launch is latency-bound and more
