@@ -29,7 +29,9 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -74,6 +76,37 @@ struct CopyService {
 };
 
 namespace {
+
+// Live services.  A process that exits without destroying its server must not
+// leave a service kernel polling pinned host memory the runtime is about to
+// unmap: an exit handler, registered after the runtime's own state exists
+// (so it runs before the runtime's teardown), stops every live service and
+// waits for its kernel.
+std::mutex g_live_mu;
+std::set<CopyService*>* g_live = nullptr;
+
+void stop_live_services() {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (!g_live) return;
+  for (CopyService* c : *g_live) {
+    if (c->stop) __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
+    if (c->running.load()) (void)hipEventSynchronize(c->ev);
+  }
+}
+
+void register_live(CopyService* c) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (!g_live) {
+    g_live = new std::set<CopyService*>();
+    std::atexit(stop_live_services);
+  }
+  g_live->insert(c);
+}
+
+void unregister_live(CopyService* c) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (g_live) g_live->erase(c);
+}
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -174,12 +207,14 @@ int copysvc_create(int device, CopyService** out) {
     copysvc_destroy(c);
     return rc;
   }
+  register_live(c);
   *out = c;
   return 0;
 }
 
 void copysvc_destroy(CopyService* c) {
   if (!c) return;
+  unregister_live(c);
   if (c->stop) __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
   if (c->running.load()) (void)hipEventSynchronize(c->ev);  // exits within one poll
   if (c->stream) (void)hipStreamSynchronize(c->stream);
