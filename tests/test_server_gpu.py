@@ -1521,6 +1521,37 @@ def test_copy_service_many_rounds_racing_pullers(port):
     assert st["service_launches"] >= 2
 
 
+def test_service_push_waits_for_running_producer():
+    """A blocking device push served by the copy service (no stream of the
+    server's is involved) still honours the order_after event PSServer hands
+    over: the producer still running on the caller's stream (a long spin, then
+    the fill) lands before the service copies the data, and the round folds
+    the filled values."""
+    from prophet_amd.server import PSServer
+    dt, N, n = DType.FLOAT32, 2, 1 << 20
+    srv = PSServer(N)
+    dev = torch.device("cuda:0")
+    xs = [torch.zeros(n, device=dev) for _ in range(N)]
+    torch.cuda.synchronize()
+    ts = [threading.Thread(target=srv.push, args=(9, w, xs[w], dt)) for w in range(N)]
+    for t in ts:                                         # init round
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(200_000_000)                      # ~0.1 s on the current stream
+    xs[0].fill_(1.5)
+    xs[1].fill_(2.25)
+    srv.push(9, 0, xs[0], dt)                            # blocking: through the service
+    srv.push(9, 1, xs[1], dt)
+    out = torch.empty(n, device=dev)
+    srv.pull(9, out)
+    st = srv.stats()
+    srv.close()
+    assert st["service_pushes"] >= 2
+    assert torch.all(out == 3.75)
+
+
 def _ptr_copy(ptr, src):
     from prophet_amd.reducer import GpuReducer
     GpuReducer().copy(ptr, src, src.numel() * src.element_size())
