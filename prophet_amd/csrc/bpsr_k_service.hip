@@ -76,8 +76,14 @@ __device__ __forceinline__ void copy_plain(unsigned char* dst, const unsigned ch
 // moves the consecutive run of posted jobs it finds into the device ring
 // (tagged words: no ordering needed), and decides the exit.
 __device__ void fetcher(const SvcArgs& a) {
-  if (threadIdx.x >= 64) return;
-  const uint32_t l = threadIdx.x;
+  // kPollers waves poll the same ring half a round trip apart, so a posted
+  // job is seen sooner; moving a job twice writes the same tagged words.
+  // Wave 0 decides the exit; the others follow the exit word.
+  constexpr uint32_t kPollers = 2;
+  if (threadIdx.x >= 64 * kPollers) return;
+  const uint32_t wave = threadIdx.x / 64;
+  const uint32_t l = threadIdx.x % 64;
+  if (wave) __builtin_amdgcn_s_sleep(12);
   uint32_t kWin = 8;
   uint64_t seen = a.start;  // jobs below are in the device ring (or were never this launch's)
   const uint64_t t_begin = wall_clock64();
@@ -111,6 +117,11 @@ __device__ void fetcher(const SvcArgs& a) {
       continue;
     }
     kWin = 8;
+    if (wave) {
+      if (ld_dev64(a.dev + 2)) return;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
     const uint32_t stop = __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const bool drained = a.start + ld_dev64(a.dev + 1) >= seen;
     if (stop || now - t_begin > a.max_ticks || (drained && now - t_idle > a.idle_ticks)) {
