@@ -2006,6 +2006,15 @@ const void* service_src(byteps_server* s, const void* data, size_t len, int loca
     return nullptr;
   return on_this_device(s, data) ? data : nullptr;
 }
+// A service copy that failed because the service gave up (a job not served
+// in time): the same bytes through the key lane's d2h stream instead, so the
+// call still completes (later calls take the lanes: service_get).
+int fallback_copy(byteps_server* s, KeyState* ks, void* dst, const void* src, size_t len) {
+  Lane& L = *s->lanes[ks->lane];
+  hipError_t e = hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToDevice, L.d2h);
+  if (e == hipSuccess) e = hipStreamSynchronize(L.d2h);
+  return e == hipSuccess ? 0 : hip_fail(e, "copy (after the copy service gave up)");
+}
 // The events given to byteps_server_order_after so far, waited for on the
 // host before a service copy (the service copies on no stream of ours).
 int wait_order_gate(byteps_server* s) {
@@ -2053,9 +2062,10 @@ int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, si
   lk.unlock();
   if (int rc = wait_order_gate(s)) return rc;
   int rc = copysvc_copy(svc, out, store, len);
+  if (rc && copysvc_broken(svc)) rc = fallback_copy(s, ks, out, store, len);
+  else if (!rc) s->n_service_pulls.fetch_add(1, std::memory_order_relaxed);
   if (rc) return rc;
   s->n_pulls.add();
-  s->n_service_pulls.fetch_add(1, std::memory_order_relaxed);
   lk.lock();
   count_pull(s, ks);
   return BYTEPS_REDUCE_OK;
@@ -2093,7 +2103,9 @@ int service_push(byteps_server* s, CopyService* svc, uint64_t key, int worker, c
   }
   lk.unlock();
   if ((rc = wait_order_gate(s))) return rc;  // the data's producer on the caller's stream
-  if ((rc = copysvc_copy(svc, ks->slot[worker], src, len))) return rc;
+  if ((rc = copysvc_copy(svc, ks->slot[worker], src, len)) && copysvc_broken(svc))
+    rc = fallback_copy(s, ks, ks->slot[worker], src, len);
+  if (rc) return rc;
   s->n_service_pushes.fetch_add(1, std::memory_order_relaxed);
   lk.lock();
   if (ks->error) return key_error(ks);
