@@ -73,6 +73,8 @@ struct CopyService {
   std::mutex mu;
   uint64_t scan_from = 0;               // under mu: every job below is done
   std::atomic<uint64_t> launches{0};
+  int timeout_ms = kTimeoutMs;
+  bool stall = false;  // tests only (BPSR_COPYSVC_TEST_STALL_MS): copiers serve nothing
 };
 
 namespace {
@@ -150,6 +152,7 @@ int svc_launch(CopyService* c) {
   a.idle_ticks = c->idle_ticks;
   a.max_ticks = c->max_ticks;
   a.wgs = kSvcWgs;
+  a.stall = c->stall ? 1u : 0u;
   hipError_t e = hipMemsetAsync(c->dev, 0, 4 * sizeof(uint64_t), c->stream);
   if (e == hipSuccess) e = launch_copy_service(a, c->stream);
   if (e == hipSuccess) e = hipEventRecord(c->ev, c->stream);
@@ -173,6 +176,12 @@ int copysvc_create(int device, CopyService** out) {
                            : fail(BYTEPS_REDUCE_EHIP, "copy service: no wall clock rate");
   }
   c->idle_ticks = (uint64_t)khz * kIdleUs / 1000;
+  // tests of the give-up path: a service whose copiers serve nothing, and a
+  // short give-up time
+  if (const char* v = getenv("BPSR_COPYSVC_TEST_STALL_MS")) {
+    c->stall = true;
+    c->timeout_ms = std::max(1, atoi(v));
+  }
   c->max_ticks = (uint64_t)khz * kMaxMs;
   int prio_lo = 0, prio_hi = 0;
   e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
@@ -249,11 +258,11 @@ int wait_job(CopyService* c, uint64_t j, int64_t t0) {
           return rc;
         }
       }
-      if (now - t0 > kTimeoutMs * 1000000ll) {
+      if (now - t0 > c->timeout_ms * 1000000ll) {
         c->broken.store(true);
         __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
         return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
-                    (unsigned long long)j, kTimeoutMs);
+                    (unsigned long long)j, c->timeout_ms);
       }
     }
   }
@@ -314,11 +323,11 @@ int copysvc_test(CopyService* c, uint64_t first, uint64_t n, int64_t posted_ns, 
           return rc;
         }
       }
-      if (now - posted_ns > kTimeoutMs * 1000000ll) {
+      if (now - posted_ns > c->timeout_ms * 1000000ll) {
         c->broken.store(true);
         __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
         return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
-                    (unsigned long long)j, kTimeoutMs);
+                    (unsigned long long)j, c->timeout_ms);
       }
     }
     return 0;

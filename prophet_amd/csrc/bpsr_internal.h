@@ -336,6 +336,7 @@ struct SvcArgs {
   uint64_t idle_ticks;     // exit after this long without a new job ...
   uint64_t max_ticks;      // ... or once this launch is this old (a relaunch takes over)
   uint32_t wgs;            // fetcher + copiers
+  uint32_t stall;          // tests only: copiers serve no job (the give-up path)
   uint64_t* trace;         // probes only (null in the product): per slot, wall clock at
                            // [0] fetched, [1] picked up, [2] copied and drained
 };

@@ -145,7 +145,7 @@ __device__ void copier(const SvcArgs& a) {
       uint32_t st = 0;
       for (;;) {
         const uint64_t w0 = ld_dev64(dw + 0), w1 = ld_dev64(dw + 1), w2 = ld_dev64(dw + 2);
-        if ((w0 >> 48) == tag && (w1 >> 48) == tag && (w2 >> 48) == tag) {
+        if (!a.stall && (w0 >> 48) == tag && (w1 >> 48) == tag && (w2 >> 48) == tag) {
           s_job[0] = w0 & kSvcMask;
           s_job[1] = w1 & kSvcMask;
           s_job[2] = w2 & kSvcMask;

@@ -1446,6 +1446,56 @@ def test_blocking_device_pulls_through_copy_service(port, service, monkeypatch):
     assert len(stream_s) == len(keys) and sorted(stream_s)[len(keys) // 2] < 0.05, stream_s
 
 
+def test_copy_service_give_up_falls_back_to_lane_copies(port, monkeypatch):
+    """The copy service's give-up path: with BPSR_COPYSVC_TEST_STALL_MS the
+    service's copiers serve nothing and a job is given up after that many ms.
+    The pull that met the stalled service still completes, through the key's
+    lane stream, and every later pull goes to lane copies directly; every
+    pulled byte equals the oracle's left fold."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_PULL_SERVICE", "1")
+    monkeypatch.setenv("BPSR_COPYSVC_TEST_STALL_MS", "100")
+    dt, N, R = DType.FLOAT32, 2, 3
+    sizes = [1, 1001, 300_007]
+    keys = list(range(140, 140 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=2)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    acks = threading.Semaphore(0)
+
+    def push_all(r, j, k):       # a blocking push may wait for the other workers'
+        for w in range(N):
+            srv.push_async(k, w, src[(w, r, j)], dt, lambda kk, ww, st: acks.release())
+        for _ in range(N):
+            assert acks.acquire(timeout=30)
+
+    for j, k in enumerate(keys):
+        push_all(0, j, k)                                       # init round
+    first_s = None
+    for r in range(1, R + 1):
+        for j, k in enumerate(keys):
+            push_all(r, j, k)
+            _, _, order = srv.key_info(k)
+            want = np.zeros(sizes[j] * es, np.uint8)
+            port.sum_n(want, [data(dt, sizes[j], w, r, j) for w in order], sizes[j] * es, dt)
+            for w in range(N):
+                out = torch.full((sizes[j],), -1.0, device=dev)
+                t0 = time.perf_counter()
+                srv.pull(k, out)
+                if first_s is None:
+                    first_s = time.perf_counter() - t0
+                assert_bytes_match(dt, out.cpu().numpy().view(np.uint8), want,
+                                   nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
+    st = srv.stats()
+    srv.close()
+    assert first_s >= 0.09, first_s                            # the first pull met the stall
+    assert st["service_pulls"] == 0 and st["service_launches"] >= 1
+    assert st["pulls"] == N * R * len(keys)
+
+
 def test_copy_service_many_rounds_racing_pullers(port):
     """The pull copy service under load: 4 worker threads, 24 keys of random
     sizes (1 element … 700 K fp32, so jobs of 1 … 11 chunks), 12 rounds; each
