@@ -70,7 +70,9 @@ int main() {
           std::vector<double> f, cpy;
           for (uint64_t j = p0 + 20 * T; j < p1; ++j) {
             const uint64_t* t = &tr[(j % bpsr::kSvcRing) * 4];
-            f.push_back((double)(t[1] - t[0]) * 1e3 / khz);
+            // signed: both polling waves stamp [0], so the later one may land
+            // after the copier picked the job up (a negative gap, not a wrap)
+            f.push_back((double)(int64_t)(t[1] - t[0]) * 1e3 / khz);
             cpy.push_back((double)(t[2] - t[1]) * 1e3 / khz);
           }
           std::sort(f.begin(), f.end());
