@@ -49,6 +49,11 @@
 extern "C" {
 #endif
 
+/* Only the declarations below leave libbpsr.so: it is compiled with
+ * -fvisibility=hidden and linked with the reference's export policy
+ * (byteps.lds:1-8, global: *byteps*; local: *). */
+#pragma GCC visibility push(default)
+
 typedef struct byteps_prophet_config {
   int64_t batch_size;           /* Z_BATCH_SIZE                                     */
   int64_t net_b;                /* Z_NET_B (multiplied by 125, :27)                 */
@@ -218,6 +223,8 @@ int byteps_prophet_loop_end(byteps_prophet_loop* l, double timeout_s);
  * since create: telemetry for how many groups went out together. */
 int byteps_prophet_loop_release_calls(byteps_prophet_loop* l, uint64_t* calls);
 int byteps_prophet_loop_destroy(byteps_prophet_loop* l);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

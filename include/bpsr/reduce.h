@@ -49,6 +49,11 @@
 extern "C" {
 #endif
 
+/* Only the declarations below leave libbpsr.so: it is compiled with
+ * -fvisibility=hidden and linked with the reference's export policy
+ * (byteps.lds:1-8, global: *byteps*; local: *). */
+#pragma GCC visibility push(default)
+
 /* 3: byteps_server_config.engine_blocking; bpsr/shard.h */
 #define BYTEPS_REDUCE_ABI_VERSION 3
 
@@ -256,6 +261,8 @@ const char* byteps_reduce_last_error(void);
  * environment: BPSR_VPT, BPSR_NT, BPSR_MAX_GRID, BPSR_OCC. */
 int byteps_reduce_set_tuning(int vpt, int nt, int max_grid, int occ);
 int byteps_reduce_get_tuning(int* vpt, int* nt, int* max_grid, int* occ);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,11 @@
 extern "C" {
 #endif
 
+/* Only the declarations below leave libbpsr.so: it is compiled with
+ * -fvisibility=hidden and linked with the reference's export policy
+ * (byteps.lds:1-8, global: *byteps*; local: *). */
+#pragma GCC visibility push(default)
+
 enum byteps_server_policy { BYTEPS_SERVER_FUSED = 0, BYTEPS_SERVER_INCREMENTAL = 1 };
 enum byteps_server_location { BYTEPS_SERVER_HOST = 0, BYTEPS_SERVER_DEVICE = 1 };
 
@@ -385,6 +390,8 @@ int byteps_server_group_pull_many(byteps_server_group* g, const uint64_t* keys,
  * instance). */
 int byteps_server_group_order_after(byteps_server_group* g, const uint64_t* keys, int n,
                                     void* event);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

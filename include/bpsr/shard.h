@@ -68,6 +68,11 @@
 extern "C" {
 #endif
 
+/* Only the declarations below leave libbpsr.so: it is compiled with
+ * -fvisibility=hidden and linked with the reference's export policy
+ * (byteps.lds:1-8, global: *byteps*; local: *). */
+#pragma GCC visibility push(default)
+
 #define BYTEPS_SHARD_UNIQUE_ID_BYTES 128 /* sizeof(ncclUniqueId) */
 
 typedef struct byteps_shard_comm byteps_shard_comm;
@@ -129,6 +134,8 @@ int byteps_shard_reduce_root(byteps_shard_comm* comm, int root, const void* loca
 /* Whole-vector broadcast from `root` into every rank's `buf` (in place). */
 int byteps_shard_broadcast(byteps_shard_comm* comm, int root, void* buf, size_t elems, int dtype,
                            void* stream);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

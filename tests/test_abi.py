@@ -37,12 +37,40 @@ def test_library_exports_every_header_symbol():
     lib = reducer.load_library()
     for name in header_functions():
         assert hasattr(lib, name), name
+
+def test_library_exports_nothing_but_the_header_api():
+    """The reference's export policy (byteps.lds:1-8, global: *byteps*;
+    local: *, passed by setup.py:207): EVERY defined dynamic symbol of
+    libbpsr.so -- functions, data, vtables, typeinfo, template instantiations,
+    kernel host stubs -- is one of the C functions include/bpsr/*.h declares.
+    Nothing from bpsr:: or libstdc++ joins the global scope of a process that
+    loads the library RTLD_GLOBAL (byteps/server/__init__.py:22-23)."""
     out = subprocess.run(["nm", "-D", "--defined-only", reducer.LIB_PATH],
                          capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r"\bT (byteps_\w+)", out))
-    assert set(header_functions()) <= exported
-    # every exported C-ABI name matches *byteps* (reference byteps.lds:1-8)
-    assert all("byteps" in s for s in exported)
+    defined = {}
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) == 3:
+            defined[parts[2]] = parts[1]
+    assert defined, out
+    assert set(defined) == set(header_functions()), sorted(set(defined) ^ set(header_functions()))
+    assert all(kind == "T" for kind in defined.values()), defined
+    assert all(re.fullmatch(r"byteps_\w+", s) and "byteps" in s for s in defined)
+
+
+def test_library_build_applies_the_export_policy():
+    """The build keeps the policy: hidden visibility by default, the version
+    script on the link line, and the script's only global pattern byteps_*
+    (a subset of the reference's *byteps*)."""
+    mk = open(os.path.join(ROOT, "prophet_amd", "csrc", "Makefile")).read()
+    assert "-fvisibility=hidden" in mk and "--version-script=$(HERE)bpsr.lds" in mk
+    lds = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "prophet_amd", "csrc", "bpsr.lds")).read(),
+                 flags=re.S)
+    assert re.sub(r"\s+", " ", lds).strip() == "{ global: byteps_*; local: *; };"
+    for h in HEADERS:
+        text = open(h).read()
+        assert text.count("#pragma GCC visibility push(default)") == 1, h
+        assert text.count("#pragma GCC visibility pop") == 1, h
 
 
 def test_version_and_dtype_sizes():
