@@ -60,6 +60,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 LEAD_CYCLES = 2_000_000  # spin ahead of a timed block (~1 ms of GPU clock)
 GIB = float(1 << 30)
 WATCHDOG_EXIT = 3  # every rank's status when the N > 1 watchdog fires
+RCCL_EXIT = 4      # every rank's status when the communicator is not N ranks on N GPUs
 METRIC = "GiB/s device-resident N-way gradient-bucket sum (fp32/fp16), 1/2/4/8 GPUs"
 # --dtype name -> (byteps DataType id, torch dtype name); ids: common.h:52-65 (+ bf16 = 11)
 DTYPES = {"f32": (0, "float32"), "f64": (1, "float64"), "f16": (2, "float16"),
@@ -497,6 +498,55 @@ def shard_comm(dev):
         pass
     return (ShardComm.from_group(device=dev.index),
             "library-owned RCCL communicator (unique id over the torch group)")
+
+
+def rccl_rank_view(dev, comm, rank: int) -> dict:
+    """This rank's view of the communicator the byteps_shard_* calls use
+    (byteps_shard_comm_info: RCCL's own ncclCommCount / ncclCommUserRank /
+    ncclCommCuDevice, read when the communicator was made or wrapped,
+    nccl_manager.cc:74-127), the device torch bound, its PCI address, the RCCL
+    version the library bound, and the visible device count."""
+    import torch
+    from prophet_amd.shard import rccl_version
+    p = torch.cuda.get_device_properties(dev)
+    return {"rank": rank, "comm_world": comm.world, "comm_rank": comm.rank,
+            "comm_device": comm.device, "device": dev.index,
+            "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "rccl_version": rccl_version(), "device_count": torch.cuda.device_count()}
+
+
+def rccl_problems(views: list, world: int) -> list:
+    """What makes a set of per-rank communicator views NOT 'N ranks on N
+    distinct GPUs' (empty when the communicator is what the line claims)."""
+    out = []
+    if len(views) != world:
+        out.append(f"{len(views)} rank views for WORLD_SIZE={world}")
+    for v in views:
+        if v["comm_world"] != world:
+            out.append(f"rank {v['rank']}: communicator world {v['comm_world']} != {world}")
+        if v["comm_rank"] != v["rank"]:
+            out.append(f"rank {v['rank']}: communicator rank {v['comm_rank']}")
+        if v["comm_device"] != v["device"]:
+            out.append(f"rank {v['rank']}: communicator device {v['comm_device']} "
+                       f"!= bound device {v['device']}")
+    buses = [v["pci_bus_id"] for v in views]
+    if len(set(buses)) != len(buses):
+        out.append(f"ranks share a GPU: {buses}")
+    if len({v["rccl_version"] for v in views}) > 1:
+        out.append("ranks bound different RCCL versions")
+    return out
+
+
+def rccl_object(dev, comm, world: int, rank: int, view: dict | None = None) -> dict:
+    """The line's ``rccl`` object at N > 1 on GPUs: every rank's view,
+    gathered over the torch group, and the problems found (empty = the
+    exchange legs' communicator had N ranks on N distinct GPUs).  ``view``
+    replaces this rank's own (the CPU test of the failing path)."""
+    import torch.distributed as dist
+    views = [None] * world
+    dist.all_gather_object(views, view if view is not None else rccl_rank_view(dev, comm, rank))
+    return {"transport": "rccl", "world": world, "ranks": views,
+            "problems": rccl_problems(views, world)}
 
 
 def _transport(comm) -> str:
@@ -1315,12 +1365,34 @@ def main(argv=None):
     # (byteps_shard_*), the path a core_loops.cc caller binds; gloo
     # rehearsals and the CPU self-test keep torch.distributed P2P
     comm = None
-    if uses_shard_abi(world, cuda, rehearse) and not args.no_scatter:
+    if world == 1:
+        pass
+    elif not uses_shard_abi(world, cuda, rehearse):
+        line["rccl"] = {"transport": "gloo, no RCCL", "world": world}
+    elif args.no_scatter:
+        line["rccl"] = {"transport": "not used (--no-scatter)", "world": world}
+
+    def make_comm():
+        """N > 1 on GPUs (under the watchdog): the shard communicator, then
+        every rank's view of it; a communicator that is not N ranks on N
+        distinct GPUs fails the run (RCCL_EXIT on every rank)."""
+        nonlocal comm
+        if os.environ.get("BPSR_BENCH_TEST_RCCL") == "shared_device":
+            # test hook (CPU self-test): every rank claims GPU 0 of a world-N
+            # communicator, as a mis-bound launch would
+            line["rccl"] = rccl_object(dev, None, world, rank, view={
+                "rank": rank, "comm_world": world, "comm_rank": rank, "comm_device": 0,
+                "device": 0, "pci_bus_id": "0000:05:00", "rccl_version": 0, "device_count": 1})
+            return not line["rccl"]["problems"]
         try:
             comm, how = shard_comm(dev)
             line["shard_comm"] = how
         except Exception as e:  # report, never hide
             line["shard_comm"] = {"error": repr(e)}
+            line["rccl"] = {"transport": "rccl", "world": world, "error": repr(e)}
+            return False
+        line["rccl"] = rccl_object(dev, comm, world, rank)
+        return not line["rccl"]["problems"]
 
     def extra_legs(state=None):
         def leg(name):
@@ -1413,6 +1485,14 @@ def main(argv=None):
     watchdog = threading.Timer(limit_s, on_timeout)
     watchdog.daemon = True
     watchdog.start()
+    if (uses_shard_abi(world, cuda, rehearse) and not args.no_scatter) or \
+            os.environ.get("BPSR_BENCH_TEST_RCCL") == "shared_device":
+        state["leg"] = "rccl"
+        if not make_comm():
+            watchdog.cancel()
+            line["error"] = f"rccl: {line['rccl'].get('problems') or line['rccl'].get('error')}"
+            print(f"bench rank {rank}: {line['error']}", file=sys.stderr)
+            emit_and_maybe_exit(RCCL_EXIT)
     extra_legs(state)
     watchdog.cancel()
     emit_and_maybe_exit(None)

@@ -95,6 +95,9 @@ int byteps_shard_comm_wrap(void* nccl_comm, byteps_shard_comm** comm);
 int byteps_shard_comm_init_local(int world, const int* devices, byteps_shard_comm** comms);
 int byteps_shard_comm_destroy(byteps_shard_comm* comm);
 int byteps_shard_comm_info(const byteps_shard_comm* comm, int* world, int* rank, int* device);
+/* ncclGetVersion of the RCCL this library bound (e.g. 22703 for 2.27.3): the
+ * N > 1 bench line records it with each rank's communicator view. */
+int byteps_shard_rccl_version(int* version);
 
 /* Worker local reduce, PostNcclCalls(REDUCE) without reduce roots: rank g's
  * `dst` (owned(g) elements; may be `local` + lo(g) * size, in place as the

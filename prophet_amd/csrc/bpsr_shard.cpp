@@ -52,6 +52,7 @@ struct Rccl {
   ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t,
                             hipStream_t) = nullptr;
   const char* (*ErrorString)(ncclResult_t) = nullptr;
+  ncclResult_t (*GetVersion)(int*) = nullptr;  // optional (byteps_shard_rccl_version)
 };
 
 template <class F>
@@ -86,6 +87,7 @@ const Rccl& rccl() {
       x.err = "librccl.so.1 lacks an entry point this library needs";
       return x;
     }
+    (void)sym(h, "ncclGetVersion", &x.GetVersion);
     x.ok = true;
     return x;
   }();
@@ -445,6 +447,17 @@ int byteps_shard_comm_info(const byteps_shard_comm* c, int* world, int* rank, in
   if (rank) *rank = c->rank;
   if (device) *device = c->device;
   return BYTEPS_REDUCE_OK;
+}
+
+int byteps_shard_rccl_version(int* version) {
+  if (!version) return fail(BYTEPS_REDUCE_EARGS, "null version");
+  *version = 0;
+  if (int rc = rccl_loaded()) return rc;
+  const Rccl& r = rccl();
+  if (!r.GetVersion) return fail(BYTEPS_REDUCE_ERCCL, "librccl.so.1 has no ncclGetVersion");
+  const ncclResult_t e = r.GetVersion(version);
+  return e == ncclSuccess ? BYTEPS_REDUCE_OK
+                          : fail(BYTEPS_REDUCE_ERCCL, "ncclGetVersion: %s", r.ErrorString(e));
 }
 
 int byteps_shard_reduce_scatter(byteps_shard_comm* c, const void* local, void* const* recv_slots,

@@ -89,7 +89,7 @@ SHARD_EXPORTS = (
     "byteps_shard_comm_init", "byteps_shard_comm_wrap", "byteps_shard_comm_init_local",
     "byteps_shard_comm_destroy", "byteps_shard_comm_info", "byteps_shard_reduce_scatter",
     "byteps_shard_allgather", "byteps_shard_scatter_reduce", "byteps_shard_reduce_root",
-    "byteps_shard_broadcast",
+    "byteps_shard_broadcast", "byteps_shard_rccl_version",
 )
 UNIQUE_ID_BYTES = 128
 
@@ -115,6 +115,7 @@ def _lib():
                                                   _int, _int, _vp]
         L.byteps_shard_reduce_root.argtypes = [_vp, _int, _vp, P(_vp), _vp, _sz, _int, _int, _vp]
         L.byteps_shard_broadcast.argtypes = [_vp, _int, _vp, _sz, _int, _vp]
+        L.byteps_shard_rccl_version.argtypes = [P(_int)]
         L._shard_bound = True
     return L
 
@@ -130,6 +131,13 @@ def owner_range_native(n_elems: int, world: int, rank: int) -> tuple[int, int]:
     _check(_lib().byteps_shard_owner_range(n_elems, world, rank, ctypes.byref(lo),
                                            ctypes.byref(hi)))
     return int(lo.value), int(hi.value)
+
+
+def rccl_version() -> int:
+    """byteps_shard_rccl_version: ncclGetVersion of the RCCL the library bound."""
+    v = _int()
+    _check(_lib().byteps_shard_rccl_version(ctypes.byref(v)))
+    return int(v.value)
 
 
 def reduce_roots_from_env(env=None) -> list[int]:

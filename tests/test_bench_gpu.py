@@ -179,6 +179,7 @@ torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 dist.barrier()
 comm, how = bench.shard_comm(dev)
+rccl = bench.rccl_object(dev, comm, 1, 0)
 E = 1_000_003
 sc = bench.scatter_leg(dev, 1, 0, 8, reps=2, n_elems=E, comm=comm)
 lr = bench.local_reduce_leg(dev, 1, 0, reps=2, n_elems=E, comm=comm)
@@ -196,7 +197,8 @@ PortReducer(nthreads=4).sum_n(want, [p.cpu().numpy().view(np.uint8) for p in pus
 oracle_ok = bool(np.array_equal(owned.cpu().numpy().view(np.uint8), want))
 comm.close()
 dist.destroy_process_group()
-print(json.dumps({"how": how, "scatter": sc, "local_reduce": lr, "oracle_ok": oracle_ok}))
+print(json.dumps({"how": how, "scatter": sc, "local_reduce": lr, "oracle_ok": oracle_ok,
+                  "rccl": rccl}))
 '''
 
 
@@ -205,7 +207,8 @@ def test_exchange_legs_through_shard_abi_on_rccl_world1():
     1 on this box: the communicator comes from the torch process group
     (bench.shard_comm), every exchange is a byteps_shard_* call over RCCL
     (transport "rccl-shard-abi"), and both legs' results are exact; the same
-    scatter_reduce call equals the oracle's left fold bit for bit."""
+    scatter_reduce call equals the oracle's left fold bit for bit; the
+    line's ``rccl`` object reports a world-1 communicator on the bound GPU."""
     env = dict(os.environ, BPSR_ROOT=ROOT, MASTER_ADDR="127.0.0.1")
     import socket
     s = socket.socket()
@@ -224,3 +227,10 @@ def test_exchange_legs_through_shard_abi_on_rccl_world1():
     assert sc["exact_vs_torch_fold"] is True and sc["scatter_fold_ms"] > 0
     assert lr["exact_vs_rank_order_fold"] is True and lr["allreduce_ms"] > 0
     assert out["oracle_ok"] is True
+    # the line's rccl object: the communicator RCCL made has world 1, this
+    # rank, the bound device; no problems
+    rc = out["rccl"]
+    assert rc["world"] == 1 and rc["problems"] == [], rc
+    v = rc["ranks"][0]
+    assert (v["comm_world"], v["comm_rank"], v["comm_device"], v["device"]) == (1, 0, 0, 0), v
+    assert v["rccl_version"] > 20000 and v["device_count"] >= 1 and v["pci_bus_id"]

@@ -59,6 +59,9 @@ def test_launcher_one_line_n_ranks(n):
         # the CPU self-test moves slices with torch P2P over gloo
         assert sc["scatter"]["transport"] == lr["transport"] == "torch-p2p"
         assert "shard_comm" not in line
+        assert line["rccl"] == {"transport": "gloo, no RCCL", "world": n}
+    if n == 1:
+        assert "rccl" not in line
 
 
 def test_exchange_transport_rule():
@@ -74,6 +77,55 @@ def test_exchange_transport_rule():
     assert not bench.uses_shard_abi(1, cuda=True, rehearse=False)
     assert bench._transport(object()) == "rccl-shard-abi"
     assert bench._transport(None) == "torch-p2p"
+
+
+def test_rccl_problems_rule():
+    """The N > 1 line's ``rccl`` check (bench.rccl_problems): a communicator
+    of N ranks on N distinct GPUs passes; a wrong world, a rank mismatch, a
+    communicator on another device than the rank bound, two ranks on one GPU
+    and mixed RCCL versions are each reported."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def views(n, over=None):
+        vs = [{"rank": r, "comm_world": n, "comm_rank": r, "comm_device": r, "device": r,
+               "pci_bus_id": f"0000:{0x05 + 0x10 * r:02x}:00", "rccl_version": 22707,
+               "device_count": n} for r in range(n)]
+        for (r, k), v in (over or {}).items():
+            vs[r][k] = v
+        return vs
+    for n in (2, 4, 8):
+        assert bench.rccl_problems(views(n), n) == []
+    assert bench.rccl_problems(views(8), 4)                       # 8 views, WORLD_SIZE 4
+    bad = {(1, "comm_world"): 1, (2, "comm_rank"): 5, (3, "comm_device"): 0,
+           (4, "rccl_version"): 22500}
+    for k, v in bad.items():
+        p = bench.rccl_problems(views(8, {k: v}), 8)
+        assert len(p) == 1, (k, p)
+    shared = views(8, {(5, "pci_bus_id"): "0000:05:00", (5, "device"): 0,
+                       (5, "comm_device"): 0})
+    assert any("share a GPU" in s for s in bench.rccl_problems(shared, 8))
+
+
+def test_rccl_check_failure_fails_the_run():
+    """Every rank of a world-2 run whose communicator views say 'two ranks on
+    one GPU' (test hook) exits RCCL_EXIT; rank 0 still prints the line, with
+    the gathered views, the problem and an "error" field."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["BPSR_BENCH_TEST_RCCL"] = "shared_device"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--workers", "3", "--bucket-mib", "0.0625",
+           "--sets", "2", "--no-cpu-baseline", "--scaling-elems", "10007"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    sys.path.insert(0, ROOT)
+    import bench
+    assert r.returncode == bench.RCCL_EXIT, r.stderr[-3000:]
+    line = json.loads(r.stdout)
+    rc = line["rccl"]
+    assert rc["world"] == 2 and len(rc["ranks"]) == 2
+    assert any("share a GPU" in p for p in rc["problems"])
+    assert line["error"].startswith("rccl:")
 
 
 def test_torchrun_launch_one_line():
