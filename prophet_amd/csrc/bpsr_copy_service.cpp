@@ -16,13 +16,20 @@
 // implicit synchronisation with the legacy NULL stream, so PyTorch's default
 // stream does not wait for a running service (a CU-masked stream would have
 // its own queue but is a blocking stream: DESIGN.md §9).  It exits by
-// itself after kIdleUs without a job or kMaxMs of age, and is relaunched by
-// the next poster that finds it gone; a job stranded by an exit (posted just
-// as the leader decided to stop) is served by the relaunch, which starts at
-// the oldest job still pending and skips jobs already done.  A relaunch
-// happens only after the old launch has completed, so no job is copied by two
-// launches at once (a late second copy could overwrite a buffer its caller
-// already reuses).
+// itself after kIdleUs without a job or kMaxUs of age (busy or not), storing
+// its launch number to the pinned `exited` word, and a waiting or posting
+// thread that sees the word relaunches it at once; a job stranded by an exit
+// is served by the relaunch, which starts at the oldest job still pending and
+// skips jobs already done.  The age limit bounds what a device-wide
+// synchronisation elsewhere in the process (torch.cuda.synchronize,
+// hipDeviceSynchronize, hipFree) waits for the service: the running launch's
+// remaining age plus at most one relaunch's (include/bpsr/server.h).
+// A relaunch happens only after the old launch has completed, so no job is
+// copied by two launches at once (a late second copy could overwrite a buffer
+// its caller already reuses).  For the same reason a give-up (a job not served
+// in kTimeoutMs) raises `stop` and waits for the running launch to end before
+// any caller learns that the service is off and copies the bytes another way:
+// the fetcher checks `stop` on every pass and moves nothing after it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,9 +51,14 @@ namespace {
 constexpr uint32_t kSvcWgs = 65;             // workgroups per launch: the fetcher + 64 copiers
 constexpr size_t kChunk = 64 << 10;          // one job's bytes at most (a large copy spreads)
 // A launch's idle exit (short: a device-wide synchronisation waits for a
-// running service; a pull burst keeps it alive) and its age limit.
-constexpr int kIdleUs = 500, kMaxMs = 2000;
+// running service; a pull burst keeps it alive) and its age limit (a
+// relaunch costs ~20 us of posting latency, so 1 ms keeps that near 2 %).
+#ifndef BPSR_SVC_MAX_US  // (probe builds only: tools/dbg/copysvc_probe.cpp)
+#define BPSR_SVC_MAX_US 1000
+#endif
+constexpr int kIdleUs = 500, kMaxUs = BPSR_SVC_MAX_US;
 constexpr int kCheckUs = 200;                // a waiter's liveness check period
+constexpr int64_t kExitPollNs = 2000;        // ... while the launch is exiting
 constexpr int kTimeoutMs = 10000;            // a job's give-up (reported, not retried)
 }  // namespace
 
@@ -56,25 +68,26 @@ struct CopyService {
   hipEvent_t ev = nullptr;       // the current launch's completion
   SvcJob* ring = nullptr;        // pinned host
   uint64_t* done = nullptr;      // pinned host, one 64-B line per slot (kDoneStride words)
-  uint32_t* stop = nullptr;      // pinned host
+  uint32_t* stop = nullptr;      // pinned host: [0] stop, [16] exited (its own 64-B line)
+  uint32_t* exited = nullptr;
   SvcJob* ring_d = nullptr;      // their device views
   uint64_t* done_d = nullptr;
   uint32_t* stop_d = nullptr;
   uint64_t* dev = nullptr;       // device words of the kernel
   SvcJob* dring = nullptr;       // device ring
   uint64_t* trace = nullptr;     // probes only
-  uint64_t idle_ticks = 0, max_ticks = 0;
+  uint64_t idle_ticks = 0, max_ticks = 0, stall_ticks = 0;
   // Posting is lock-free (a job index from `posted`, then the slot's words);
   // `mu` serialises only launches and liveness checks.
   std::atomic<uint64_t> posted{0};      // job indices handed out
   std::atomic<int64_t> last_post_ns{0};
   std::atomic<bool> running{false};     // written under mu
+  std::atomic<uint32_t> gen{0};         // the current launch's number (written under mu)
   std::atomic<bool> broken{false};      // a job timed out: the service is off for good
   std::mutex mu;
   uint64_t scan_from = 0;               // under mu: every job below is done
   std::atomic<uint64_t> launches{0};
   int timeout_ms = kTimeoutMs;
-  bool stall = false;  // tests only (BPSR_COPYSVC_TEST_STALL_MS): copiers serve nothing
 };
 
 namespace {
@@ -121,11 +134,35 @@ bool job_done(const CopyService* c, uint64_t j) {
   return __atomic_load_n(&c->done[(j % kSvcRing) * kDoneStride], __ATOMIC_ACQUIRE) >= j + 1;
 }
 
-// With mu held: a launch is serving unless its event says it is gone.
+// The running launch has decided to exit (its fetcher stored its number):
+// a thread with a pending job relaunches now rather than at its next check.
+bool svc_exiting(const CopyService* c) {
+  return c->running.load() && __atomic_load_n(c->exited, __ATOMIC_ACQUIRE) == c->gen.load();
+}
+
+// With mu held: a launch is running until its event says it is gone (one
+// that decided to exit finishes the copies it started first; the caller then
+// polls it rather than blocking on it with mu held, so a give-up can still
+// fire meanwhile).
 bool svc_alive(CopyService* c) {
   if (!c->running.load()) return false;
   if (hipEventQuery(c->ev) == hipSuccess) c->running.store(false);
   return c->running.load();
+}
+
+// With mu held: give up — raise `stop`, wait until the running launch has
+// ended (it moves and starts no job after seeing `stop`; copies already under
+// way finish first), and only then mark the service off, so that no caller
+// copies a job's bytes another way while the kernel may still write them.
+int svc_give_up(CopyService* c, uint64_t j) {
+  __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
+  if (c->running.load()) {
+    (void)hipEventSynchronize(c->ev);
+    c->running.store(false);
+  }
+  c->broken.store(true);
+  return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
+              (unsigned long long)j, c->timeout_ms);
 }
 
 // With mu held: start a launch at the oldest job not done (jobs handed out
@@ -144,6 +181,7 @@ int svc_launch(CopyService* c) {
   a.ring = c->ring_d;
   a.done = c->done_d;
   a.stop = c->stop_d;
+  a.exited = c->stop_d + 16;
   a.dev = c->dev;
   a.dring = c->dring;
   a.trace = c->trace;
@@ -151,12 +189,14 @@ int svc_launch(CopyService* c) {
   a.check_below = posted;
   a.idle_ticks = c->idle_ticks;
   a.max_ticks = c->max_ticks;
+  a.stall_ticks = c->stall_ticks;
   a.wgs = kSvcWgs;
-  a.stall = c->stall ? 1u : 0u;
+  a.gen = c->gen.load() + 1;
   hipError_t e = hipMemsetAsync(c->dev, 0, 4 * sizeof(uint64_t), c->stream);
   if (e == hipSuccess) e = launch_copy_service(a, c->stream);
   if (e == hipSuccess) e = hipEventRecord(c->ev, c->stream);
   if (e != hipSuccess) return hip_fail(e, "copy service launch");
+  c->gen.store(a.gen);
   c->running.store(true);
   c->launches.fetch_add(1, std::memory_order_relaxed);
   return 0;
@@ -176,13 +216,13 @@ int copysvc_create(int device, CopyService** out) {
                            : fail(BYTEPS_REDUCE_EHIP, "copy service: no wall clock rate");
   }
   c->idle_ticks = (uint64_t)khz * kIdleUs / 1000;
-  // tests of the give-up path: a service whose copiers serve nothing, and a
-  // short give-up time
+  // tests of the give-up path: a short give-up time, and copiers that hold
+  // every job three times that long before copying it (unless stopped)
   if (const char* v = getenv("BPSR_COPYSVC_TEST_STALL_MS")) {
-    c->stall = true;
     c->timeout_ms = std::max(1, atoi(v));
+    c->stall_ticks = (uint64_t)khz * 3 * c->timeout_ms;
   }
-  c->max_ticks = (uint64_t)khz * kMaxMs;
+  c->max_ticks = (uint64_t)khz * kMaxUs / 1000;
   int prio_lo = 0, prio_hi = 0;
   e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (e == hipSuccess && prio_lo == prio_hi) {
@@ -195,7 +235,7 @@ int copysvc_create(int device, CopyService** out) {
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->ring), sizeof(SvcJob) * kSvcRing, fl);
   if (e == hipSuccess)
     e = hipHostMalloc(reinterpret_cast<void**>(&c->done), sizeof(uint64_t) * kSvcRing * kDoneStride, fl);
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->stop), 64, fl);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&c->stop), 128, fl);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dev), 256);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->dring), sizeof(SvcJob) * kSvcRing);
   // on the service's own (non-blocking) stream: a NULL-stream memset would
@@ -206,7 +246,8 @@ int copysvc_create(int device, CopyService** out) {
   if (e == hipSuccess) {
     std::memset(c->ring, 0, sizeof(SvcJob) * kSvcRing);
     std::memset(c->done, 0, sizeof(uint64_t) * kSvcRing * kDoneStride);
-    *c->stop = 0;
+    std::memset(c->stop, 0, 128);
+    c->exited = c->stop + 16;
     e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->ring_d), c->ring, 0);
   }
   if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&c->done_d), c->done, 0);
@@ -237,8 +278,23 @@ void copysvc_destroy(CopyService* c) {
   delete c;
 }
 
+// With mu held, for a job j not done: keep a launch serving, or give up.
+int svc_check(CopyService* c, uint64_t j, int64_t now, int64_t t0) {
+  if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+  if (!svc_alive(c)) {
+    const int rc = svc_launch(c);
+    if (rc) {
+      c->broken.store(true);
+      return rc;
+    }
+  }
+  if (now - t0 > c->timeout_ms * 1000000ll) return svc_give_up(c, j);
+  return 0;
+}
+
 // Waits for job j's done word: spin, then yield; every kCheckUs without it,
-// make sure a launch is serving.  0, or an error (the service then stays off).
+// or as soon as the launch signals its exit, make sure a launch is serving.
+// 0, or an error (the service then stays off).
 int wait_job(CopyService* c, uint64_t j, int64_t t0) {
   int64_t t_check = now_ns();
   for (;;) {
@@ -246,24 +302,12 @@ int wait_job(CopyService* c, uint64_t j, int64_t t0) {
     for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
     const int64_t now = now_ns();
     if (now - t0 > 50'000) std::this_thread::yield();
-    if (now - t_check > kCheckUs * 1000ll) {
+    const int64_t since = now - t_check;
+    if (since > kCheckUs * 1000ll || (since > kExitPollNs && svc_exiting(c))) {
       t_check = now;
       std::lock_guard<std::mutex> g(c->mu);
       if (job_done(c, j)) return 0;
-      if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
-      if (!svc_alive(c)) {
-        const int rc = svc_launch(c);
-        if (rc) {
-          c->broken.store(true);
-          return rc;
-        }
-      }
-      if (now - t0 > c->timeout_ms * 1000000ll) {
-        c->broken.store(true);
-        __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
-        return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
-                    (unsigned long long)j, c->timeout_ms);
-      }
+      if (const int rc = svc_check(c, j, now, t0)) return rc;
     }
   }
 }
@@ -293,8 +337,9 @@ int copysvc_post(CopyService* c, void* dst, const void* src, size_t len, uint64_
   }
   // a launch idle for most of kIdleUs may be exiting: look after posting
   const int64_t prev = c->last_post_ns.exchange(t0);
-  if (!c->running.load() || t0 - prev > kIdleUs * 500ll) {
+  if (!c->running.load() || t0 - prev > kIdleUs * 500ll || svc_exiting(c)) {
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
     if (!svc_alive(c) && (rc = svc_launch(c))) {
       c->broken.store(true);
       return rc;
@@ -310,25 +355,13 @@ int copysvc_test(CopyService* c, uint64_t first, uint64_t n, int64_t posted_ns, 
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t j = first + i;
     if (job_done(c, j)) continue;
-    // not yet: past kCheckUs since posting, make sure a launch is serving
+    // not yet: past kCheckUs since posting (or the launch is exiting), make
+    // sure a launch is serving
     const int64_t now = now_ns();
-    if (now - posted_ns > kCheckUs * 1000ll) {
+    if (now - posted_ns > kCheckUs * 1000ll || svc_exiting(c)) {  // (the caller polls)
       std::lock_guard<std::mutex> g(c->mu);
       if (job_done(c, j)) continue;
-      if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
-      if (!svc_alive(c)) {
-        const int rc = svc_launch(c);
-        if (rc) {
-          c->broken.store(true);
-          return rc;
-        }
-      }
-      if (now - posted_ns > c->timeout_ms * 1000000ll) {
-        c->broken.store(true);
-        __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
-        return fail(BYTEPS_REDUCE_ETIMEOUT, "copy service: job %llu not served in %d ms",
-                    (unsigned long long)j, c->timeout_ms);
-      }
+      if (const int rc = svc_check(c, j, now, posted_ns)) return rc;
     }
     return 0;
   }

@@ -325,18 +325,22 @@ struct SvcJob {      // 32 B: dst, src, len, each | tag << 48; one pad word
 // 1..65535, never 0 (zeroed slots); one slot's successive jobs differ
 // (4096 and 65535 are coprime)
 __host__ __device__ inline uint64_t svc_tag(uint64_t job) { return job % 0xFFFFull + 1; }
+constexpr uint64_t kSvcExitDone = 1, kSvcExitStop = 2;
 struct SvcArgs {
   const SvcJob* ring;      // host ring (device view)
   SvcJob* dring;           // device ring
   uint64_t* done;          // host words: done[slot * kDoneStride] = job + 1 once the copy is visible
-  const uint32_t* stop;    // host word: nonzero = exit now
+  const uint32_t* stop;    // host word: nonzero = exit now, copying nothing more
+  uint32_t* exited;        // host word: the fetcher stores `gen` when it decides to exit
   uint64_t* dev;           // device words: [1] jobs completed, [2] exit flag
+                           // (kSvcExitDone: copy what was fetched; kSvcExitStop: copy nothing)
   uint64_t start;          // first job index of this launch
   uint64_t check_below;    // jobs below this may be done already (a relaunch): look first
   uint64_t idle_ticks;     // exit after this long without a new job ...
   uint64_t max_ticks;      // ... or once this launch is this old (a relaunch takes over)
+  uint64_t stall_ticks;    // tests only: a copier holds every job this long (0 in the product)
   uint32_t wgs;            // fetcher + copiers
-  uint32_t stall;          // tests only: copiers serve no job (the give-up path)
+  uint32_t gen;            // this launch's number (for `exited`)
   uint64_t* trace;         // probes only (null in the product): per slot, wall clock at
                            // [0] fetched, [1] picked up, [2] copied and drained
 };

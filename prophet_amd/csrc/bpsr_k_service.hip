@@ -3,10 +3,10 @@
 // pinned job ring.
 //   workgroup 0, the fetcher (one wave): polls the next slots of the host
 //     ring; moves each newly posted job's tagged words into the same slot of
-//     a device ring (sc1 stores), so copiers never read over PCIe; decides
-//     when the launch ends — after idle_ticks without a new job with every
-//     fetched job completed, once max_ticks have passed, or when the host
-//     raises `stop` — and raises the exit word.
+//     a device ring, so copiers never read over PCIe; decides when the
+//     launch ends — after idle_ticks without a new job with every fetched job
+//     completed, once max_ticks have passed, or when the host raises `stop` —
+//     and raises the exit word (and the host's `exited` word).
 //   workgroups 1..wgs-1, the copiers: copier g polls its next job's words in
 //     the device ring until all three carry the job's tag, copies the job,
 //     and stores the job's done word to the host.  16-B aligned jobs load with sc1 (L1 bypassed: no acquire
@@ -71,64 +71,88 @@ __device__ __forceinline__ void copy_plain(unsigned char* dst, const unsigned ch
   }
 }
 
-// One wave: polls a window of the host ring's next slots each pass (one
-// PCIe round trip; 8 slots, 64 while the last pass found a full window),
-// moves the consecutive run of posted jobs it finds into the device ring
-// (tagged words: no ordering needed), and decides the exit.
+// One wave per poller: polls a window of the host ring's next slots each pass
+// (one PCIe round trip; 8 slots, 64 while the last pass found a full window)
+// and moves the consecutive run of posted jobs it finds into the device ring.
+// kPollers waves poll the same ring half a round trip apart, so a posted job
+// is seen sooner.  A wave moves only the jobs it claims by raising the shared
+// `s_seen` past them, so each job's words are stored by ONE wave: a late store
+// can never put job j's words back over job j + kSvcRing's (j + kSvcRing is
+// posted only once j is done, i.e. once a copier read the claimed store).
+// Wave 0 decides the exit — on the host's stop word (checked every pass, in
+// the same round trip as the ring), at max_ticks of age even while busy, or
+// after idle_ticks without a new job with every fetched job completed — and
+// stores the launch's number to the host's `exited` word, so a waiting host
+// thread relaunches at once; wave 1 follows the exit word.
 __device__ void fetcher(const SvcArgs& a) {
-  // kPollers waves poll the same ring half a round trip apart, so a posted
-  // job is seen sooner; moving a job twice writes the same tagged words.
-  // Wave 0 decides the exit; the others follow the exit word.
   constexpr uint32_t kPollers = 2;
+  __shared__ uint64_t s_seen;  // jobs below are claimed (in the device ring, or not this launch's)
+  if (threadIdx.x == 0) s_seen = a.start;
+  __syncthreads();
   if (threadIdx.x >= 64 * kPollers) return;
   const uint32_t wave = threadIdx.x / 64;
   const uint32_t l = threadIdx.x % 64;
   if (wave) __builtin_amdgcn_s_sleep(12);
   uint32_t kWin = 8;
-  uint64_t seen = a.start;  // jobs below are in the device ring (or were never this launch's)
   const uint64_t t_begin = wall_clock64();
   uint64_t t_idle = t_begin;
   for (;;) {
-    const uint64_t j = seen + l;
+    const uint64_t base = __hip_atomic_load(&s_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t j = base + l;
     const uint64_t slot = j % kSvcRing;
     const uint64_t tag = svc_tag(j);
-    uint64_t w0 = 0, w1 = 0, w2 = 0;
+    uint64_t w0 = 0, w1 = 0, w2 = 0, sig = 0;
     if (l < kWin) {
       const uint64_t* hw = reinterpret_cast<const uint64_t*>(a.ring + slot);
       w0 = ld_host64(hw + 0);
       w1 = ld_host64(hw + 1);
       w2 = ld_host64(hw + 2);
     }
+    if (l == 0)  // the exit signal, in the same round trip
+      sig = wave ? ld_dev64(a.dev + 2)
+                 : __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sig = __builtin_amdgcn_readfirstlane((uint32_t)sig);
     const bool valid = l < kWin && (w0 >> 48) == tag && (w1 >> 48) == tag && (w2 >> 48) == tag;
     const uint64_t vmask = __ballot(valid);
     const uint64_t run = ~vmask ? __builtin_ctzll(~vmask) : 64;  // consecutive posted jobs
-    if (valid && l < run) {
-      uint64_t* dw = reinterpret_cast<uint64_t*>(a.dring + slot);
-      st_dev64(dw + 0, w0);
-      st_dev64(dw + 1, w1);
-      st_dev64(dw + 2, w2);
-      if (a.trace) st_dev64(a.trace + slot * 4 + 0, wall_clock64());
+    if (run && !sig) {  // nothing more is moved once the exit is signalled
+      uint64_t old = 0;
+      if (l == 0)
+        old = __hip_atomic_fetch_max(&s_seen, base + run, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+      old = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(old >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)old);
+      if (valid && l < run && j >= old) {  // claimed by this wave
+        uint64_t* dw = reinterpret_cast<uint64_t*>(a.dring + slot);
+        st_dev64(dw + 0, w0);
+        st_dev64(dw + 1, w1);
+        st_dev64(dw + 2, w2);
+        if (a.trace) st_dev64(a.trace + slot * 4 + 0, wall_clock64());
+      }
     }
     const uint64_t now = wall_clock64();
-    if (run) {
-      seen += run;
-      t_idle = now;
+    if (wave) {
+      if (sig) return;
+      if (!run) __builtin_amdgcn_s_sleep(1);
       kWin = run == kWin ? 64 : 8;
       continue;
     }
-    kWin = 8;
-    if (wave) {
-      if (ld_dev64(a.dev + 2)) return;
-      __builtin_amdgcn_s_sleep(1);
-      continue;
+    bool quit = sig || now - t_begin > a.max_ticks;
+    if (run) {
+      t_idle = now;
+    } else if (!quit) {
+      const uint64_t seen = __hip_atomic_load(&s_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      quit = a.start + ld_dev64(a.dev + 1) >= seen && now - t_idle > a.idle_ticks;
     }
-    const uint32_t stop = __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const bool drained = a.start + ld_dev64(a.dev + 1) >= seen;
-    if (stop || now - t_begin > a.max_ticks || (drained && now - t_idle > a.idle_ticks)) {
-      if (l == 0) st_dev64(a.dev + 2, 1);
+    if (quit) {
+      if (l == 0) {
+        st_dev64(a.dev + 2, sig ? kSvcExitStop : kSvcExitDone);
+        __hip_atomic_store(a.exited, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (!run) __builtin_amdgcn_s_sleep(1);
+    kWin = run == kWin ? 64 : 8;
   }
 }
 
@@ -145,7 +169,7 @@ __device__ void copier(const SvcArgs& a) {
       uint32_t st = 0;
       for (;;) {
         const uint64_t w0 = ld_dev64(dw + 0), w1 = ld_dev64(dw + 1), w2 = ld_dev64(dw + 2);
-        if (!a.stall && (w0 >> 48) == tag && (w1 >> 48) == tag && (w2 >> 48) == tag) {
+        if ((w0 >> 48) == tag && (w1 >> 48) == tag && (w2 >> 48) == tag) {
           s_job[0] = w0 & kSvcMask;
           s_job[1] = w1 & kSvcMask;
           s_job[2] = w2 & kSvcMask;
@@ -160,6 +184,19 @@ __device__ void copier(const SvcArgs& a) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+      }
+      // tests only: hold the job; a stop meanwhile drops it uncopied (the
+      // host word itself: the fetcher may have left at its age limit)
+      if (st == 1 && a.stall_ticks) {
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < a.stall_ticks) {
+          if (ld_dev64(a.dev + 2) == kSvcExitStop ||
+              __hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+            st = 2;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
+        }
       }
       s_state = st;
     }

@@ -1448,10 +1448,11 @@ def test_blocking_device_pulls_through_copy_service(port, service, monkeypatch):
 
 def test_copy_service_give_up_falls_back_to_lane_copies(port, monkeypatch):
     """The copy service's give-up path: with BPSR_COPYSVC_TEST_STALL_MS the
-    service's copiers serve nothing and a job is given up after that many ms.
-    The pull that met the stalled service still completes, through the key's
-    lane stream, and every later pull goes to lane copies directly; every
-    pulled byte equals the oracle's left fold."""
+    service's copiers hold every job 3 x that many ms and a job is given up
+    after that many ms.  The pull that met the stalled service still
+    completes, through the key's lane stream, and every later pull goes to
+    lane copies directly; every pulled byte equals the oracle's left fold; the
+    held job is never copied once the pull has returned."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_PULL_SERVICE", "1")
     monkeypatch.setenv("BPSR_COPYSVC_TEST_STALL_MS", "100")
@@ -1487,13 +1488,106 @@ def test_copy_service_give_up_falls_back_to_lane_copies(port, monkeypatch):
                 srv.pull(k, out)
                 if first_s is None:
                     first_s = time.perf_counter() - t0
+                    first_out = out                             # the held job's destination
                 assert_bytes_match(dt, out.cpu().numpy().view(np.uint8), want,
                                    nan_class_f32_f64=False, what=f"r{r} key {j} w{w}")
+            if r == 1 and j == 0:
+                # The copiers hold every job 3 x 100 ms and would then copy it.
+                # The give-up waited for the service launch to end (the stop
+                # dropped the held job), so the buffer the fallback filled is
+                # the caller's again: a late service copy would overwrite the
+                # marker written here.
+                first_out.fill_(-7.0)
+                torch.cuda.synchronize()
+                time.sleep(0.45)
+                assert torch.all(first_out == -7.0), "the copy service wrote after its give-up"
     st = srv.stats()
     srv.close()
     assert first_s >= 0.09, first_s                            # the first pull met the stall
     assert st["service_pulls"] == 0 and st["service_launches"] >= 1
     assert st["pulls"] == N * R * len(keys)
+
+
+def test_device_sync_bounded_while_threads_pull_through_service(port):
+    """include/bpsr/server.h: a device-wide synchronisation elsewhere in the
+    process (torch.cuda.synchronize = hipDeviceSynchronize) waits for a
+    running copy service at most its remaining age plus one relaunch's (the
+    service's age limit is 1 ms).  8 worker threads push and pull 4 device
+    keys through the service continuously while the main thread times 150
+    device synchronisations; every pulled byte of the last round equals the
+    oracle's fold in the recorded arrival order."""
+    import sys
+    from prophet_amd.server import PSServer
+    dt, N = DType.FLOAT32, 8
+    sizes = [16, 1000, 65_536, 300_007]
+    keys = list(range(200, 200 + len(sizes)))
+    es = elem_size(dt)
+    srv = PSServer(N, engine_lanes=4)
+    dev = torch.device("cuda:0")
+    src = {(w, j): torch.from_numpy(data(dt, n, w, 5, j)).to(dev)
+           for w in range(N) for j, n in enumerate(sizes)}
+    outs = {(w, j): torch.empty(n, dtype=torch.float32, device=dev)
+            for w in range(N) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    stop = threading.Event()
+    flag = [False]
+    bar = threading.Barrier(N, action=lambda: flag.__setitem__(0, stop.is_set()))
+    errors, rounds = [], [0] * N
+
+    def worker(w):
+        try:
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, j)], dt)                 # init round
+            while True:
+                bar.wait(timeout=60)
+                if flag[0]:
+                    return
+                for j, k in enumerate(keys):
+                    srv.push(k, w, src[(w, j)], dt)
+                for j, k in enumerate(keys):
+                    srv.pull(k, outs[(w, j)])
+                rounds[w] += 1
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+            bar.abort()
+
+    old_switch = sys.getswitchinterval()
+    sys.setswitchinterval(1e-4)          # the timing thread gets the GIL back promptly
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    sync_s = []
+    try:
+        for t in ts:
+            t.start()
+        t_end = time.perf_counter() + 30
+        while srv.stats()["service_pulls"] < 200 and time.perf_counter() < t_end and not errors:
+            time.sleep(0.001)
+        for _ in range(150):
+            if errors:
+                break
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            sync_s.append(time.perf_counter() - t0)
+            time.sleep(0.002)
+    finally:
+        stop.set()
+        for t in ts:
+            t.join(timeout=60)
+        sys.setswitchinterval(old_switch)
+    assert not errors, errors
+    st = srv.stats()
+    orders = {j: srv.key_info(k)[2] for j, k in enumerate(keys)}
+    srv.close()
+    assert st["service_pulls"] >= 1000, st
+    sync_s.sort()
+    # before the age limit (2 s) a synchronisation under continuous pulls
+    # waited for the whole launch
+    assert sync_s[len(sync_s) // 2] < 0.004 and sync_s[-1] < 0.010, sync_s[-10:]
+    for j, n in enumerate(sizes):
+        want = np.zeros(n * es, np.uint8)
+        port.sum_n(want, [data(dt, n, w, 5, j) for w in orders[j]], n * es, dt)
+        for w in range(N):
+            assert_bytes_match(dt, outs[(w, j)].cpu().numpy().view(np.uint8), want,
+                               nan_class_f32_f64=False, what=f"key {j} w{w}")
 
 
 def test_copy_service_many_rounds_racing_pullers(port):

@@ -1,8 +1,11 @@
 // Probe (not product code): latency of the pull copy service
 // (bpsr_copy_service.cpp) against hipMemcpyAsync + hipStreamSynchronize, per
 // copy size and number of concurrent posting threads.
-//   hipcc -O2 -std=c++17 -I include -I prophet_amd/csrc tools/dbg/copysvc_probe.cpp \
-//     -o tools/dbg/copysvc_probe -L prophet_amd -lbpsr -Wl,-rpath,'$ORIGIN/../../prophet_amd' -lpthread
+//   make -C prophet_amd/csrc && hipcc -O2 -std=c++17 --offload-arch=gfx950 -I include \
+//     -I prophet_amd/csrc -c tools/dbg/copysvc_probe.cpp -o prophet_amd/csrc/build/probe.o && \
+//   hipcc --offload-arch=gfx950 prophet_amd/csrc/build/probe.o prophet_amd/csrc/build/bpsr_*.o \
+//     -o tools/dbg/copysvc_probe -ldl -lpthread
+// (linked to the objects: libbpsr.so exports only the byteps_* C ABI)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
