@@ -747,15 +747,17 @@ def fp16_leg(dev, red, N: int, B: int, steps: int, sets: int = 3) -> dict:
 
 
 def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int = 256 << 20,
-            reps: int = 3) -> dict:
+            reps: int = 3, link: dict | None = None) -> dict:
     """BASELINE config 5 end to end, key-space sharded: 16 workers' 256 MiB
     bf16 pushes (4 GiB) start in pinned host memory, as ps-lite receive
     buffers would (server.cc:174); each GPU streams ITS slice of every push
     (owner_ranges, core_loops.cc:208-211) host -> HBM -> fold -> host through
     ``StreamingReducer`` (H2D, fold and D2H on three streams; ``reduce_from_host``
     with the aggregate pulled back), over its own PCIe link, no collective.
-    Node rate = all pushed bytes / (max over ranks of the blocking call).
-    PCIe-inclusive: never ``value``.  Exactness: strided windows of the pulled
+    Node rate = all pushed bytes / (max over ranks of the blocking call);
+    ``frac_of_link`` = this GPU's H2D rate (its slices of the pushes) over the
+    same run's measured pinned H2D rate (``link``).  PCIe-inclusive: never
+    ``value``.  Exactness: strided windows of the pulled
     slice against torch's own bf16 left fold (fp32 add, RNE to bf16 per add)
     of the same windows on the device."""
     import torch
@@ -799,21 +801,68 @@ def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int =
                                      out.view(torch.bfloat16)[w0:w1].view(torch.int16)))
     ok = _all_true(dist, dev, ok)
     total = n_workers * bucket_bytes
-    return {"workload": (f"config 5: {n_workers}-way bf16, {n_workers} x {bucket_bytes >> 20} MiB "
-                         f"pinned host pushes ({total / GIB:.0f} GiB), key-space sharded over "
-                         f"{world} GPU(s), streamed H2D + fold + D2H, aggregate back in host memory"),
-            "node_e2e_GiBps": round(total / t / GIB, 1),
-            "per_gpu_e2e_GiBps": round(n_workers * nb / t / GIB, 1),
-            "ms": round(t * 1e3, 2), "reps": reps, "pcie_inclusive": True,
-            "exact_vs_torch_fold_windows": ok}
+    out = {"workload": (f"config 5: {n_workers}-way bf16, {n_workers} x {bucket_bytes >> 20} MiB "
+                        f"pinned host pushes ({total / GIB:.0f} GiB), key-space sharded over "
+                        f"{world} GPU(s), streamed H2D + fold + D2H, aggregate back in host memory"),
+           "node_e2e_GiBps": round(total / t / GIB, 1),
+           "per_gpu_e2e_GiBps": round(n_workers * nb / t / GIB, 1),
+           "ms": round(t * 1e3, 2), "reps": reps, "pcie_inclusive": True,
+           "exact_vs_torch_fold_windows": ok}
+    if link and link.get("h2d_GBps"):
+        out["frac_of_link"] = round(n_workers * nb / t / (link["h2d_GBps"] * 1e9), 4)
+    return out
 
 
 # --------------------------------------------------------------------------
 # config 1 through the PS server group, host-resident, one server per GPU
 
 
+def pcie_leg(dev, nbytes: int = 64 << 20, reps: int = 10) -> dict:
+    """This GPU's PCIe link, measured in the same run as the host-resident
+    objects (their rate "including H2D and D2H" needs the link's
+    own rate beside it): pinned host <-> HBM copies of ``nbytes`` on a side
+    stream, H2D alone, D2H alone, and both at once on two streams (the link is
+    full duplex); median over ``reps`` of HIP-event timings."""
+    import torch
+    h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def timed(fn):
+        ts = []
+        for i in range(reps + 2):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            if i >= 2:
+                ts.append(time.perf_counter() - t0)
+        return statistics.median(ts)
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            h2.copy_(d2, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+    t_h2d, t_d2h, t_both = timed(h2d), timed(d2h), timed(both)
+    return {"workload": f"pinned host <-> HBM copies of {nbytes >> 20} MiB on side streams "
+                        f"(median of {reps})",
+            "h2d_GBps": round(nbytes / t_h2d / 1e9, 2),
+            "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
+            "bidir_GBps": round(2 * nbytes / t_both / 1e9, 2)}
+
+
 def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
-                     bucket_bytes: int = 64 << 20, rounds: int = 10, lanes: int = 4) -> dict:
+                     bucket_bytes: int = 64 << 20, rounds: int = 10, lanes: int = 4,
+                     link: dict | None = None) -> dict:
     """BASELINE config 1's server rounds from host memory on every GPU of the
     node: each rank's process is one PS server (a byteps_server_group_* group
     with ONE instance, on this rank's GPU, whole keys by the reference's djb2
@@ -821,23 +870,27 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     cfg1-shaped bucket: 2 workers' 64 MiB fp32 gradients as the 17 BytePS
     partitions of 4,096,000 B (operations.cc:99-136, declared key = rank), in
     pinned host memory as ps-lite's receive buffers would be.  A round, in
-    BytePS's worker loop shape (core_loops.cc:492-564: a push loop and a pull
-    loop per worker): each worker's push thread pushes its 17 partitions
-    (byteps_server_group_push: H2D into the receive slots, the fold on the
-    lane issuers) and its pull thread pulls each partition back into pinned
-    host memory as soon as that partition's push returned, so the D2H of
-    partition k overlaps the H2D of partition k + 1 (PCIe is full duplex).
-    Two pull forms, timed separately: the zero-copy pull response
-    (``byteps_server_group_pull_host_view`` — server.cc:42-70 answers a pull
-    with an SArray over its own buffer, which ps-lite then sends: ONE D2H per
-    partition and round into the pinned mirror, shared by both workers; the
-    headline form) and copying pulls into each worker's own pinned buffer
-    (``byteps_server_group_pull``: one D2H per worker).  Weak scaling: at N
-    GPUs, N buckets over N PCIe links.  Node rate = all ranks' pushed bytes /
-    the slowest rank's median round.  PCIe-inclusive; compare with
-    ``cpu_baseline`` (the reference's host-core round).  Exactness: every
-    worker's pull equals torch's sum of the two pushes (fp32, two operands:
-    the left fold in either arrival order)."""
+    BytePS's worker loop shape (core_loops.cc:492-564: every partition's ZPush
+    is issued at once, and each partition's ZPull waits on the server for its
+    round): each worker's push thread hands its 17 partitions to ONE
+    byteps_server_group_push_many call (all 17 H2D copies in flight on the
+    lanes' copy streams, each round folded as it completes), while its pull
+    thread pulls the partitions in order, each answered as soon as that
+    partition's round is folded — so D2H runs beside the H2D of later
+    partitions (PCIe is full duplex).  Two pull forms, timed separately: the
+    zero-copy pull response (``byteps_server_group_pull_host_view`` —
+    server.cc:42-70 answers a pull with an SArray over its own buffer, which
+    ps-lite then sends: ONE D2H per partition and round into the pinned
+    mirror, shared by both workers; the headline form) and copying pulls into
+    each worker's own pinned buffer (``byteps_server_group_pull``: one D2H per
+    worker).  The threads persist across rounds (a barrier starts each).  Weak
+    scaling: at N GPUs, N buckets over N PCIe links.  Node rate = all ranks'
+    pushed bytes / the slowest rank's median round; ``frac_of_link`` = the
+    per-GPU push (H2D) rate over the same run's measured pinned H2D rate
+    (``link``).  PCIe-inclusive; compare with ``cpu_baseline`` (the
+    reference's host-core round).  Exactness: every worker's pull equals
+    torch's sum of the two pushes (fp32, two operands: the left fold in either
+    arrival order)."""
     import threading
     import torch
     from prophet_amd.buckets import partition_tensor
@@ -860,39 +913,47 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     dsts = [[outs[w][o:o + ln] for _, o, ln in parts] for w in range(n_workers)]
     errors = []
     views = {}
+    # persistent threads: a push thread and a pull thread per worker; the
+    # main thread joins each round through two barriers (start, end)
+    mode = {"pull": None, "quit": False}
+    start = threading.Barrier(2 * n_workers + 1)
+    end = threading.Barrier(2 * n_workers + 1)
 
-    def rnd(init=False, view=False):
-        pushed = [[threading.Event() for _ in parts] for _ in range(n_workers)]
-
-        def pusher(w):
+    def pusher(w):
+        while True:
+            start.wait()
+            if mode["quit"]:
+                return
             try:
-                for i, k in enumerate(keys):
-                    grp.push(k, w, srcs[w][i], DType.FLOAT32)
-                    pushed[w][i].set()
+                grp.push_many(keys, w, srcs[w], DType.FLOAT32)
             except Exception as e:  # noqa: BLE001 — reported below
                 errors.append(repr(e))
-                for ev in pushed[w]:
-                    ev.set()
+            end.wait()
 
-        def puller(w):
+    def puller(w):
+        while True:
+            start.wait()
+            if mode["quit"]:
+                return
             try:
-                for i, k in enumerate(keys):
-                    pushed[w][i].wait()
-                    if errors:
-                        return
-                    if view:
+                if mode["pull"] == "view":
+                    for i, k in enumerate(keys):
                         views[(w, i)] = grp.pull_view(k)
-                    else:
+                elif mode["pull"] == "copy":
+                    for i, k in enumerate(keys):
                         grp.pull(k, dsts[w][i])
             except Exception as e:  # noqa: BLE001 — reported below
                 errors.append(repr(e))
-        ts = [threading.Thread(target=pusher, args=(w,)) for w in range(n_workers)]
-        if not init:
-            ts += [threading.Thread(target=puller, args=(w,)) for w in range(n_workers)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
+            end.wait()
+    ts = [threading.Thread(target=f, args=(w,), daemon=True)
+          for w in range(n_workers) for f in (pusher, puller)]
+    for th in ts:
+        th.start()
+
+    def rnd(pull):
+        mode["pull"] = pull
+        start.wait(timeout=120)
+        end.wait(timeout=120)
         if errors:
             raise RuntimeError(errors[0])
     want = host[0].clone()
@@ -900,42 +961,58 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
         want += h
     wantb = want.view(torch.uint8)
 
-    def timed(view):
-        rnd(view=view)
+    def timed(pull):
+        rnd(pull)
         times = []
         for _ in range(rounds):
             if multi:
                 dist.barrier()
             t0 = time.perf_counter()
-            rnd(view=view)
+            rnd(pull)
             times.append(time.perf_counter() - t0)
         return _max_over_ranks(dist, dev, [statistics.median(times)])[0]
 
-    rnd(init=True)
-    # copying pulls first: once a key has been viewed, the server mirrors
-    # every later round of it (one D2H more per round)
-    tc = timed(False)     # copying pulls into every worker's own buffer
-    ok = all(bool(torch.equal(o, wantb)) for o in outs)
-    t = timed(True)       # zero-copy pull responses (the views of the last round stay valid)
-    ok = ok and all(bool(torch.equal(torch.frombuffer(views[(w, i)], dtype=torch.uint8),
-                                     wantb[o:o + ln]))
-                    for w in range(n_workers) for i, (_, o, ln) in enumerate(parts))
+    try:
+        rnd(None)            # init round: pushes only
+        # copying pulls first: once a key has been viewed, the server mirrors
+        # every later round of it (one D2H more per round)
+        tc = timed("copy")   # copying pulls into every worker's own buffer
+        ok = all(bool(torch.equal(o, wantb)) for o in outs)
+        t = timed("view")    # zero-copy pull responses (the last round's views stay valid)
+        ok = ok and all(bool(torch.equal(torch.frombuffer(views[(w, i)], dtype=torch.uint8),
+                                         wantb[o:o + ln]))
+                        for w in range(n_workers) for i, (_, o, ln) in enumerate(parts))
+    finally:
+        mode["quit"] = True
+        try:
+            start.wait(timeout=30)
+        except threading.BrokenBarrierError:
+            pass
+        for th in ts:
+            th.join(timeout=30)
     ok = _all_true(dist, dev, ok)
     grp.close()
     total = world * n_workers * bucket_bytes
-    return {"workload": (f"config 1 per GPU: {n_workers} workers x {bucket_bytes >> 20} MiB fp32 "
-                         f"as {len(parts)} partitions in pinned host memory, one PS server "
-                         f"(byteps_server_group_*, one instance, djb2 hash) per GPU, a push "
-                         f"thread and a pull thread per worker, {world} GPU(s) / PCIe links"),
-            "pull": "host_view (zero-copy pull response, server.cc:42-70)",
-            "node_GiBps": round(total / t / GIB, 2),
-            "per_gpu_GiBps": round(n_workers * bucket_bytes / t / GIB, 2),
-            "round_ms": round(t * 1e3, 3),
-            "copying_pulls": {"node_GiBps": round(total / tc / GIB, 2),
-                              "per_gpu_GiBps": round(n_workers * bucket_bytes / tc / GIB, 2),
-                              "round_ms": round(tc * 1e3, 3)},
-            "rounds": rounds, "lanes": lanes,
-            "pcie_inclusive": True, "exact_vs_torch_sum": ok}
+    out = {"workload": (f"config 1 per GPU: {n_workers} workers x {bucket_bytes >> 20} MiB fp32 "
+                        f"as {len(parts)} partitions in pinned host memory, one PS server "
+                        f"(byteps_server_group_*, one instance, djb2 hash) per GPU; per worker "
+                        f"one push_many of its partitions (all in flight) and a pull thread, "
+                        f"{world} GPU(s) / PCIe links"),
+           "pull": "host_view (zero-copy pull response, server.cc:42-70)",
+           "node_GiBps": round(total / t / GIB, 2),
+           "per_gpu_GiBps": round(n_workers * bucket_bytes / t / GIB, 2),
+           "round_ms": round(t * 1e3, 3),
+           "copying_pulls": {"node_GiBps": round(total / tc / GIB, 2),
+                             "per_gpu_GiBps": round(n_workers * bucket_bytes / tc / GIB, 2),
+                             "round_ms": round(tc * 1e3, 3)},
+           "rounds": rounds, "lanes": lanes,
+           "pcie_inclusive": True, "exact_vs_torch_sum": ok}
+    if link and link.get("h2d_GBps"):
+        # the round's H2D (every worker's push) against the link's own H2D rate
+        h2d = link["h2d_GBps"] * 1e9
+        out["frac_of_link"] = round(n_workers * bucket_bytes / t / h2d, 4)
+        out["copying_pulls"]["frac_of_link"] = round(n_workers * bucket_bytes / tc / h2d, 4)
+    return out
 
 
 # --------------------------------------------------------------------------
@@ -1421,10 +1498,19 @@ def main(argv=None):
                     fold=None if cuda else _torch_fold, comm=comm)
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}
+        link = None
+        if cuda and not (args.no_server and args.no_e2e):
+            leg("pcie")
+            try:
+                link = line["pcie"] = pcie_leg(dev)
+            except Exception as e:  # report, never hide
+                line["pcie"] = {"error": repr(e)}
+        elif not cuda:
+            line["pcie"] = {"skipped": "the PCIe probe needs a GPU (--device cpu)"}
         leg("server_cfg1")
         if cuda and not args.no_server:
             try:
-                line["server_cfg1"] = server_group_leg(dev, world, rank)
+                line["server_cfg1"] = server_group_leg(dev, world, rank, link=link)
             except Exception as e:  # report, never hide
                 line["server_cfg1"] = {"error": repr(e)}
         elif not args.no_server:
@@ -1433,7 +1519,7 @@ def main(argv=None):
             leg("e2e_cfg5")
             try:
                 line["e2e_cfg5"] = e2e_leg(dev, world, rank,
-                                           bucket_bytes=args.e2e_bucket_mib << 20)
+                                           bucket_bytes=args.e2e_bucket_mib << 20, link=link)
             except Exception as e:  # report, never hide
                 line["e2e_cfg5"] = {"error": repr(e)}
 

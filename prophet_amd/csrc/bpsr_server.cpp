@@ -254,6 +254,12 @@ struct KeyState {
   std::atomic<int> kq_key{-1};
   bool keyed = false;
   bool round_copied = false;
+  // a copy of this round is covered only by the lane's copy mark (a batched
+  // device copy); otherwise every copy of the round recorded `copied` after
+  // itself on the lane's (in-order) copy stream, so the round's fold can wait
+  // for its own copies instead of every copy the lane has queued (a worker's
+  // push_many of host data queues all its partitions' H2D at once)
+  bool round_mark_copy = false;
   hipEvent_t copied = nullptr;
   hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
   bool has_done = false;
@@ -391,6 +397,9 @@ struct byteps_server {
   hipStream_t gate_stream = nullptr;
   hipEvent_t gate_ev = nullptr;
   std::atomic<uint64_t> gate_seq{0}, gate_done{0};
+  // events that bound a push_many's host copies in flight (push_many_host)
+  std::mutex ev_pool_mu;
+  std::vector<hipEvent_t> ev_pool;
 };
 
 namespace bpsr {
@@ -422,16 +431,9 @@ int bind_cached(const byteps_server* s) {
   return s->combine && t_bound_device == s->cfg.device ? 0 : force_device(s);
 }
 
-// Make the lane's fold stream wait for its copies, unless it already waits
-// for the latest copy mark (push_ready-only rounds have no copies to wait for).
-hipError_t wait_copies(Lane& L) {
-  const uint64_t c = L.copy_seq.load();
-  if (c != L.fold_copy_seen.load()) {
-    const hipError_t e = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
-    if (e != hipSuccess) return e;
-    L.fold_copy_seen.store(c);
-  }
-  // and for the pull copies issued from the stores (a fold rewrites a store)
+// Make the lane's fold stream wait for the pull copies issued from the
+// stores (a fold rewrites a store), unless it already waits for the latest.
+hipError_t wait_pull_copies(Lane& L) {
   const uint64_t p = L.pull_seq.load();
   if (p != L.fold_pull_seen.load()) {
     const hipError_t e = hipStreamWaitEvent(L.fold, L.d2h_mark, 0);
@@ -439,6 +441,19 @@ hipError_t wait_copies(Lane& L) {
     L.fold_pull_seen.store(p);
   }
   return hipSuccess;
+}
+
+// Make the lane's fold stream wait for its copies, unless it already waits
+// for the latest copy mark (push_ready-only rounds have no copies to wait for),
+// and for its pull copies.
+hipError_t wait_copies(Lane& L) {
+  const uint64_t c = L.copy_seq.load();
+  if (c != L.fold_copy_seen.load()) {
+    const hipError_t e = hipStreamWaitEvent(L.fold, L.copy_mark, 0);
+    if (e != hipSuccess) return e;
+    L.fold_copy_seen.store(c);
+  }
+  return wait_pull_copies(L);
 }
 
 // Hand a launch's completion event to the lane's completer (combining):
@@ -842,6 +857,7 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
   ks->keyed = keyed;  // a keyed consumer's fold, tracked by the keyed completer
   ks->fold_lane = keyed ? -1 : ks->lane;
   ks->round_copied = false;
+  ks->round_mark_copy = false;
   if (mark) {  // a single fold: its own event, and the lane's mark
     hipError_t e = hipEventRecord(ks->done, L.fold);
     if (e == hipSuccess) e = hipEventRecord(L.fold_mark, L.fold);
@@ -1250,6 +1266,7 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
     ks->fold_lane = ks->lane;
     ks->keyed = false;
     ks->round_copied = false;
+    ks->round_mark_copy = false;
     ks->has_done = true;
     ks->inited = true;
     std::fill(ks->got.begin(), ks->got.end(), 0);
@@ -1386,7 +1403,19 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
     Lane& L = *s->lanes[jobs[i].ks->lane];
     std::lock_guard<std::mutex> bg(L.batch_mu);
     std::vector<byteps_bucket_desc> d(e - i);
-    hipError_t we0 = wait_copies(L);  // every copy of the lane
+    // The rounds' copies: each round's own copy events when every copy of
+    // every round in the batch recorded one, else every copy of the lane.
+    bool lane_wide = false;
+    std::vector<hipEvent_t> evs;
+    for (size_t k = i; k < e && !lane_wide; ++k) {
+      KeyState* ks = jobs[k].ks;
+      std::lock_guard<std::mutex> g(ks->mu);
+      if (ks->round_mark_copy) lane_wide = true;
+      else if (ks->round_copied) evs.push_back(ks->copied);
+    }
+    hipError_t we0 = lane_wide ? wait_copies(L) : wait_pull_copies(L);
+    for (size_t k = 0; !lane_wide && we0 == hipSuccess && k < evs.size(); ++k)
+      we0 = hipStreamWaitEvent(L.fold, evs[k], 0);
     int rc = we0 == hipSuccess ? 0 : hip_fail(we0, "hipStreamWaitEvent");
     for (size_t k = i; k < e; ++k) {
       KeyState* ks = jobs[k].ks;
@@ -1683,16 +1712,14 @@ void* device_view(void* out, int location) {
   return nullptr;
 }
 
-// Copying pulls: hipMemcpyAsync (SDMA) by default — measured 2-6 % faster
-// than the copy kernel for blocking pulls and equal behind non-blocking
-// pushes (profiles/r02_cfg1_*); BPSR_SERVER_PULL_COPY=kernel writes device or
-// pinned destinations with the library's copy kernel instead.
-bool pull_by_kernel() {
-  static const bool on = [] {
-    const char* v = getenv("BPSR_SERVER_PULL_COPY");
-    return v && std::string(v) == "kernel";
-  }();
-  return on;
+// Copying pulls into pinned host memory: the library's copy kernel writes
+// the destination through its device view, so the D2H runs beside the push
+// H2D copies (SDMA) at the link's full-duplex rate — two SDMA copies, one per
+// direction, share ~54 GB/s, SDMA H2D + kernel D2H move 87 GB/s together
+// (tools/pcie_probe.py, r05s04).  Device destinations and pageable memory:
+// hipMemcpyAsync.
+void* pull_kernel_dst(void* out, int location) {
+  return location == BYTEPS_SERVER_HOST ? device_view(out, location) : nullptr;
 }
 
 KeyState* key_for_pull(byteps_server* s, uint64_t key) {
@@ -1906,6 +1933,7 @@ int byteps_server_destroy(byteps_server* s) {
   }
   if (s->kq) (void)byteps_reduce_blockq_destroy(s->kq);
   copysvc_destroy(s->svc);
+  for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
   if (s->gate_ev) (void)hipEventDestroy(s->gate_ev);
   if (s->gate_stream) (void)hipStreamDestroy(s->gate_stream);
   for (hipEvent_t e : s->kq_ev)
@@ -2224,6 +2252,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
     cj.ack.worker = worker;
     cj.direct = direct;
     ks->round_copied = true;
+    ks->round_mark_copy = true;
     {
       Lane& L = *s->lanes[ks->lane];
       std::lock_guard<std::mutex> g(L.comb_mu);
@@ -2356,15 +2385,15 @@ int byteps_server_pull(byteps_server* s, uint64_t key, void* out, size_t len, in
   s->n_pulls.add();
   s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
   // The copy runs on the lane's d2h stream behind the key's last issued fold,
-  // queued under the key lock (hipMemcpyAsync; the copy kernel on request,
-  // pull_by_kernel).  No per-thread
+  // queued under the key lock (the copy kernel into pinned host memory,
+  // pull_kernel_dst; hipMemcpyAsync otherwise).  No per-thread
   // streams: a transport's pull threads come and go, and a stream per thread
   // (round 1) cost a stream creation per new thread and multiplied the
   // streams sharing the process's few hardware queues.
   Lane& L = *s->lanes[ks->lane];
   hipError_t e = ks->has_done ? hipStreamWaitEvent(L.d2h, ks->fold_ev, 0) : hipSuccess;
   if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-  void* dv = pull_by_kernel() ? device_view(out, location) : nullptr;
+  void* dv = pull_kernel_dst(out, location);
   if (dv) {
     if ((rc = byteps_reduce_copy(dv, ks->store, len, L.d2h))) return rc;
   } else {
@@ -2586,6 +2615,120 @@ int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n,
   return issue_deferred(s, defer);
 }
 
+// A push_many's host copies in flight at most (per call): 4 partitions of
+// BytePS's 4,096,000-B bound.  The transport's calls of different workers then
+// interleave on the link partition by partition, so rounds complete — and are
+// folded and pulled back — while later partitions are still crossing PCIe,
+// instead of one worker's whole batch landing before any other worker's.
+constexpr size_t kHostPushInflight = 16u << 20;
+
+hipEvent_t pool_take(byteps_server* s) {
+  {
+    std::lock_guard<std::mutex> g(s->ev_pool_mu);
+    if (!s->ev_pool.empty()) {
+      hipEvent_t e = s->ev_pool.back();
+      s->ev_pool.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
+}
+
+void pool_give(byteps_server* s, hipEvent_t e) {
+  std::lock_guard<std::mutex> g(s->ev_pool_mu);
+  s->ev_pool.push_back(e);
+}
+
+// byteps_server_push_many from host memory, in BytePS's order (core_loops.cc:
+// 492-564 issues every partition's ZPush as it comes): key by key, the H2D
+// copy into the slot on the key's lane (its own `copied` event, and the lane's
+// copy mark), then the arrival, whose completed round goes to the issuer at
+// once — with at most kHostPushInflight bytes of this call's copies in flight.
+// Every slot was found free before (the caller's step 1).  Returns once every
+// copy has landed (the blocking contract).
+int push_many_host(byteps_server* s, std::vector<KeyState*>& ks_of, const void* const* datas,
+                   const size_t* lens, int n, int worker) {
+  struct Flight {
+    hipEvent_t ev;
+    size_t bytes;
+  };
+  std::deque<Flight> flight;
+  size_t in_flight = 0;
+  int rc = 0;
+  auto retire = [&](size_t need) -> int {
+    while (!flight.empty() && (need == 0 || in_flight + need > kHostPushInflight)) {
+      const hipError_t e = hipEventSynchronize(flight.front().ev);
+      pool_give(s, flight.front().ev);
+      in_flight -= flight.front().bytes;
+      flight.pop_front();
+      if (e != hipSuccess) return hip_fail(e, "push copy");
+    }
+    return 0;
+  };
+  std::vector<char> lane_ready(s->lanes.size(), 0);
+  std::vector<FoldJob> defer;
+  for (int i = 0; i < n && !rc; ++i) {
+    KeyState* ks = ks_of[i];
+    Lane& L = *s->lanes[ks->lane];
+    if ((rc = retire(lens[i]))) break;
+    hipEvent_t fe = pool_take(s);
+    if (!fe) {
+      rc = fail(BYTEPS_REDUCE_EHIP, "hipEventCreate (push window)");
+      break;
+    }
+    {
+      std::lock_guard<std::mutex> bg(L.batch_mu);
+      hipError_t e = hipSuccess;
+      if (!lane_ready[ks->lane]) {  // once per lane: behind the lane's folds so far
+        lane_ready[ks->lane] = 1;
+        e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
+      }
+      {
+        std::lock_guard<std::mutex> g(ks->mu);
+        // keyed folds run on the consumer's stream, not behind the fold mark
+        if (e == hipSuccess && ks->keyed && ks->has_done)
+          e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(ks->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice, L.copy);
+        if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
+      }
+      if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
+      if (e == hipSuccess) L.copy_seq.fetch_add(1);
+      if (e == hipSuccess) e = hipEventRecord(fe, L.copy);
+      if (e != hipSuccess) {
+        pool_give(s, fe);
+        rc = hip_fail(e, "push copy");
+        break;
+      }
+    }
+    flight.push_back({fe, lens[i]});
+    in_flight += lens[i];
+    std::unique_lock<std::mutex> lk(ks->mu);
+    ks->round_copied = true;
+    const bool init_round = !ks->inited;
+    if ((rc = arrive(s, ks, worker, &defer))) break;
+    if (init_round && !ks->inited) {  // held until every worker's init push is in
+      lk.unlock();
+      if ((rc = issue_deferred(s, defer))) break;
+      lk.lock();
+      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
+      if (ks->error) {
+        rc = key_error(ks);
+        break;
+      }
+    }
+    lk.unlock();
+    if (!defer.empty() && (rc = issue_deferred(s, defer))) break;
+  }
+  if (!defer.empty()) {
+    const int r2 = issue_deferred(s, defer);
+    if (!rc) rc = r2;
+  }
+  const int r3 = retire(0);
+  return rc ? rc : r3;
+}
+
 int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* const* datas,
                             const size_t* lens, int n, int worker, int dtype, int location) {
   if (!s || n < 0 || (n > 0 && (!keys || !datas || !lens)))
@@ -2610,6 +2753,11 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     if (ks->error) return key_error(ks);
     by_lane[ks->lane].push_back(i);
   }
+  // host data (the default engine, sync mode): copies and arrivals key by key
+  if (location == BYTEPS_SERVER_HOST && s->combine && !s->cfg.async_mode) {
+    if ((rc = push_many_host(s, ks_of, datas, lens, n, worker))) return rc;
+    return BYTEPS_REDUCE_OK;
+  }
   for (size_t l = 0; l < by_lane.size(); ++l) {
     if (by_lane[l].empty()) continue;
     Lane& L = *s->lanes[l];
@@ -2628,9 +2776,15 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
         if ((e = hipStreamWaitEvent(L.copy, w, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
     }
     if (location == BYTEPS_SERVER_HOST) {
+      // each key's own copy event: its round folds once ITS copies have
+      // landed, while the lane's later partitions are still crossing PCIe
       for (int i : by_lane[l]) {
         e = hipMemcpyAsync(ks_of[i]->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice,
                            L.copy);
+        if (e == hipSuccess) {
+          std::lock_guard<std::mutex> g(ks_of[i]->mu);
+          e = hipEventRecord(ks_of[i]->copied, L.copy);
+        }
         if (e != hipSuccess) return hip_fail(e, "push copy");
       }
     } else {
@@ -2657,6 +2811,7 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
     KeyState* ks = ks_of[i];
     std::unique_lock<std::mutex> lk(ks->mu);
     ks->round_copied = true;
+    if (location != BYTEPS_SERVER_HOST) ks->round_mark_copy = true;
     const bool init_round = !ks->inited;
     if ((rc = arrive(s, ks, worker, &defer))) {
       lk.unlock();
@@ -2718,6 +2873,10 @@ int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const*
       if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
       if (location == BYTEPS_SERVER_HOST) {
         for (int i : ready[l]) {
+          if (void* dv = pull_kernel_dst(outs[i], location)) {
+            if (int rc = byteps_reduce_copy(dv, ks_of[i]->store, lens[i], L.d2h)) return rc;
+            continue;
+          }
           e = hipMemcpyAsync(outs[i], ks_of[i]->store, lens[i], hipMemcpyDeviceToHost, L.d2h);
           if (e != hipSuccess) return hip_fail(e, "pull copy");
         }
@@ -2903,5 +3062,12 @@ void server_fail_key(byteps_server* s, uint64_t key, int rc) {
 }
 
 bool server_pulls_async(const byteps_server* s) { return s->combine && !s->cfg.async_mode; }
+
+bool server_key_inited(byteps_server* s, uint64_t key) {
+  KeyState* ks = get_key(s, key, false);
+  if (!ks) return false;
+  std::lock_guard<std::mutex> g(ks->mu);
+  return ks->inited;
+}
 
 }  // namespace bpsr

@@ -115,6 +115,14 @@ struct Acks {
   std::condition_variable cv;
   int remaining = 0;
   int status = 0;
+  std::vector<size_t> inst_bytes;  // host pieces not acknowledged yet, per instance
+};
+
+// One host piece's acknowledgement: its bytes leave the instance's window.
+struct PieceAck {
+  Acks* a;
+  size_t inst;
+  size_t len;
 };
 
 void ack_cb(void* ctx, uint64_t, int, int status) {
@@ -234,6 +242,25 @@ struct PushPiece {
   bool split;  // one piece of a range-split key (stamped)
   int pos;
 };
+// A call's host pieces in flight at most per instance (one PCIe link each):
+// 4 of BytePS's 4,096,000-B partitions.  Different workers' calls (transport
+// threads) then interleave on the link partition by partition, so a key's
+// round completes — and is folded and pulled back — while later partitions
+// are still crossing, instead of after one worker's whole batch
+// (core_loops.cc:492-564 sends every partition as it is ready; the network
+// interleaves the workers).  Measured r05s09/r05s10 (profiles/README.md).
+constexpr size_t kHostPieceWindow = 16u << 20;
+
+void piece_ack_cb(void* ctx, uint64_t, int, int status) {
+  PieceAck* p = static_cast<PieceAck*>(ctx);
+  Acks* a = p->a;
+  std::lock_guard<std::mutex> g(a->mu);
+  if (status && !a->status) a->status = status;
+  a->inst_bytes[p->inst] -= p->len;
+  --a->remaining;
+  a->cv.notify_all();
+}
+
 int scatter_pushes(byteps_server_group* g, std::vector<PushPiece>& pcs, int worker, int dtype,
                    int location) {
   for (const PushPiece& p : pcs)
@@ -249,18 +276,35 @@ int scatter_pushes(byteps_server_group* g, std::vector<PushPiece>& pcs, int work
     pcs[i].pos = stamp(g, pcs[i].key, worker);
   }
   Acks acks;
+  const bool windowed = location == BYTEPS_SERVER_HOST;
+  acks.inst_bytes.assign(g->inst.size(), 0);
+  std::vector<PieceAck> pa(pcs.size());
   int rc = 0;
   size_t queued = 0;
-  for (const PushPiece& p : pcs) {
+  for (size_t i = 0; i < pcs.size(); ++i) {
+    const PushPiece& p = pcs[i];
+    size_t inst = 0;
+    while (inst < g->inst.size() && g->inst[inst] != p.s) ++inst;
+    // init pushes are answered only once every worker's is in: outside the
+    // window, or workers pushing their keys in different orders would wait
+    // for each other's windows
+    const bool counted = windowed && bpsr::server_key_inited(p.s, p.key);
+    pa[i] = {&acks, inst, counted ? p.len : 0};
     {
-      std::lock_guard<std::mutex> lk(acks.mu);
+      std::unique_lock<std::mutex> lk(acks.mu);
+      if (counted)  // the instance's window (a piece larger than it goes alone)
+        acks.cv.wait(lk, [&] {
+          return acks.inst_bytes[inst] == 0 || acks.inst_bytes[inst] + p.len <= kHostPieceWindow;
+        });
       ++acks.remaining;
+      acks.inst_bytes[inst] += pa[i].len;
     }
-    rc = bpsr::server_push_async_at(p.s, p.key, worker, p.data, p.len, dtype, location, ack_cb,
-                                    &acks, p.pos);
+    rc = bpsr::server_push_async_at(p.s, p.key, worker, p.data, p.len, dtype, location,
+                                    piece_ack_cb, &pa[i], p.pos);
     if (rc) {
       std::lock_guard<std::mutex> lk(acks.mu);
       --acks.remaining;
+      acks.inst_bytes[inst] -= pa[i].len;
       break;
     }
     ++queued;

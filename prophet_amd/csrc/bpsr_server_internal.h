@@ -22,6 +22,9 @@ int server_check_key(byteps_server* s, uint64_t key, size_t len, int dtype);
 // Fail `key` on this instance as a failed fold would: every waiter and every
 // later call on it gets `rc`.
 void server_fail_key(byteps_server* s, uint64_t key, int rc);
+// Has the key's init round completed on this instance (false: unknown key)?
+// An init push is answered only once every worker's init push is in.
+bool server_key_inited(byteps_server* s, uint64_t key);
 // Does byteps_server_pull_into_async work on this instance (default engine,
 // sync mode)?
 bool server_pulls_async(const byteps_server* s);

@@ -82,6 +82,12 @@ def test_bench_one_gpu_line_has_every_object():
     assert "error" not in srv, srv
     assert srv["exact_vs_torch_sum"] is True and srv["node_GiBps"] > 0
     assert srv["pull"].startswith("host_view") and srv["copying_pulls"]["node_GiBps"] > 0
+    # the link measured in the same run, and each host-resident object's share of it
+    link = line["pcie"]
+    assert "error" not in link, link
+    assert link["h2d_GBps"] > 1 and link["d2h_GBps"] > 1 and link["bidir_GBps"] > 1
+    assert 0 < srv["frac_of_link"] < 1.5 and 0 < srv["copying_pulls"]["frac_of_link"] < 1.5
+    assert 0 < e2e["frac_of_link"] < 1.5
 
 
 def test_server_group_leg_matches_oracle():

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +101,34 @@ int main() {
       CK(hipMemcpy(h.data(), dst[t], 8u << 20, hipMemcpyDeviceToHost));
       if (h[0] != (char)(t + 1) || h[(8u << 20) - 1] != (char)(t + 1)) printf("MISMATCH t=%d\n", t);
     }
+  }
+  {  // a device-wide synchronisation while 8 threads copy through the service
+    const int T = 8;
+    std::vector<char*> src(T), dst(T);
+    for (int t = 0; t < T; ++t) {
+      CK(hipMalloc(&src[t], 1u << 20));
+      CK(hipMalloc(&dst[t], 1u << 20));
+    }
+    std::atomic<bool> stop{false};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        while (!stop.load())
+          if (bpsr::copysvc_copy(svc, dst[t], src[t], 64u << 10)) std::abort();
+      });
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    std::vector<double> s;
+    for (int i = 0; i < 200; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      CK(hipDeviceSynchronize());
+      s.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+      std::this_thread::sleep_for(std::chrono::microseconds(1500));
+    }
+    stop.store(true);
+    for (auto& x : th) x.join();
+    std::sort(s.begin(), s.end());
+    printf("{\"device_sync_under_8_copiers_us\": {\"p50\": %.0f, \"p90\": %.0f, \"p99\": %.0f, \"max\": %.0f}}\n",
+           s[s.size() / 2], s[s.size() * 9 / 10], s[s.size() * 99 / 100], s.back());
   }
   printf("launches %llu\n", (unsigned long long)bpsr::copysvc_launches(svc));
   bpsr::copysvc_destroy(svc);
