@@ -755,8 +755,9 @@ def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int =
     ``StreamingReducer`` (H2D, fold and D2H on three streams; ``reduce_from_host``
     with the aggregate pulled back), over its own PCIe link, no collective.
     Node rate = all pushed bytes / (max over ranks of the blocking call);
-    ``frac_of_link`` = this GPU's H2D rate (its slices of the pushes) over the
-    same run's measured pinned H2D rate (``link``).  PCIe-inclusive: never
+    ``frac_of_link`` = the link's shortest time for this GPU's H2D (its slices
+    of the pushes) and D2H (the aggregate slice) over the measured time
+    (link_bound_s, ``link`` measured in the same run).  PCIe-inclusive: never
     ``value``.  Exactness: strided windows of the pulled
     slice against torch's own bf16 left fold (fp32 add, RNE to bf16 per add)
     of the same windows on the device."""
@@ -808,8 +809,7 @@ def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int =
            "per_gpu_e2e_GiBps": round(n_workers * nb / t / GIB, 1),
            "ms": round(t * 1e3, 2), "reps": reps, "pcie_inclusive": True,
            "exact_vs_torch_fold_windows": ok}
-    if link and link.get("h2d_GBps"):
-        out["frac_of_link"] = round(n_workers * nb / t / (link["h2d_GBps"] * 1e9), 4)
+    out.update(link_fracs(n_workers * nb, nb, t, link))    # every push in, the aggregate out
     return out
 
 
@@ -817,12 +817,40 @@ def e2e_leg(dev, world: int, rank: int, n_workers: int = 16, bucket_bytes: int =
 # config 1 through the PS server group, host-resident, one server per GPU
 
 
-def pcie_leg(dev, nbytes: int = 64 << 20, reps: int = 10) -> dict:
+def link_bound_s(h2d_bytes: float, d2h_bytes: float, link: dict) -> float:
+    """Shortest time this GPU's link (``pcie_leg``'s measured rates) can move
+    ``h2d_bytes`` in and ``d2h_bytes`` out: while both directions run each gets
+    half the measured both-ways rate (the link shares it: 2 x ~43 GB/s, not
+    2 x 54), the rest goes at its own one-way rate."""
+    both = min(h2d_bytes, d2h_bytes)
+    t = both / (link["bidir_GBps"] * 1e9 / 2)
+    if h2d_bytes > d2h_bytes:
+        t += (h2d_bytes - d2h_bytes) / (link["h2d_GBps"] * 1e9)
+    else:
+        t += (d2h_bytes - h2d_bytes) / (link["d2h_GBps"] * 1e9)
+    return t
+
+
+def link_fracs(h2d_bytes: float, d2h_bytes: float, t: float, link: dict | None) -> dict:
+    """A host-resident object's use of the link: ``frac_of_link`` = the
+    link's shortest time for the object's H2D + D2H bytes (link_bound_s) over
+    its measured time; ``frac_of_h2d`` = its H2D rate over the link's one-way
+    H2D rate (ignores the D2H the object must also move)."""
+    if not link or not link.get("h2d_GBps"):
+        return {}
+    return {"frac_of_link": round(link_bound_s(h2d_bytes, d2h_bytes, link) / t, 4),
+            "frac_of_h2d": round(h2d_bytes / t / (link["h2d_GBps"] * 1e9), 4),
+            "link_bound_ms": round(link_bound_s(h2d_bytes, d2h_bytes, link) * 1e3, 3)}
+
+
+def pcie_leg(dev, red=None, nbytes: int = 64 << 20, reps: int = 10) -> dict:
     """This GPU's PCIe link, measured in the same run as the host-resident
     objects (their rate "including H2D and D2H" needs the link's
-    own rate beside it): pinned host <-> HBM copies of ``nbytes`` on a side
-    stream, H2D alone, D2H alone, and both at once on two streams (the link is
-    full duplex); median over ``reps`` of HIP-event timings."""
+    own rate beside it): pinned host <-> HBM copies of ``nbytes`` on side
+    streams — H2D alone (SDMA, hipMemcpyAsync), D2H alone (SDMA), and both at
+    once the way the server moves them (SDMA H2D + the copy kernel writing
+    pinned host memory: two SDMA copies share one engine's ~54 GB/s, this mix
+    runs full duplex, tools/pcie_probe.py); median over ``reps``."""
     import torch
     h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
     h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
@@ -849,15 +877,23 @@ def pcie_leg(dev, nbytes: int = 64 << 20, reps: int = 10) -> dict:
         with torch.cuda.stream(s2):
             h2.copy_(d2, non_blocking=True)
 
+    def d2h_kernel():
+        red.copy(h2, d2, nbytes, stream=s2)
+
     def both():
         h2d()
+        d2h_kernel() if red is not None else d2h()
+
+    def both_sdma():
+        h2d()
         d2h()
-    t_h2d, t_d2h, t_both = timed(h2d), timed(d2h), timed(both)
+    t_h2d, t_d2h, t_both, t_bs = timed(h2d), timed(d2h), timed(both), timed(both_sdma)
     return {"workload": f"pinned host <-> HBM copies of {nbytes >> 20} MiB on side streams "
-                        f"(median of {reps})",
+                        f"(median of {reps}); bidir = SDMA H2D + copy-kernel D2H at once",
             "h2d_GBps": round(nbytes / t_h2d / 1e9, 2),
             "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
-            "bidir_GBps": round(2 * nbytes / t_both / 1e9, 2)}
+            "bidir_GBps": round(2 * nbytes / t_both / 1e9, 2),
+            "bidir_sdma_only_GBps": round(2 * nbytes / t_bs / 1e9, 2)}
 
 
 def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
@@ -886,8 +922,8 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
     worker).  The threads persist across rounds (a barrier starts each).  Weak
     scaling: at N GPUs, N buckets over N PCIe links.  Node rate = all ranks'
     pushed bytes / the slowest rank's median round; ``frac_of_link`` = the
-    per-GPU push (H2D) rate over the same run's measured pinned H2D rate
-    (``link``).  PCIe-inclusive; compare with ``cpu_baseline`` (the
+    link's shortest time for the round's H2D and D2H bytes (link_bound_s, from
+    the same run's measured rates ``link``) over the round.  PCIe-inclusive; compare with ``cpu_baseline`` (the
     reference's host-core round).  Exactness: every worker's pull equals
     torch's sum of the two pushes (fp32, two operands: the left fold in either
     arrival order)."""
@@ -1007,12 +1043,106 @@ def server_group_leg(dev, world: int, rank: int, n_workers: int = 2,
                              "round_ms": round(tc * 1e3, 3)},
            "rounds": rounds, "lanes": lanes,
            "pcie_inclusive": True, "exact_vs_torch_sum": ok}
-    if link and link.get("h2d_GBps"):
-        # the round's H2D (every worker's push) against the link's own H2D rate
-        h2d = link["h2d_GBps"] * 1e9
-        out["frac_of_link"] = round(n_workers * bucket_bytes / t / h2d, 4)
-        out["copying_pulls"]["frac_of_link"] = round(n_workers * bucket_bytes / tc / h2d, 4)
+    # the link: every worker's push in; one D2H per partition (views: the
+    # shared mirror) or one per worker (copying pulls) out
+    out.update(link_fracs(n_workers * bucket_bytes, bucket_bytes, t, link))
+    out["copying_pulls"].update(link_fracs(n_workers * bucket_bytes, n_workers * bucket_bytes,
+                                           tc, link))
     return out
+
+
+def server_cfg3_leg(dev, rounds: int = 20, lanes: int = 4, N: int = 8) -> dict:
+    """BASELINE config 3's keys through the GPU-resident PS server on this GPU,
+    in the reference server's shape (server.cc:147-308 behind ps-lite's ONE
+    receive thread, server.cc:149): 8 workers' ResNet-50 fp16 gradients as the
+    165 BytePS partitions (keys in Prophet block order) sit in the receive
+    slots (an RDMA transport's writes into HBM); per round the receive thread
+    signals every arrival (byteps_server_push_ready) and answers every pull
+    with a zero-copy device view of the store
+    (byteps_server_pull_device_view); the round ends with the last view, i.e.
+    every key folded.  The timed loop is native (tools/cfg3srv_drv.cpp through
+    ctypes: no Python per call).  Two ways: ``launch`` — the default path,
+    lane issuers batching each completed round into fold launches; and
+    ``device_releases`` — BPSR_SERVER_RELEASE=device, one keyed consumer
+    launch per epoch releasing each key on the device when its last push
+    arrives.  Median round over ``rounds``; ``frac_of_roofline`` =
+    (N + 1) x 51,114,064 B / round / 8 TB/s.  Exactness: one further round
+    pulls every key into every worker's buffer, checked bit for bit against
+    torch's own fp16 left fold (fp32 add, RNE per add) in the arrival order
+    the server recorded for each key."""
+    import ctypes
+    import torch
+    from prophet_amd.buckets import partition_all, prophet_blocks, resnet50_param_sizes
+    drv_path = os.path.join(ROOT, "tools", "libcfg3srv.so")
+    if not os.path.exists(drv_path):
+        raise RuntimeError(f"{drv_path} not built (make -C tools)")
+    drv = ctypes.CDLL(drv_path)
+    _vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    drv.cfg3srv_run.argtypes = [_int, ctypes.POINTER(_sz), ctypes.POINTER(_sz), _int,
+                                ctypes.POINTER(_vp), ctypes.POINTER(_vp), _int, _int,
+                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_int)]
+    sizes = [n * 2 for n in resnet50_param_sizes()]
+    parts = partition_all(sizes)
+    toff = [0]
+    for n in sizes:
+        toff.append(toff[-1] + n)
+    total = toff[-1]
+    table = [p for blk in prophet_blocks(len(sizes)) for p in parts if p.tensor in set(blk)]
+    np_ = len(table)
+    offs = (_sz * np_)(*[toff[p.tensor] + p.offset for p in table])
+    lens = (_sz * np_)(*[p.len for p in table])
+    gen = torch.Generator(device=dev)
+    grads = []
+    for k in range(N):
+        gen.manual_seed(5000 + k)
+        grads.append(torch.randn(total // 2, device=dev, generator=gen).half())
+    outs = [torch.empty_like(g) for g in grads]
+    torch.cuda.synchronize()
+    alg = (N + 1) * total
+    res_all = {}
+    for name, rel in (("launch", None), ("device_releases", "device")):
+        old = os.environ.pop("BPSR_SERVER_RELEASE", None)
+        if rel:
+            os.environ["BPSR_SERVER_RELEASE"] = rel
+        res = (ctypes.c_double * 8)()
+        orders = (_int * (np_ * N))()
+        for o in outs:
+            o.fill_(float("nan"))
+        torch.cuda.synchronize()
+        try:
+            rc = drv.cfg3srv_run(np_, offs, lens, N, (_vp * N)(*[g.data_ptr() for g in grads]),
+                                 (_vp * N)(*[o.data_ptr() for o in outs]), rounds, lanes, res,
+                                 orders)
+        finally:
+            os.environ.pop("BPSR_SERVER_RELEASE", None)
+            if old is not None:
+                os.environ["BPSR_SERVER_RELEASE"] = old
+        if rc:
+            raise RuntimeError(f"cfg3srv_run ({name}) returned {rc}")
+        ok = True
+        for i, p in enumerate(table):
+            lo = (toff[p.tensor] + p.offset) // 2
+            n = p.len // 2
+            order = [orders[i * N + w] for w in range(N)]
+            ok = ok and sorted(order) == list(range(N))
+            acc = grads[order[0]][lo:lo + n].clone()
+            for w in order[1:]:
+                acc.add_(grads[w][lo:lo + n])
+            want = acc.view(torch.int16)
+            ok = ok and all(bool(torch.equal(o[lo:lo + n].view(torch.int16), want)) for o in outs)
+        ms = res[0]
+        res_all[name] = {"round_ms": round(ms, 4), "min_ms": round(res[1], 4),
+                         "max_ms": round(res[7], 4), "push_phase_ms": round(res[2], 4),
+                         "frac_of_roofline": round(alg / (ms * 1e-3) / (HBM_PEAK_GBPS * 1e9), 4),
+                         "fold_launches_per_round": round(res[3], 1),
+                         "consumer_launches_per_round": round(res[4], 2),
+                         "key_releases_per_round": round(res[5], 1),
+                         "exact_vs_torch_fold_in_recorded_order": ok}
+    return {"workload": (f"config 3's keys through the PS server: {N} workers' ResNet-50 fp16 "
+                         f"({total} B each) as {np_} BytePS partitions in the receive slots; ONE "
+                         f"receive thread per round: push_ready for every (key, worker), then a "
+                         f"device view per pull (tools/cfg3srv_drv.cpp, native)"),
+            "alg_bytes_per_round": alg, "rounds": rounds, "lanes": lanes, **res_all}
 
 
 # --------------------------------------------------------------------------
@@ -1502,7 +1632,7 @@ def main(argv=None):
         if cuda and not (args.no_server and args.no_e2e):
             leg("pcie")
             try:
-                link = line["pcie"] = pcie_leg(dev)
+                link = line["pcie"] = pcie_leg(dev, red)
             except Exception as e:  # report, never hide
                 line["pcie"] = {"error": repr(e)}
         elif not cuda:
@@ -1535,6 +1665,11 @@ def main(argv=None):
                 line["cfg3_blockq"] = cfg3_leg(dev, red)
             except Exception as e:  # report, never hide
                 line["cfg3_blockq"] = {"error": repr(e)}
+        if cuda and not args.no_cfg3 and not args.no_server:
+            try:
+                line["server_cfg3"] = server_cfg3_leg(dev)
+            except Exception as e:  # report, never hide
+                line["server_cfg3"] = {"error": repr(e)}
         if rank == 0 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(N, int(dtype_id), args.cpu_sample_mib)

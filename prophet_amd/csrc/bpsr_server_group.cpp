@@ -243,13 +243,18 @@ struct PushPiece {
   int pos;
 };
 // A call's host pieces in flight at most per instance (one PCIe link each):
-// 4 of BytePS's 4,096,000-B partitions.  Different workers' calls (transport
+// one of BytePS's 4,096,000-B partitions (a larger piece goes alone).  Different workers' calls (transport
 // threads) then interleave on the link partition by partition, so a key's
 // round completes — and is folded and pulled back — while later partitions
 // are still crossing, instead of after one worker's whole batch
 // (core_loops.cc:492-564 sends every partition as it is ready; the network
-// interleaves the workers).  Measured r05s09/r05s10 (profiles/README.md).
-constexpr size_t kHostPieceWindow = 16u << 20;
+// interleaves the workers).  Config 1's first round completes at 0.6-0.8 ms
+// instead of 1.1-1.2 (16 MiB window) or 1.8-2.0 ms (none); rounds with
+// copying pulls 4.2-4.4 ms instead of 5.0-5.4 (r05s12, profiles/README.md).
+#ifndef BPSR_HOST_PIECE_WINDOW  // (probe builds only: tools/cfg1_round_probe.py --lib)
+#define BPSR_HOST_PIECE_WINDOW (4u << 20)
+#endif
+constexpr size_t kHostPieceWindow = BPSR_HOST_PIECE_WINDOW;
 
 void piece_ack_cb(void* ctx, uint64_t, int, int status) {
   PieceAck* p = static_cast<PieceAck*>(ctx);
@@ -494,6 +499,18 @@ int byteps_server_group_init_key(byteps_server_group* g, uint64_t key, size_t le
   return declare(g, key, len, dtype);
 }
 
+// Would every instance holding a piece of `key` accept a push of `len`
+// bytes of `dtype`?  Checked before the group declares the key on first sight,
+// so a refused first push leaves no declaration behind (as init_key: the
+// instances first, then the group).
+int check_pieces(byteps_server_group* g, uint64_t key, size_t len, int dtype) {
+  std::vector<Piece> ps;
+  route(g, key, len, &ps);
+  for (const Piece& p : ps)
+    if (int rc = bpsr::server_check_key(g->inst[p.server], key, p.len, dtype)) return rc;
+  return 0;
+}
+
 int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, const void* data,
                              size_t len, int dtype, int location) {
   int rc = check_group(g);
@@ -502,7 +519,7 @@ int byteps_server_group_push(byteps_server_group* g, uint64_t key, int worker, c
   if (worker < 0 || worker >= g->cfg.server.num_workers)
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker,
                 g->cfg.server.num_workers);
-  if ((rc = declare(g, key, len, dtype))) return rc;
+  if ((rc = check_pieces(g, key, len, dtype)) || (rc = declare(g, key, len, dtype))) return rc;
   std::vector<Piece> ps;
   route(g, key, len, &ps);
   const char* d = static_cast<const char*>(data);
@@ -569,8 +586,10 @@ int byteps_server_group_push_many(byteps_server_group* g, const uint64_t* keys,
   std::vector<Piece> ps;
   for (int i = 0; i < n; ++i) {
     if (!datas[i]) return fail(BYTEPS_REDUCE_EARGS, "null data for key %d", i);
-    if ((rc = declare(g, keys[i], lens[i], dtype))) return rc;
+    if ((rc = check_pieces(g, keys[i], lens[i], dtype))) return rc;
   }
+  for (int i = 0; i < n; ++i)
+    if ((rc = declare(g, keys[i], lens[i], dtype))) return rc;
   if (g->cfg.server.engine_blocking) {
     // the engine's blocking contract: each instance's keys as one batched call
     const size_t ns = g->inst.size();

@@ -75,6 +75,13 @@ def test_bench_one_gpu_line_has_every_object():
     assert c3["exact_vs_torch_fold"] is True
     for k in ("live", "pre_released"):
         assert 0 < c3[k]["frac_of_roofline"] < 1
+    s3 = line["server_cfg3"]             # config 3's keys through the server, two ways
+    assert "error" not in s3, s3
+    for k in ("launch", "device_releases"):
+        assert s3[k]["exact_vs_torch_fold_in_recorded_order"] is True, s3[k]
+        assert 0 < s3[k]["frac_of_roofline"] < 1
+    assert s3["device_releases"]["consumer_launches_per_round"] >= 1
+    assert s3["launch"]["consumer_launches_per_round"] == 0
     e2e = line["e2e_cfg5"]
     assert "error" not in e2e, e2e
     assert e2e["exact_vs_torch_fold_windows"] is True and e2e["pcie_inclusive"] is True
@@ -86,8 +93,9 @@ def test_bench_one_gpu_line_has_every_object():
     link = line["pcie"]
     assert "error" not in link, link
     assert link["h2d_GBps"] > 1 and link["d2h_GBps"] > 1 and link["bidir_GBps"] > 1
-    assert 0 < srv["frac_of_link"] < 1.5 and 0 < srv["copying_pulls"]["frac_of_link"] < 1.5
-    assert 0 < e2e["frac_of_link"] < 1.5
+    for obj in (srv, srv["copying_pulls"], e2e):
+        assert 0 < obj["frac_of_link"] < 1.5 and 0 < obj["frac_of_h2d"] < 1.5, obj
+        assert obj["link_bound_ms"] > 0
 
 
 def test_server_group_leg_matches_oracle():

@@ -107,6 +107,23 @@ def test_rccl_problems_rule():
     assert any("share a GPU" in s for s in bench.rccl_problems(shared, 8))
 
 
+def test_link_bound_model():
+    """bench.link_bound_s: H2D and D2H share the measured both-ways rate while
+    both run, the rest goes one way; link_fracs reports the object's time
+    against that bound and its H2D rate against the one-way rate."""
+    sys.path.insert(0, ROOT)
+    import bench
+    L = {"h2d_GBps": 50.0, "d2h_GBps": 40.0, "bidir_GBps": 80.0}
+    assert abs(bench.link_bound_s(100e9, 0, L) - 2.0) < 1e-12          # one way, H2D
+    assert abs(bench.link_bound_s(0, 80e9, L) - 2.0) < 1e-12           # one way, D2H
+    assert abs(bench.link_bound_s(80e9, 80e9, L) - 2.0) < 1e-12        # both: 40 + 40
+    assert abs(bench.link_bound_s(120e9, 40e9, L) - (1.0 + 80e9 / 50e9)) < 1e-12
+    f = bench.link_fracs(120e9, 40e9, 5.2, L)
+    assert f["frac_of_link"] == round(2.6 / 5.2, 4) and f["link_bound_ms"] == 2600.0
+    assert f["frac_of_h2d"] == round(120e9 / 5.2 / 50e9, 4)
+    assert bench.link_fracs(1, 1, 1.0, None) == {}
+
+
 def test_rccl_check_failure_fails_the_run():
     """Every rank of a world-2 run whose communicator views say 'two ranks on
     one GPU' (test hook) exits RCCL_EXIT; rank 0 still prints the line, with

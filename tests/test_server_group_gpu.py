@@ -253,6 +253,51 @@ def test_group_push_validation_and_partial_failure():
     grp.close()
 
 
+@pytest.mark.parametrize("many", [False, True], ids=["push", "push_many"])
+def test_group_refused_first_push_declares_nothing(many):
+    """the first push of an undeclared key that an instance
+    refuses (a dtype it does not know) leaves no declaration in the group, so
+    the key's correct pushes then go through (whole and split keys) and fold
+    to the oracle's sum."""
+    from prophet_amd.reducer import EDTYPE, ReduceError
+    from prophet_amd.server import PSServerGroup
+    dt, N, n = DType.FLOAT32, 2, 70_001
+    grp = PSServerGroup(N, devices=[0, 0], split="range", split_min_bytes=4096)
+    keys = [5, 6]
+    sizes = [n, 3]                                       # split, and whole (< split_min)
+    ins = {(w, j): data(dt, sizes[j], w, 0, j) for w in range(N) for j in range(2)}
+    for j, k in enumerate(keys):
+        with pytest.raises(ReduceError) as e:
+            if many:
+                grp.push_many([k], 0, [ins[(0, j)]], 9)
+            else:
+                grp.push(k, 0, ins[(0, j)], 9)
+        assert e.value.code == EDTYPE
+    for rnd in range(2):
+        r = {(w, j): data(dt, sizes[j], w, rnd, j) for w in range(N) for j in range(2)}
+
+        def worker(w):
+            if many:
+                grp.push_many(keys, w, [r[(w, 0)], r[(w, 1)]], dt)
+            else:
+                for j, k in enumerate(keys):
+                    grp.push(k, w, r[(w, j)], dt)
+        ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+    for j, k in enumerate(keys):
+        out = np.zeros(sizes[j] * 4, np.uint8)
+        grp.pull(k, out)
+        # two fp32 operands: the left fold in either arrival order is one sum
+        want = np.zeros(sizes[j] * 4, np.uint8)
+        PortReducer(nthreads=4).sum_n(want, [data(dt, sizes[j], w, 1, j) for w in range(N)],
+                                      sizes[j] * 4, dt)
+        assert np.array_equal(out, want), k
+    grp.close()
+
+
 def test_group_host_view_of_whole_keys():
     """byteps_server_group_pull_host_view: a key held whole by one instance is
     answered with that instance's pinned mirror (the zero-copy pull response

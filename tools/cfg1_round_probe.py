@@ -21,8 +21,13 @@ def main():
     ap.add_argument("--pull", default="view", choices=["view", "copy", "none"])
     ap.add_argument("--lanes", type=int, default=4)
     ap.add_argument("--push", default="many", choices=["many", "single"])
+    ap.add_argument("--lib", default=None, help="another build of libbpsr.so (A/B)")
     a = ap.parse_args()
     import torch
+    torch.cuda.init()        # torch's HIP runtime first (as every product caller)
+    if a.lib:
+        from prophet_amd import reducer
+        reducer.load_library(a.lib)
     from prophet_amd.buckets import partition_tensor
     from prophet_amd.dtypes import DType
     from prophet_amd.server import PSServerGroup
@@ -67,7 +72,8 @@ def main():
         return stamps
     rnd("none")
     for r in range(a.rounds):
-        print(json.dumps({"round": r, "pull": a.pull, "push": a.push, **rnd(a.pull)}), flush=True)
+        print(json.dumps({"round": r, "pull": a.pull, "push": a.push, "lib": a.lib or "default",
+                          **rnd(a.pull)}), flush=True)
     grp.close()
 
 
