@@ -686,8 +686,9 @@ struct byteps_reduce_blockq {
   // per key, (arrival order << 32 | epoch) words, the control word in pinned
   // host memory so the server reads a timeout without a copy.
   bool keyed = false;
-  uint64_t* kwords = nullptr;       // device, one per block
-  uint64_t* khwords = nullptr;      // pinned host, two per block (epoch parity)
+  bool wide = false;                // 9..16 sources: a second word per block (positions 8..15)
+  uint64_t* kwords = nullptr;       // device, one per block [+ the second words after them]
+  uint64_t* khwords = nullptr;      // pinned host, two per block (epoch parity) [+ second words]
   uint64_t* khwords_dev = nullptr;
   BlockqCtl* hctl = nullptr;        // pinned host
   BlockqCtl* hctl_dev = nullptr;
@@ -864,6 +865,7 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   Q.helper = 0;
   Q.hflags = nullptr;
   Q.keyed = 0;
+  Q.wide = 0;
   Q.kwords = nullptr;
   Q.khwords = nullptr;
   Q.kcnt = nullptr;
@@ -1089,23 +1091,28 @@ int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double 
       return fail(BYTEPS_REDUCE_EARGS, "keyed queue: key %d has %d sources (1..%d)", k,
                   buckets[k].n, kKeyedMaxSrcs);
   std::vector<int> block_end((size_t)nkeys);
-  for (int k = 0; k < nkeys; ++k) block_end[(size_t)k] = k + 1;
+  bool wide = false;
+  for (int k = 0; k < nkeys; ++k) {
+    block_end[(size_t)k] = k + 1;
+    wide = wide || buckets[k].n > kKeyedNarrowSrcs;
+  }
   byteps_reduce_blockq* q = nullptr;
   int rc = byteps_reduce_blockq_create(buckets, nkeys, block_end.data(), nkeys, dtype,
                                        kModeReference, &q);
   if (rc) return rc;
   q->keyed = true;
+  q->wide = wide;
   if (timeout_s > 0) q->timeout_s = timeout_s;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q->kwords), sizeof(uint64_t) * (size_t)nkeys);
-  if (e == hipSuccess) e = hipMemset(q->kwords, 0, sizeof(uint64_t) * (size_t)nkeys);
+  const size_t nw = (size_t)nkeys * (wide ? 2 : 1);  // words per copy (device / host parity)
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q->kwords), sizeof(uint64_t) * nw);
+  if (e == hipSuccess) e = hipMemset(q->kwords, 0, sizeof(uint64_t) * nw);
   void* p = nullptr;
   void* d = nullptr;
   if (e == hipSuccess)
-    e = hipHostMalloc(&p, sizeof(uint64_t) * 2 * (size_t)nkeys,
-                      hipHostMallocCoherent | hipHostMallocMapped);
+    e = hipHostMalloc(&p, sizeof(uint64_t) * 2 * nw, hipHostMallocCoherent | hipHostMallocMapped);
   if (e == hipSuccess) {
     q->khwords = static_cast<uint64_t*>(p);
-    for (int i = 0; i < 2 * nkeys; ++i) __atomic_store_n(q->khwords + i, (uint64_t)0, __ATOMIC_RELEASE);
+    for (size_t i = 0; i < 2 * nw; ++i) __atomic_store_n(q->khwords + i, (uint64_t)0, __ATOMIC_RELEASE);
     e = hipHostGetDevicePointer(&d, p, 0);
     q->khwords_dev = static_cast<uint64_t*>(d);
   }
@@ -1155,6 +1162,7 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   Q.helper = 1;  // workgroup 0 forwards the host words
   Q.hflags = nullptr;
   Q.keyed = 1;
+  Q.wide = q->wide ? 1 : 0;
   Q.kwords = q->kwords;
   Q.khwords = q->khwords_dev;
   Q.kcnt = q->kcnt;
@@ -1192,13 +1200,18 @@ void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t
   *launched = keyq_launched(q);
 }
 
-int keyq_release(byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s) {
+int keyq_release(byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s) {
   const uint32_t ep = q->rel_epoch[(size_t)key] + 1;
-  const uint64_t w = key_word(perm, ep);
+  const uint64_t w = key_word((uint32_t)perm, ep);
+  const uint64_t w2 = key_word((uint32_t)(perm >> 32), ep);  // wide: positions 8..15
+  const size_t second = (size_t)q->nblocks + (size_t)key;
   if (s) {
-    const hipError_t e = launch_key_release(q->kwords, (uint32_t)key, w, s);
+    const hipError_t e = launch_key_release(q->kwords, (uint32_t)key, w,
+                                            q->wide ? q->kwords + second : nullptr, w2, s);
     if (e != hipSuccess) return hip_fail(e, "keyed release");
   } else {
+    // the second word first: the helper forwards a block once both carry the epoch
+    if (q->wide) __atomic_store_n(q->khwords + 2 * second + (ep & 1u), w2, __ATOMIC_RELEASE);
     __atomic_store_n(q->khwords + 2 * (size_t)key + (ep & 1u), w, __ATOMIC_RELEASE);
   }
   __atomic_store_n(&q->rel_epoch[(size_t)key], ep, __ATOMIC_RELEASE);

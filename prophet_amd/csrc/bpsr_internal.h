@@ -120,6 +120,8 @@ struct BlockqLaunch {
   // block per key, a tile waits for its OWN block only, and the block's word
   // (arrival order << 32 | epoch) says in which order its sources fold.
   uint32_t keyed;
+  uint32_t wide;             // 9..16 sources: a second word per block, kwords[nblocks + b]
+                             // (order positions 8..15), khwords likewise after the first words
   uint64_t* kwords;          // device words, one per block (helper / stream releases write them)
   const uint64_t* khwords;   // host words (device view), two per block by epoch parity
   uint32_t* herr;            // host word (device view): the helper mirrors ctl->err there
@@ -131,10 +133,12 @@ struct BlockqLaunch {
   uint32_t* khdone;          // host words (device view), one per block
 };
 // Arrival order of a keyed block: position m's source is worker
-// (perm >> 4m) & 7 (at most 8 sources); kKeySkip: the round is folded
+// (perm >> 4m) & 15 — positions 0..7 in the block's word, 8..15 in its second
+// word (wide queues, 9..16 sources); kKeySkip: the round is folded
 // elsewhere, the tiles only pass.
 constexpr uint32_t kKeySkip = 0xffffffffu;
-constexpr int kKeyedMaxSrcs = 8;
+constexpr int kKeyedMaxSrcs = 16;
+constexpr int kKeyedNarrowSrcs = 8;   // one word per block
 inline uint64_t key_word(uint32_t perm, uint32_t epoch) {
   return ((uint64_t)perm << 32) | epoch;
 }
@@ -270,8 +274,11 @@ hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bo
                          int dtype, int mode, hipStream_t s);
 hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s);
-// Stream-ordered keyed release: kwords[block] = word (system scope, release).
-hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word, hipStream_t s);
+// Stream-ordered keyed release: kwords[block] = word (system scope, release);
+// a wide queue's second word first (word2_at = &kwords[nblocks + block], else
+// null).
+hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,
+                              uint64_t* word2_at, uint64_t word2, hipStream_t s);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.
@@ -385,7 +392,7 @@ uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
 uint32_t keyq_launched(struct byteps_reduce_blockq* q);
 // Both of the above under one lock.
 void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched);
-int keyq_release(struct byteps_reduce_blockq* q, int key, uint32_t perm, hipStream_t s);
+int keyq_release(struct byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s);
 bool keyq_failed(struct byteps_reduce_blockq* q);
 // The key's fold for `epoch` is complete and visible device-wide (its block's
 // last tile stored the completion word): a lock-free host read.

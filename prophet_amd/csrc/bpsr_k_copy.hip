@@ -124,13 +124,18 @@ hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count
 
 // Keyed release behind the stream's earlier work (a round whose pushes were
 // copied into their slots on that stream): one lane stores the block's word.
-__global__ void key_release_kernel(uint64_t* kwords, uint32_t block, uint64_t word) {
-  if (threadIdx.x == 0)
+__global__ void key_release_kernel(uint64_t* kwords, uint32_t block, uint64_t word,
+                                   uint64_t* word2_at, uint64_t word2) {
+  if (threadIdx.x == 0) {
+    if (word2_at) __hip_atomic_store(word2_at, word2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(kwords + block, word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word, hipStream_t s) {
-  hipLaunchKernelGGL(key_release_kernel, dim3(1), dim3(64), 0, s, kwords, block, word);
+hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,
+                              uint64_t* word2_at, uint64_t word2, hipStream_t s) {
+  hipLaunchKernelGGL(key_release_kernel, dim3(1), dim3(64), 0, s, kwords, block, word, word2_at,
+                     word2);
   return hipGetLastError();
 }
 

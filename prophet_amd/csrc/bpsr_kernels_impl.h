@@ -106,9 +106,9 @@ __device__ __forceinline__ vec16 fold_vector_exact(const XS& srcs, int n, uint64
 // NS > 0: exactly NS sources; NS < 0: at most -NS (<= 8) sources, n at run
 // time, one load group with compile-time indices (so `srcs` may be a register
 // array); NS == 0: any n.  `xsrcs` (memory) serves the exact NaN replay.
-template <class Op, int VPT, int NT, int NS, bool GUARD, class XS = SrcPtrs>
-__device__ __forceinline__ void fold_tile_body(const unsigned char* const* srcs,
-                                               const XS& xsrcs, int n,
+template <class Op, int VPT, int NT, int NS, bool GUARD, class XS = SrcPtrs,
+          class SP = const unsigned char* const*>
+__device__ __forceinline__ void fold_tile_body(const SP& srcs, const XS& xsrcs, int n,
                                                unsigned char* dst, uint64_t vec_off,
                                                uint64_t v0, uint64_t nvec, int lane) {
   constexpr int NSA = NS < 0 ? -NS : NS;
@@ -174,9 +174,9 @@ struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
 
-template <class Op, int VPT, int NT, int NS, class Mid = NoMid, class XS = SrcPtrs>
-__device__ __forceinline__ void fold_tile_full_buf(const unsigned char* const* srcs,
-                                                   const XS& xsrcs, int n,
+template <class Op, int VPT, int NT, int NS, class Mid = NoMid, class XS = SrcPtrs,
+          class SP = const unsigned char* const*>
+__device__ __forceinline__ void fold_tile_full_buf(const SP& srcs, const XS& xsrcs, int n,
                                                    unsigned char* dst, uint64_t byte0, int lane,
                                                    const Mid& mid = Mid()) {
   constexpr int kAux = NT ? 2 : 0;               // loads: 2 = nt
@@ -677,15 +677,23 @@ __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
       const uint32_t b = base + lane;
       if (b < Q.nblocks && (uint32_t)ld_agent64(Q.kwords + b) != Q.epoch) {
         const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);
+        // a wide queue's second words follow the first ones (the host stores
+        // the second before the first; a tile checks the second's epoch too)
+        const uint64_t h2 =
+            Q.wide ? ld_sys64(Q.khwords + 2 * (uint64_t)(Q.nblocks + b) + par) : 0;
         // relaxed: the word publishes no data of this workgroup (the round's
         // data landed before the host's store), and a release at system
         // scope would write back the XCD's whole L2 — once per key, while the
         // consumer's own stores fill it (measured: the epoch's consumer took
         // 0.49 ms instead of ~0.1 for config 3's 165 keys)
-        if ((uint32_t)h == Q.epoch)
+        if ((uint32_t)h == Q.epoch && (!Q.wide || (uint32_t)h2 == Q.epoch)) {
+          if (Q.wide)
+            __hip_atomic_store(Q.kwords + Q.nblocks + b, h2, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(Q.kwords + b, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
+        } else {
           pending = true;
+        }
       }
     }
     if (__ballot(pending) == 0) return;
@@ -708,6 +716,16 @@ struct PermSrcs {
   uint32_t perm;
   __device__ __forceinline__ const unsigned char* operator[](int k) const {
     return m[(perm >> (4 * k)) & 7u];
+  }
+};
+
+// The same for up to 16 sources (a wide keyed queue): position k is worker
+// (perm >> 4k) & 15, perm from the block's two release words.
+struct PermSrcs16 {
+  const unsigned char* const* m;
+  uint64_t perm;
+  __device__ __forceinline__ const unsigned char* operator[](int k) const {
+    return m[(perm >> (4 * k)) & 15u];
   }
 };
 
@@ -768,6 +786,39 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
   if (perm == kKeySkip) {
     keep_prefetch(pf);
     key_tile_done<NT>(Q, blk, true);  // nothing stored: the count stays per epoch
+    return;
+  }
+  if (Q.wide) {
+    // 9..16 workers: the order's positions 8..15 are in the block's second
+    // word, released before the first (it may still be on its way here)
+    uint64_t hi = ld_agent64(Q.kwords + Q.nblocks + blk);
+    const uint64_t t0 = wall_clock64();
+    while ((uint32_t)hi != Q.epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      hi = ld_agent64(Q.kwords + Q.nblocks + blk);
+      if (wall_clock64() - t0 > Q.timeout_ticks) {
+        __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+    const uint64_t perm64 = ((hi >> 32) << 32) | perm;
+    const unsigned char* const* m =
+        reinterpret_cast<const unsigned char* const*>(rec + kTileHeadBytes);
+    const PermSrcs16 ps{m, perm64};
+    if (r.kind == kTileElem) {
+      const BatchEntry& e = Q.L.entries[r.b];
+      fold_elements<Op, PermSrcs16>(PermSrcs16{e.srcs, perm64}, e.n, e.dst, e.g,
+                                    e.aligned != 0, (uint64_t)r.a * kBlock + threadIdx.x,
+                                    (uint64_t)r.c * kBlock);
+    } else if (r.kind == kTileFull) {
+      fold_tile_full_buf<Op, VPT, NT, 0, NoMid, PermSrcs16>(ps, ps, (int)r.n, r.dst, 0,
+                                                            threadIdx.x);
+    } else {
+      fold_tile_body<Op, VPT, NT, 0, true, PermSrcs16>(ps, ps, (int)r.n, r.dst, 0, 0, r.a,
+                                                        threadIdx.x);
+    }
+    keep_prefetch(pf);
+    key_tile_done<NT>(Q, blk, r.kind == kTileFull && NT == kPolWt);
     return;
   }
   // fast path: the 8 pointers permuted in registers (selects); element work

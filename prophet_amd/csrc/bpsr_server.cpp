@@ -946,9 +946,9 @@ bool keyed_member(byteps_server* s, KeyState* ks) {
 // device releases were turned off meanwhile (the caller folds with a launch).
 int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
                 bool skip = false) {
-  uint32_t perm = 0;
-  for (size_t m = 0; m < order.size(); ++m) perm |= (uint32_t)order[m] << (4 * m);
-  if (skip) perm = kKeySkip;
+  uint64_t perm = 0;  // position m's worker in bits 4m..4m+3 (16 positions)
+  for (size_t m = 0; m < order.size(); ++m) perm |= (uint64_t)order[m] << (4 * m);
+  if (skip) perm = ((uint64_t)kKeySkip << 32) | kKeySkip;
   hipEvent_t ev = nullptr;
   uint64_t seq = 0;
   const int kk = ks->kq_key.load();

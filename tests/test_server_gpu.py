@@ -1701,8 +1701,10 @@ def _ptr_copy(ptr, src):
     GpuReducer().copy(ptr, src, src.numel() * src.element_size())
 
 
-@pytest.mark.parametrize("dt", [DType.FLOAT32, DType.FLOAT16], ids=lambda d: DType(d).name)
-def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
+@pytest.mark.parametrize("N,dt", [(8, DType.FLOAT32), (8, DType.FLOAT16), (16, DType.FLOAT32),
+                                  (16, DType.BFLOAT16)],
+                         ids=["8-FLOAT32", "8-FLOAT16", "16-FLOAT32", "16-BFLOAT16"])
+def test_device_release_rounds_bit_exact(port, N, dt, monkeypatch):
     """BPSR_SERVER_RELEASE=device: after the init round one keyed block queue
     folds every key, a round's last push_ready stores the release word (no
     launch); blocking device pushes land through the copy service and are
@@ -1713,10 +1715,12 @@ def test_device_release_rounds_bit_exact(port, dt, monkeypatch):
     blocking device pushes and 1 of non-blocking ones; pulls as device views,
     blocking device copies and host copies.  Every pull equals the oracle's
     left fold in the recorded arrival order; one consumer launch per round;
-    lane folds only in the non-blocking round."""
+    lane folds only in the non-blocking round.  16 workers: the wide keyed
+    queue (the order's positions 8..15 in each block's second release word)
+    keeps device releases — the same counts, bit-exact (bf16 included)."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
-    N, R = 8, 5
+    R = 5
     sizes = [1, 7, 1000, 4096 + 5, 65_536 + 3, 300_001]        # elements per key
     keys = list(range(40, 40 + len(sizes)))
     es = elem_size(dt)
