@@ -54,8 +54,9 @@ extern "C" {
  * (byteps.lds:1-8, global: *byteps*; local: *). */
 #pragma GCC visibility push(default)
 
-/* 3: byteps_server_config.engine_blocking; bpsr/shard.h */
-#define BYTEPS_REDUCE_ABI_VERSION 3
+/* 3: byteps_server_config.engine_blocking; bpsr/shard.h
+ * 4: byteps_server_config.release; byteps_shard_rccl_version */
+#define BYTEPS_REDUCE_ABI_VERSION 4
 
 /* Data type ids: byteps/common/common.h:52-65 (mshadow order), plus bf16 as a
  * build extension (the reference has none). */

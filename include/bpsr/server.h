@@ -46,6 +46,7 @@ extern "C" {
 #pragma GCC visibility push(default)
 
 enum byteps_server_policy { BYTEPS_SERVER_FUSED = 0, BYTEPS_SERVER_INCREMENTAL = 1 };
+enum byteps_server_release { BYTEPS_SERVER_RELEASE_LAUNCH = 0, BYTEPS_SERVER_RELEASE_DEVICE = 1 };
 enum byteps_server_location { BYTEPS_SERVER_HOST = 0, BYTEPS_SERVER_DEVICE = 1 };
 
 typedef struct byteps_server_config {
@@ -66,6 +67,13 @@ typedef struct byteps_server_config {
                           no pull counting (server.cc:284-285); a pull issued
                           before the round's last push sees the previous
                           round, as in the reference.  0 = the default engine */
+  int release;         /* byteps_server_release: how a finished round is folded
+                          — LAUNCH (0): the lane issuers' batched fold
+                          launches; DEVICE (1): device releases (below).
+                          byteps_server_config_from_env picks DEVICE, the
+                          dedicated server process of server.cc:339-400 where
+                          nothing else runs on the GPU (BPSR_SERVER_RELEASE=
+                          launch|device overrides either way)               */
 } byteps_server_config;
 
 typedef struct byteps_server byteps_server;
@@ -74,11 +82,18 @@ typedef struct byteps_server byteps_server;
  * them: DMLC_NUM_WORKER, BYTEPS_SERVER_ENGINE_THREAD, BYTEPS_ENABLE_ASYNC
  * (here "1" means asynchronous; the reference reads the flag inverted,
  * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
- * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0. */
+ * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0, and
+ * release = DEVICE: the server process that byteps_server() (server.cc:
+ * 339-400) starts does nothing else on its GPU, so device releases' one rule
+ * for other GPU users of the process — no device-wide wait while an epoch is
+ * open — holds; config 3's keys from one receive thread then fold at 0.50 of
+ * the HBM roofline instead of 0.25-0.35 (the bench line's server_cfg3).  The
+ * rounds that cannot be device-released fall back by themselves (see below). */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
-/* Device releases (BPSR_SERVER_RELEASE=device; sync mode, fused policy, the
- * default engine, num_workers <= 8): at the first round completion after the
+/* Device releases (release = DEVICE or BPSR_SERVER_RELEASE=device; sync mode,
+ * fused policy, the default engine, num_workers <= 16 — otherwise the server
+ * folds with launches): at the first round completion after the
  * init round the server builds ONE keyed block queue over every declared key
  * of that key's dtype (each key's receive slots in worker order and its
  * store).  From then on a round's last arrival issues no launch: it stores

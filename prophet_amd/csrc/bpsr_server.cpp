@@ -1775,6 +1775,8 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   cfg->enable_schedule = (sc && atoi(sc) != 0) ? 1 : 0;
   const char* eb = getenv("BYTEPS_SERVER_ENGINE_BLOCKING");  // server.cc:324
   cfg->engine_blocking = (eb && atoi(eb) != 0) ? 1 : 0;
+  // the dedicated server process: nothing else waits on its GPU (server.h)
+  cfg->release = BYTEPS_SERVER_RELEASE_DEVICE;
   return BYTEPS_REDUCE_OK;
 }
 
@@ -1794,7 +1796,13 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
   if (s->schedule || s->blocking) s->combine = false;
   if (const char* fl = getenv("BPSR_SERVER_INFLIGHT")) s->inflight = std::max(1L, atol(fl));
-  if (const char* r = getenv("BPSR_SERVER_RELEASE")) s->dev_release = std::string(r) == "device";
+  if (cfg->release != BYTEPS_SERVER_RELEASE_LAUNCH && cfg->release != BYTEPS_SERVER_RELEASE_DEVICE)
+    return fail(BYTEPS_REDUCE_EARGS, "unknown release %d", cfg->release);
+  s->dev_release = cfg->release == BYTEPS_SERVER_RELEASE_DEVICE;
+  if (const char* r = getenv("BPSR_SERVER_RELEASE")) {  // overrides the config either way
+    if (std::string(r) == "device") s->dev_release = true;
+    else if (std::string(r) == "launch") s->dev_release = false;
+  }
   if (const char* ps = getenv("BPSR_SERVER_PULL_SERVICE")) s->pull_service = atoi(ps) != 0;
   if (const char* t = getenv("BPSR_SERVER_RELEASE_TIMEOUT_S"))
     if (atof(t) > 0) s->kq_timeout_s = atof(t);

@@ -46,7 +46,10 @@ PUSH_CB = ctypes.CFUNCTYPE(None, _vp, _u64, _int, _int)
 class ServerConfig(ctypes.Structure):
     _fields_ = [("num_workers", _int), ("engine_lanes", _int), ("policy", _int),
                 ("async_mode", _int), ("device", _int), ("enable_schedule", _int),
-                ("engine_blocking", _int)]
+                ("engine_blocking", _int), ("release", _int)]
+
+
+RELEASE_LAUNCH, RELEASE_DEVICE = 0, 1
 
 
 class GroupConfig(ctypes.Structure):
@@ -205,13 +208,22 @@ def config_from_env() -> ServerConfig:
 class PSServer:
     def __init__(self, num_workers: int, engine_lanes: int = 4, policy: int = FUSED,
                  async_mode: bool = False, device: int = 0, enable_schedule: bool = False,
-                 engine_blocking: bool = False):
+                 engine_blocking: bool = False, release: int = RELEASE_LAUNCH):
         self.lib = _lib()
         self.cfg = ServerConfig(num_workers, engine_lanes, policy, int(async_mode), device,
-                                int(enable_schedule), int(engine_blocking))
+                                int(enable_schedule), int(engine_blocking), int(release))
         self.handle = _vp()
         self._pending = {}
         _check(self.lib.byteps_server_create(ctypes.byref(self.cfg), ctypes.byref(self.handle)))
+
+    @classmethod
+    def from_env(cls) -> "PSServer":
+        """The dedicated server process's server (byteps_server(),
+        server.cc:339-400): byteps_server_config_from_env — device releases
+        by default."""
+        c = config_from_env()
+        return cls(c.num_workers, c.engine_lanes, c.policy, bool(c.async_mode), c.device,
+                   bool(c.enable_schedule), bool(c.engine_blocking), c.release)
 
     def init_key(self, key: int, nbytes: int, dtype: int) -> None:
         _check(self.lib.byteps_server_init_key(self.handle, key, nbytes, int(dtype)))

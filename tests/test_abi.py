@@ -38,6 +38,7 @@ def test_library_exports_every_header_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
 
+
 def test_library_exports_nothing_but_the_header_api():
     """The reference's export policy (byteps.lds:1-8, global: *byteps*;
     local: *, passed by setup.py:207): EVERY defined dynamic symbol of
@@ -75,7 +76,7 @@ def test_library_build_applies_the_export_policy():
 
 def test_version_and_dtype_sizes():
     lib = reducer.load_library()
-    assert lib.byteps_reduce_version() == 3
+    assert lib.byteps_reduce_version() == 4
     for dt in ALL_DTYPES:
         assert lib.byteps_reduce_dtype_size(int(dt)) == elem_size(dt)
     assert lib.byteps_reduce_dtype_size(7) == reducer.EDTYPE
@@ -150,11 +151,15 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     assert c.engine_blocking == 1
     monkeypatch.setenv("BYTEPS_SERVER_ENGINE_BLOCKING", "0")
     assert server.config_from_env().engine_blocking == 0
+    # the dedicated server process folds through device releases (server.h)
+    assert c.release == server.RELEASE_DEVICE
     lib = server._lib()
     bad = server.ServerConfig(0, 4, 0, 0, 0)
     h = ctypes.c_void_p()
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
     bad = server.ServerConfig(2, 0, 0, 0, 0)      # server.cc:332 CHECK_GE(threads, 1)
+    assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
+    bad = server.ServerConfig(2, 4, 0, 0, 0, 0, 0, 7)  # no such release
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
     assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS
     assert lib.byteps_server_pull_host_view(None, 1, None, None) == reducer.EARGS

@@ -1823,6 +1823,64 @@ def test_device_release_rounds_bit_exact(port, N, dt, monkeypatch):
     assert 1 <= st["fold_launches"] - st0["fold_launches"] <= copied * len(keys)
 
 
+@pytest.mark.parametrize("release", [None, "launch"], ids=["env-default", "launch"])
+def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
+    """The dedicated server process (server.cc:339-400) builds its server from
+    the environment (byteps_server_config_from_env): device releases by
+    default — one consumer launch per round, no fold launches — and
+    BPSR_SERVER_RELEASE=launch turns them off.  4 workers, push_ready rounds
+    from the slots, pulls into device memory: bit-exact with the oracle's left
+    fold in the recorded order either way."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import RELEASE_DEVICE, PSServer
+    monkeypatch.delenv("BPSR_SERVER_RELEASE", raising=False)
+    if release:
+        monkeypatch.setenv("BPSR_SERVER_RELEASE", release)
+    monkeypatch.setenv("DMLC_NUM_WORKER", "4")
+    dt, N, R = DType.FLOAT32, 4, 3
+    sizes = [3, 4096 + 1, 200_003]
+    keys = [11, 12, 13]
+    es = elem_size(dt)
+    srv = PSServer.from_env()
+    assert srv.cfg.release == RELEASE_DEVICE and srv.cfg.num_workers == N
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)      # never the legacy NULL stream (server.h)
+    with torch.cuda.stream(st):
+        for j, k in enumerate(keys):                     # init round: blocking pushes
+            ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, sizes[j], w, 0, j), dt))
+                  for w in range(N)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(timeout=60)
+        st0 = None
+        for r in range(1, R + 1):
+            for j, k in enumerate(keys):
+                for w in range(N):
+                    x = torch.from_numpy(data(dt, sizes[j], w, r, j)).to(dev)
+                    GpuReducer().copy(srv.recv_slot(k, w), x, x.numel(), stream=st)  # bytes (uint8)
+                    st.synchronize()
+                    srv.push_ready(k, w)
+            for j, k in enumerate(keys):
+                _, _, order = srv.key_info(k)
+                want = np.zeros(sizes[j] * es, np.uint8)
+                port.sum_n(want, [data(dt, sizes[j], w, r, j) for w in order], sizes[j] * es, dt)
+                for w in range(N):
+                    o = torch.empty(sizes[j] * es, dtype=torch.uint8, device=dev)
+                    srv.pull(k, o)
+                    st.synchronize()
+                    assert np.array_equal(o.cpu().numpy(), want), (r, k, w)
+            if r == 1:
+                st0 = srv.stats()
+    s1 = srv.stats()
+    srv.close()
+    if release is None:
+        assert s1["consumer_launches"] == R and s1["key_releases"] == R * len(keys)
+        assert s1["fold_launches"] == st0["fold_launches"]
+    else:
+        assert s1["consumer_launches"] == 0 and s1["key_releases"] == 0
+
+
 def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     """The keyed queue's contract: every key completes one round per epoch.  A
     round in which one key is never pushed makes that epoch's consumer give up
