@@ -2,408 +2,13 @@
 // per-key state machine of byteps/server/server.cc:147-308 with the engine
 // threads (server.cc:70-145) replaced by HIP stream lanes and the CpuReducer
 // calls replaced by the gfx950 fold kernels.
-#include "bpsr/server.h"
-
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <deque>
-#include <limits>
-#include <memory>
-#include <mutex>
-#include <shared_mutex>
-#include <string>
-#include <thread>
-#include <unordered_map>
-#include <vector>
-
-#include "bpsr_engine_queue.h"
-#include "bpsr_internal.h"
+//
+// Split over bpsr_server*.cpp (see bpsr_server_state.h); this file: lanes and
+// their threads, the state machine, create / destroy and the single-key calls.
+#include "bpsr_server_state.h"
 
 namespace bpsr {
-namespace {
-
-constexpr size_t kSlotAlign = 64 * 1024;  // bucket rounding before the skew (prophet_amd/arena.py)
-constexpr size_t kSlotSkew = 16 * 1024;  // prophet_amd/arena.py: skewed slots
-constexpr int kMaxDebugLog = 4096;
-// pull_many issues the copies of the rounds found finished once this many
-// bytes are ready and it must wait for another round (else at the end)
-constexpr size_t kPullFlushBytes = 8u << 20;
-
-struct KeyState;
-
-// One engine message (server.h:65-75 BytePSEngineMessage): the fold work of
-// one arrival (SUM_RECV), of a finished round (COPY_MERGED, or the fused
-// left fold) or of an async push.
-enum JobKind { kSumRecv = 0, kAsyncSum = 1, kFinishIncremental = 2, kFinishFused = 3,
-               kKeyRelease = 4 };  // a device-released round whose pushes were copied
-struct FoldJob {
-  KeyState* ks = nullptr;
-  int kind = kSumRecv;
-  int w = -1;              // the arriving worker's slot
-  int acc = -1;            // the accumulator slot (first arrival), incremental policy
-  std::vector<int> order;  // arrival order of the finished round
-};
-
-struct Lane;
-// A pull ready to be answered, or a push to acknowledge, by the responder.
-struct Response {
-  uint64_t key = 0;
-  KeyState* ks = nullptr;
-  byteps_server_pull_cb cb = nullptr;
-  void* ctx = nullptr;
-  const char* view = nullptr;  // mirror holding the answered round
-  int status = 0;
-  byteps_server_push_cb push_cb = nullptr;  // set: a push acknowledgement
-  int worker = -1;
-  // a push whose copy the lane's issuer batched: acknowledge once the lane's
-  // completer has seen launch wait_seq complete (else sync `copied`); the
-  // same for a pull copied into the caller's buffer (len: its length)
-  Lane* wait_lane = nullptr;
-  uint64_t wait_seq = 0;
-  size_t len = 0;
-  uint64_t kseq = 0;  // a view of a keyed round: answered once its epoch is published
-};
-
-// A blocking call served by the non-blocking machinery: the lane issuer
-// batches the copy with whatever else piled up, the completer and responder
-// finish it, and the caller waits here without making a HIP call.  (HIP
-// calls serialise across threads: eight workers each making 4-5 calls per
-// key paid ~8 us per call)
-struct Lane;
-// BPSR_SERVER_SPIN_US: how long a blocking call's waiter polls before it
-// sleeps on a condition variable (0: sleep at once).  A sleeping waiter's
-// wake-up is a futex round trip per hand-off.
-int64_t spin_ns() {
-  static const int64_t ns = [] {
-    const char* v = getenv("BPSR_SERVER_SPIN_US");
-    return v ? std::max(0L, atol(v)) * 1000L : 0L;
-  }();
-  return ns;
-}
-// Poll `ready` for up to spin_ns(); true once it holds.
-template <class F>
-bool spin_until(F ready) {
-  const int64_t budget = spin_ns();
-  if (budget == 0) return false;
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    for (int i = 0; i < 64; ++i) {
-      if (ready()) return true;
-      __builtin_ia32_pause();
-    }
-    if (std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
-            .count() > budget)
-      return ready();
-  }
-}
-struct SyncWait {
-  std::mutex mu;
-  std::condition_variable cv;
-  bool done = false;
-  std::atomic<bool> flag{false};  // `done`, set under mu, for a spinning waiter
-  int status = 0;
-  Lane* lane = nullptr;  // a direct pull or push: the launch its copy rides in
-  uint64_t seq = 0;
-  int wait() {
-    // a waiter that saw the flag still takes mu, so it returns (and the
-    // caller's frame goes) only after finish() has let go of it
-    (void)spin_until([&] { return flag.load(std::memory_order_acquire); });
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done; });
-    return status;
-  }
-  void finish(int st) {
-    std::lock_guard<std::mutex> g(mu);
-    status = st;
-    done = true;
-    flag.store(true, std::memory_order_release);
-    cv.notify_all();
-  }
-};
-// A non-blocking pull into a caller's device buffer (byteps_server_pull_into_async)
-// whose copy waits for the lane's issuer.  `direct`: a blocking pull's waiter,
-// told the launch's seq by the issuer and then waiting on the lane's
-// completion itself (no responder hop).
-struct PullJob {
-  KeyState* ks = nullptr;
-  void* dst = nullptr;
-  size_t len = 0;
-  Response resp;
-  SyncWait* direct = nullptr;
-  uint64_t kseq = 0;  // parked on a keyed epoch: the keyed completer's seq it waits for
-};
-
-// A non-blocking push of device data whose copy into its slot waits for the
-// lane's issuer (batched with the other copies that piled up).
-struct CopyJob {
-  KeyState* ks = nullptr;
-  int w = -1;
-  const void* src = nullptr;
-  size_t len = 0;
-  Response ack;
-  SyncWait* direct = nullptr;  // a blocking push's waiter (no responder hop)
-};
-
-struct Lane {
-  hipStream_t fold = nullptr;  // folds, in round order per key
-  hipStream_t copy = nullptr;  // push copies
-  hipStream_t d2h = nullptr;   // store -> host mirror copies
-  // BYTEPS_SERVER_ENABLE_SCHEDULE: pending jobs and the thread that issues them
-  std::unique_ptr<EngineQueue<FoldJob>> q;
-  std::thread dispatcher;
-  hipEvent_t job_done = nullptr;
-  std::mutex dbg_mu;
-  std::vector<uint64_t> log;  // keys of dispatched jobs, in dispatch order
-  // batched calls (push_many / push_ready_many / pull_many): one batched
-  // launch per lane for many keys, staged through the lane's own ring
-  std::mutex batch_mu;
-  StageRing* ring = nullptr;
-  // Lane-wide marks: the latest work issued on each stream (a later record on
-  // an in-order stream covers every earlier one).  Folds wait for copy_mark
-  // (every push copy of the lane so far); batched calls wait for fold_mark /
-  // d2h_mark once per lane instead of one event per key.
-  hipEvent_t copy_mark = nullptr, fold_mark = nullptr, d2h_mark = nullptr;
-  // Combining (no scheduling, no engine blocking): the rounds single-key
-  // calls complete go to the lane's issuer thread, which issues what piled up
-  // as ONE batched fold launch while the callers go on (issuer_main).
-  std::mutex comb_mu;
-  std::condition_variable comb_cv;   // work for the issuer
-  std::vector<FoldJob> comb;
-  std::vector<CopyJob> copies;       // non-blocking device pushes, before the folds
-  std::vector<PullJob> pulls;        // non-blocking pulls into device buffers
-  bool comb_stop = false;
-  std::thread issuer;
-  // Completion of what the issuer issued, tracked on the host so waiters make
-  // no HIP call (HIP calls serialise across threads: 8 threads syncing events
-  // per key cost 3.5 us each, tools/launch_cost.cpp): the issuer appends
-  // (seq, event) per launch, the lane's completer thread waits for them in
-  // order and publishes done_seq; a key remembers the seq of its last round.
-  std::mutex done_mu;
-  std::condition_variable cq_cv;    // issuer -> completer
-  std::condition_variable done_cv;  // completer -> waiters (and the issuer)
-  struct Tracked {
-    uint64_t seq;
-    hipEvent_t ev;
-    uint32_t kq_epoch;  // != 0: the keyed consumer launch of that epoch (lane 0 only)
-  };
-  std::deque<Tracked> cq;
-  uint64_t issued_seq = 0, done_seq = 0;
-  std::atomic<uint64_t> done_pub{0};  // done_seq, readable without done_mu (spinning waiters)
-  std::atomic<const char*> where{"idle"};  // the issuer's step (BPSR_SERVER_RELEASE_DEBUG dumps)
-  bool cq_stop = false;
-  std::thread completer;
-  // copies recorded into copy_mark so far / seen by a fold's wait on it (a
-  // fold stream already waiting on the latest copy mark need not wait again)
-  std::atomic<uint64_t> copy_seq{0}, fold_copy_seen{0};
-  // pull copies recorded into d2h_mark / seen by a fold's wait on it (a
-  // fold rewrites the store those copies read)
-  std::atomic<uint64_t> pull_seq{0}, fold_pull_seen{0};
-};
-
-struct KeyState {
-  uint64_t key = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  // Set once, last, by allocate() (under mu) after the slots, store, events
-  // and lane exist; those never change afterwards, so the pull and
-  // receive-slot paths may test it and read them before taking mu.
-  std::atomic<bool> allocated{false};
-  bool inited = false;        // store initialised (round 0 done)
-  size_t len = 0;
-  int dtype = 0;
-  int lane = 0;
-  char* arena = nullptr;      // N receive slots + store
-  size_t stride = 0;
-  std::vector<char*> slot;
-  char* store = nullptr;
-  // current round
-  std::vector<char> got;      // worker pushed this round (cleared when the round's fold is issued)
-  std::vector<int> order;     // arrival order this round
-  int arrived = 0;
-  int init_count = 0;
-  int init_last = -1;         // the init round's last arrival (its push initialises the store)
-  bool stamped = false;       // this round's arrivals carry positions (a group's range split)
-  std::vector<Response> init_acks;  // non-blocking init pushes, answered together (server.cc:184-198)
-  int pending = 0;            // jobs queued on the lane, not yet issued (scheduling only)
-  int error = 0;              // sticky failure of an issued fold: every later call returns it
-  std::string error_msg;
-  // completion / pull gating (server.cc:100-114, 280-306)
-  uint64_t rounds = 0;
-  bool push_finished = false;
-  int pull_cnt = 0;
-  std::vector<int> last_order;
-  hipEvent_t done = nullptr;  // recorded on the lane's fold stream after a single fold
-  // What to wait for to see the key's last issued fold complete: `done`, or —
-  // after a batched issue (flush_folds), which records no per-key event — the
-  // lane's fold mark (a later record of it covers this fold too).
-  hipEvent_t fold_ev = nullptr;
-  uint64_t fold_seq = 0;      // lane completion seq of the last issued round (0: untracked)
-  int fold_lane = 0;          // the lane whose completer tracks fold_seq
-  std::vector<int> order_tmp; // a keyed round's order on its way out (arrive)
-  uint32_t kq_round_epoch = 0; // a keyed round: the consumer epoch that folds it
-  // device releases: the key's block in the server's keyed queue (-1: none),
-  // whether this round's last fold is a keyed consumer's, and whether a push
-  // of the current round was copied into its slot (released behind the copy)
-  std::atomic<int> kq_key{-1};
-  bool keyed = false;
-  bool round_copied = false;
-  // a copy of this round is covered only by the lane's copy mark (a batched
-  // device copy); otherwise every copy of the round recorded `copied` after
-  // itself on the lane's (in-order) copy stream, so the round's fold can wait
-  // for its own copies instead of every copy the lane has queued (a worker's
-  // push_many of host data queues all its partitions' H2D at once)
-  bool round_mark_copy = false;
-  hipEvent_t copied = nullptr;
-  hipEvent_t pulled = nullptr;  // recorded on the lane's d2h stream after a copying pull
-  bool has_done = false;
-  // pinned host mirrors of the store for zero-copy pull responses
-  // (server.cc:42-70 responds from the store itself).  Sync mode: two, by
-  // round parity, filled by ONE D2H per round.  Async mode: a ring of
-  // num_workers + 1, one D2H per pull.
-  std::vector<char*> mirror;
-  std::vector<void*> mirror_dev;  // the same pages as the device sees them
-  uint64_t mirror_next = 0;       // async ring position
-  hipEvent_t mirrored = nullptr;  // recorded on the lane's d2h stream
-  // byteps_server_pull_async requests waiting for this round to finish
-  // (the reference's q_pull_reqmeta_, server.cc:304)
-  struct Waiting {
-    byteps_server_pull_cb cb;
-    void* ctx;
-  };
-  std::vector<Waiting> waiting;
-  // byteps_server_pull_into_async requests waiting for this round
-  struct WaitingCopy {
-    void* dst;           // as the device addresses it
-    size_t len;
-    byteps_server_pull_cb cb;
-    void* ctx;
-    const void* view;    // what the callback reports (the caller's pointer)
-    SyncWait* direct;    // a blocking pull parked until the round finishes
-  };
-  std::vector<WaitingCopy> waiting_copies;
-};
-
-}  // namespace
-}  // namespace bpsr
-
-// A counter bumped by every per-key call: sharded over cache lines by
-// calling thread, so receive threads do not bounce one line per call.
-struct ShardedCount {
-  static constexpr int kShards = 16;
-  struct alignas(64) Slot {
-    std::atomic<uint64_t> v{0};
-  };
-  Slot slot[kShards];
-  static int shard() {
-    static std::atomic<int> next{0};
-    thread_local const int mine = next.fetch_add(1, std::memory_order_relaxed) % kShards;
-    return mine;
-  }
-  void add(uint64_t n = 1) { slot[shard()].v.fetch_add(n, std::memory_order_relaxed); }
-  uint64_t load() const {
-    uint64_t t = 0;
-    for (const Slot& x : slot) t += x.v.load(std::memory_order_relaxed);
-    return t;
-  }
-};
-
-struct byteps_server {
-  byteps_server_config cfg;
-  bool schedule = false;
-  bool blocking = false;  // BYTEPS_SERVER_ENGINE_BLOCKING (server.cc:324)
-  // lane issuer threads batch single-key calls' folds and device pulls
-  // (BPSR_SERVER_COMBINE=0: each call issues its own; off with scheduling or
-  // engine blocking, whose orders and completion rules are per call)
-  bool combine = true;
-  uint64_t inflight = 2;  // issuer: launches queued or running per lane (BPSR_SERVER_INFLIGHT)
-  // telemetry (byteps_server_stats)
-  std::atomic<uint64_t> n_fold_launches{0}, n_pull_launches{0}, issuer_ns{0},
-      n_copy_launches{0};
-  ShardedCount n_rounds_folded, n_pulls;
-  std::vector<std::unique_ptr<bpsr::Lane>> lanes;
-  // every call looks its key up; keys are added once: lookups share the lock
-  std::shared_mutex map_mu;
-  std::unordered_map<uint64_t, std::unique_ptr<bpsr::KeyState>> keys;
-  // ... and first probe a lock-free index of the same keys (open addressing,
-  // entries never removed before destroy; filled to half at most, later keys
-  // only in the map): a shared lock is an atomic add on one line that every
-  // calling thread bounces
-  static constexpr size_t kKeyIndex = 1u << 14;
-  std::unique_ptr<std::atomic<bpsr::KeyState*>[]> key_index{
-      new std::atomic<bpsr::KeyState*>[kKeyIndex]()};
-  size_t key_index_n = 0;  // under map_mu
-  std::vector<uint64_t> acc_load;  // server.h:112 acc_load_
-  // responder thread: SendPullResponse of queued pulls (server.cc:100-114)
-  // and SendPushResponse of non-blocking pushes (server.cc:255)
-  std::mutex rq_mu;
-  std::condition_variable rq_cv;
-  std::deque<bpsr::Response> rq;
-  bool rq_stop = false;
-  std::thread responder;
-  // Fault injection for tests (BPSR_SERVER_FAIL_AFTER=n): the (n+1)-th fold
-  // issue (init copy or engine job) and every later one fail as a failed
-  // kernel launch would.  -1 = off.
-  long fail_after = -1;
-  std::atomic<long> issued{0};
-  // Device releases (BPSR_SERVER_RELEASE=device: sync mode, fused policy, the
-  // default engine, N <= 8).  At the first round completion after the init
-  // round, ONE keyed block queue is built over every allocated key of that
-  // dtype (bpsr::keyq_*: its slots in worker order and its store).  A round's
-  // last arrival then stores the key's arrival order and release word
-  // instead of issuing a launch (behind the round's copies, a one-lane
-  // release kernel on the lane's copy stream), and one consumer launch per
-  // epoch folds every key of the queue, each as soon as it is released.
-  // Nothing reads a keyed store before lane 0's completer has seen its
-  // epoch's consumer complete: pulls parked on it are handed to their lanes
-  // then, views wait for it.  A consumer that times out (a key of the queue
-  // not pushed within BPSR_SERVER_RELEASE_TIMEOUT_S) fails the keys released
-  // in its epoch and turns device releases off for good.
-  bool dev_release = false;
-  double kq_timeout_s = 5.0;
-  std::unique_ptr<bpsr::Lane> klane;  // its completer tracks the consumer launches (no streams)
-  std::mutex kq_mu;  // guards the kq_* state below (taken after a key's mu, never before)
-  byteps_reduce_blockq* kq = nullptr;
-  bool kq_tried = false;
-  std::atomic<bool> kq_off{false};
-  std::vector<bpsr::KeyState*> kq_keys;  // block -> key
-  static constexpr int kKqRing = 64;
-  hipEvent_t kq_ev[kKqRing] = {};       // stop event of epoch e at e % kKqRing
-  uint64_t kq_ev_seq[kKqRing] = {};     // lane-0 seq of that launch
-  uint32_t kq_ev_epoch[kKqRing] = {};
-  uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
-  std::atomic<uint32_t> kq_pub_epoch{0};  // epochs launched with their kq_ev slot written
-  std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
-  std::atomic<uint64_t> n_consumer_launches{0};
-  ShardedCount n_key_releases;
-  // Blocking pulls into this device's memory (combine path): served by the
-  // pull copy service, created on first use (BPSR_SERVER_PULL_SERVICE=0: the
-  // lane issuers' batched copies instead).
-  bool pull_service = true;
-  std::mutex svc_mu;
-  bpsr::CopyService* svc = nullptr;
-  bool svc_tried = false;
-  std::atomic<uint64_t> n_service_pulls{0}, n_service_pushes{0};
-  // order_after's events for those pulls: the service copies on no stream of
-  // ours, so a caller event is also waited for on a gate stream whose event
-  // the next service pull synchronises on (a blocking call: it waits anyway)
-  std::mutex gate_mu;
-  hipStream_t gate_stream = nullptr;
-  hipEvent_t gate_ev = nullptr;
-  std::atomic<uint64_t> gate_seq{0}, gate_done{0};
-  // events that bound a push_many's host copies in flight (push_many_host)
-  std::mutex ev_pool_mu;
-  std::vector<hipEvent_t> ev_pool;
-};
-
-namespace bpsr {
-namespace {
+inline namespace srv {
 
 // The device a server call last bound on this thread.  Every entry point
 // binds the server's device (set_device), except the two per-key calls of a
@@ -626,7 +231,7 @@ bool can_push(const byteps_server* s, const KeyState* ks, int w) {
 // Bring `len` bytes into worker `w`'s slot on the lane's copy stream, after
 // the last issued fold of the key has consumed the slot.
 int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len, int loc,
-            bool wait = true) {
+            bool wait) {
   Lane& L = *s->lanes[ks->lane];
   ks->round_copied = true;
   hipError_t e = hipSuccess;
@@ -850,8 +455,8 @@ void responder_main(byteps_server* s) {
 // A round's fold is issued: publish it (caller holds ks->mu).  `mark`: also
 // raise the lane's fold mark (a batched issue raises it once, before).
 int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
-                 bool mark = true, hipEvent_t batch = nullptr, uint64_t batch_seq = 0,
-                 bool keyed = false) {
+                 bool mark, hipEvent_t batch, uint64_t batch_seq,
+                 bool keyed) {
   Lane& L = *s->lanes[ks->lane];
   s->n_rounds_folded.add();
   ks->keyed = keyed;  // a keyed consumer's fold, tracked by the keyed completer
@@ -891,207 +496,6 @@ int injected_failure(byteps_server* s) {
               s->fail_after);
 }
 
-// ------------------------------------------------------ device releases --
-
-// The keyed queue over every allocated key of `dtype` (block order = key
-// order), built once, at the first round completion after the init round
-// (caller holds s->kq_mu and that key's mu).  Keys declared later, and keys
-// of other dtypes, keep the lane launches.
-void build_kq(byteps_server* s, int dtype) {
-  std::vector<KeyState*> keys;
-  {
-    std::shared_lock<std::shared_mutex> g(s->map_mu);
-    for (auto& kv : s->keys) {
-      KeyState* k = kv.second.get();
-      if (k->allocated && k->dtype == dtype) keys.push_back(k);
-    }
-  }
-  if (keys.empty()) return;
-  std::sort(keys.begin(), keys.end(),
-            [](const KeyState* a, const KeyState* b) { return a->key < b->key; });
-  const int N = s->cfg.num_workers;
-  std::vector<byteps_bucket_desc> d(keys.size());
-  for (size_t i = 0; i < keys.size(); ++i) {
-    std::memset(&d[i], 0, sizeof(d[i]));
-    d[i].dst = keys[i]->store;
-    for (int w = 0; w < N; ++w) d[i].srcs[w] = keys[i]->slot[w];
-    d[i].len = keys[i]->len;
-    d[i].n = N;
-  }
-  if (force_device(s) || keyq_create(d.data(), (int)d.size(), dtype, s->kq_timeout_s, &s->kq)) {
-    s->kq = nullptr;  // no queue: every round keeps the lane launches
-    return;
-  }
-  s->kq_keys = keys;
-  for (size_t i = 0; i < keys.size(); ++i) keys[i]->kq_key.store((int)i);
-}
-
-// Is this finished round of `ks` device-released?  Caller holds ks->mu.
-bool keyed_member(byteps_server* s, KeyState* ks) {
-  if (!s->dev_release || s->kq_off.load()) return false;
-  std::lock_guard<std::mutex> g(s->kq_mu);
-  if (!s->kq_tried) {
-    s->kq_tried = true;
-    build_kq(s, ks->dtype);
-  }
-  return ks->kq_key.load() >= 0;
-}
-
-// Release a finished round of a keyed key (caller holds ks->mu): the arrival
-// order and the release word go to the key's block — stored from the host
-// when the round's data is in its slots already (push_ready), or by a one-lane
-// kernel on `stream` behind the round's copies — after the consumer of the
-// block's epoch has been launched (the first release of an epoch launches
-// it).  Then the round is published like an issued fold.  Returns 1 when
-// device releases were turned off meanwhile (the caller folds with a launch).
-int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
-                bool skip = false) {
-  uint64_t perm = 0;  // position m's worker in bits 4m..4m+3 (16 positions)
-  for (size_t m = 0; m < order.size(); ++m) perm |= (uint64_t)order[m] << (4 * m);
-  if (skip) perm = ((uint64_t)kKeySkip << 32) | kKeySkip;
-  hipEvent_t ev = nullptr;
-  uint64_t seq = 0;
-  const int kk = ks->kq_key.load();
-  uint32_t need = keyq_next_epoch(s->kq, kk);
-  Lane& RL = *s->lanes[ks->lane];
-  if (!s->kq_off.load() && s->kq_pub_epoch.load(std::memory_order_acquire) >= need) {
-    // the epoch's consumer is launched and its slot published: no lock (the
-    // slot cannot be reused before this epoch completes, which needs this key)
-    const int slot = (int)(need % byteps_server::kKqRing);
-    ev = s->kq_ev[slot];
-    seq = s->kq_ev_seq[slot];
-    if (stream) {
-      RL.where = "key_release: wait d2h";
-      // behind the lane's pull copies too (a store is rewritten by the fold)
-      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
-      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
-      RL.where = "key_release: release kernel";
-    }
-    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
-  } else {
-    if (stream) RL.where = "key_release: kq_mu";
-    std::lock_guard<std::mutex> g(s->kq_mu);
-    if (stream) RL.where = "key_release: launch";
-    if (s->kq_off.load()) return 1;
-    uint32_t launched = 0;
-    keyq_state(s->kq, kk, &need, &launched);
-    for (; launched < need; launched = keyq_launched(s->kq)) {
-      const uint32_t next = launched + 1;
-      const int slot = (int)(next % byteps_server::kKqRing);
-      if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
-        return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
-                    byteps_server::kKqRing);
-      hipEvent_t& e = s->kq_ev[slot];
-      if (!e) {
-        if (int rc = force_device(s)) return rc;
-        const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        if (he != hipSuccess) {
-          e = nullptr;
-          return hip_fail(he, "hipEventCreate(consumer)");
-        }
-      }
-      uint32_t got = 0;
-      hipStream_t cs = nullptr;
-      if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
-      s->kq_ev_epoch[slot] = got;
-      s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
-      s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
-      s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
-    }
-    if (stream) {
-      RL.where = "key_release: wait d2h";
-      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
-      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
-      RL.where = "key_release: release kernel";
-    }
-    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
-    const int slot = (int)(need % byteps_server::kKqRing);
-    ev = s->kq_ev[slot];
-    seq = s->kq_ev_seq[slot];
-  }
-  if (stream) RL.where = "key_release: publish";
-  if (skip) return 0;  // the round is folded by a lane launch, which publishes it
-  s->n_key_releases.add();
-  ks->kq_round_epoch = need;
-  return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
-}
-
-// The keyed completer saw epoch `epoch`'s consumer (lane seq `seq`) complete:
-// if a consumer gave up waiting, every key released at that epoch or later
-// fails (its store is not the round's fold) and device releases go off for
-// good; then the epoch is published and the pulls parked on it go to their
-// lanes' issuers (or fail with their key).
-void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
-  std::vector<PullJob> go, keep;
-  std::vector<KeyState*> failed;
-  {
-    std::lock_guard<std::mutex> g(s->kq_mu);
-    if (s->kq && keyq_failed(s->kq)) {
-      if (getenv("BPSR_SERVER_RELEASE_DEBUG")) {
-        fprintf(stderr, "bpsr server: epoch %u timed out: %s\n", epoch, keyq_debug(s->kq).c_str());
-        for (size_t l = 0; l < s->lanes.size(); ++l) {
-          Lane& L = *s->lanes[l];
-          size_t nc = 0, ncp = 0, np = 0;
-          uint64_t iss = 0;
-          {
-            std::lock_guard<std::mutex> dg(L.done_mu);
-            iss = L.issued_seq;
-          }
-          {
-            std::lock_guard<std::mutex> cg(L.comb_mu);
-            nc = L.comb.size();
-            ncp = L.copies.size();
-            np = L.pulls.size();
-          }
-          fprintf(stderr,
-                  "  lane %zu: issued %llu done %llu, queued folds %zu copies %zu pulls %zu, "
-                  "issuer at %s\n",
-                  l, (unsigned long long)iss, (unsigned long long)L.done_pub.load(), nc, ncp, np,
-                  L.where.load());
-        }
-        int rounds_done = 0, pending = 0;
-        for (KeyState* k : s->kq_keys) {
-          if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) ++rounds_done;
-          pending += k->pending;
-        }
-        fprintf(stderr, "  keys released for this epoch %d of %zu, deferred jobs %d\n",
-                rounds_done, s->kq_keys.size(), pending);
-      }
-      s->kq_off.store(true);
-      for (KeyState* k : s->kq_keys)
-        if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
-    }
-    s->kq_done_seq = seq;
-    for (PullJob& j : s->kq_parked) (j.kseq <= seq ? go : keep).push_back(j);
-    s->kq_parked.swap(keep);
-  }
-  for (KeyState* k : failed) {
-    std::lock_guard<std::mutex> g(k->mu);
-    fail(BYTEPS_REDUCE_ETIMEOUT, "device release: a key of the queue was not pushed within %.3f s "
-         "(BPSR_SERVER_RELEASE_TIMEOUT_S); its epoch's folds are void", s->kq_timeout_s);
-    fail_key(s, k, BYTEPS_REDUCE_ETIMEOUT);
-  }
-  for (PullJob& j : go) {
-    int err = 0;
-    {
-      std::lock_guard<std::mutex> g(j.ks->mu);
-      err = j.ks->error;
-    }
-    if (err) {
-      if (j.direct) {
-        j.direct->finish(err);
-      } else {
-        j.resp.status = err;
-        enqueue_response(s, j.resp);
-      }
-      continue;
-    }
-    Lane& L = *s->lanes[j.ks->lane];
-    std::lock_guard<std::mutex> g(L.comb_mu);
-    L.pulls.push_back(j);
-    L.comb_cv.notify_one();
-  }
-}
 
 // Blocking readers of a keyed round's store wait for its epoch to be
 // published (caller holds no lock); then the key's error, if it failed.
@@ -1230,8 +634,8 @@ int check_pos(const byteps_server* s, const KeyState* ks, int pos) {
 // that position of the round's order, which the group stamped for the whole
 // key, instead of its position here — every piece of the key then folds in the
 // same order (server.cc:216-250 has one order per key).
-int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = nullptr,
-           int pos = -1) {
+int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer,
+           int pos) {
   if (ks->error) return key_error(ks);
   const int N = s->cfg.num_workers;
   Lane& L = *s->lanes[ks->lane];
@@ -1650,7 +1054,7 @@ void issuer_main(byteps_server* s, int lane) {
     L.where = "window";
     {
       std::unique_lock<std::mutex> dl(L.done_mu);
-      L.done_cv.wait(dl, [&] { return L.issued_seq - L.done_seq < s->inflight; });
+      L.done_cv.wait(dl, [&] { return L.issued_seq - L.done_seq < byteps_server::kInflight; });
     }
     lk.lock();
     folds.swap(L.comb);
@@ -1694,7 +1098,7 @@ int own_key_status(KeyState* ks) {
 // Init pushes block until every worker's init push has arrived and the store
 // is initialised: the reference answers them only then (server.cc:184-198).
 int arrive_and_wait_init(byteps_server* s, KeyState* ks, int w, std::unique_lock<std::mutex>& lk,
-                         std::vector<FoldJob>* defer = nullptr) {
+                         std::vector<FoldJob>* defer) {
   const bool init_round = !ks->inited;
   int rc = arrive(s, ks, w, defer);
   if (rc || !init_round) return rc;
@@ -1753,7 +1157,7 @@ void destroy_lanes(byteps_server* s) {
     if (Lp && Lp->completer.joinable()) Lp->completer.join();
 }
 
-}  // namespace
+}  // namespace srv
 }  // namespace bpsr
 
 using namespace bpsr;
@@ -1795,7 +1199,6 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (const char* fa = getenv("BPSR_SERVER_FAIL_AFTER")) s->fail_after = atol(fa);
   if (const char* cb = getenv("BPSR_SERVER_COMBINE")) s->combine = atoi(cb) != 0;
   if (s->schedule || s->blocking) s->combine = false;
-  if (const char* fl = getenv("BPSR_SERVER_INFLIGHT")) s->inflight = std::max(1L, atol(fl));
   if (cfg->release != BYTEPS_SERVER_RELEASE_LAUNCH && cfg->release != BYTEPS_SERVER_RELEASE_DEVICE)
     return fail(BYTEPS_REDUCE_EARGS, "unknown release %d", cfg->release);
   s->dev_release = cfg->release == BYTEPS_SERVER_RELEASE_DEVICE;
@@ -1814,22 +1217,14 @@ int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   int rc = force_device(s.get());
   if (rc) return rc;
   s->acc_load.assign(cfg->engine_lanes, 0);
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  (void)prio_lo;
-  const char* pv = getenv("BPSR_SERVER_D2H_PRIORITY");
-  const bool d2h_high = pv && std::string(pv) == "high";
   for (int i = 0; i < cfg->engine_lanes; ++i) {
     s->lanes.push_back(std::make_unique<Lane>());
     Lane& L = *s->lanes.back();
     hipError_t e = hipStreamCreateWithFlags(&L.fold, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.copy, hipStreamNonBlocking);
-    // d2h streams (mirror copies, copying pulls): normal priority by default;
-    // BPSR_SERVER_D2H_PRIORITY=high puts them on a hardware queue of their own
-    // (measured: no gain for copying pulls).
-    if (e == hipSuccess)
-      e = d2h_high ? hipStreamCreateWithPriority(&L.d2h, hipStreamNonBlocking, prio_hi)
-                   : hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
+    // d2h streams (mirror copies, copying pulls): normal priority (a
+    // high-priority queue of their own measured no gain)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.d2h, hipStreamNonBlocking);
     if (e == hipSuccess && s->schedule)
       e = hipEventCreateWithFlags(&L.job_done, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -1971,206 +1366,6 @@ int byteps_server_init_key(byteps_server* s, uint64_t key, size_t len, int dtype
 
 }  // extern "C"
 
-namespace bpsr {
-namespace {
-int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
-                    int dtype, int location, byteps_server_push_cb cb, void* ctx,
-                    SyncWait* direct, int pos = -1);
-// A blocking call's wait for the lane's launch `seq` to complete.
-void wait_lane_done(Lane& L, uint64_t seq) {
-  if (spin_until([&] { return L.done_pub.load(std::memory_order_acquire) >= seq; })) return;
-  std::unique_lock<std::mutex> dl(L.done_mu);
-  L.done_cv.wait(dl, [&] { return L.done_seq >= seq; });
-}
-// Wait for a round's fold, read from the key's state under its lock (fold_seq
-// / fold_lane / kq_round_epoch).  A keyed round is readable as soon as its
-// key's completion word says so (the consumer may still be folding other
-// keys): poll that word and the keyed completer's progress for up to
-// kKeyedSpinUs, then sleep until the completer publishes the epoch (which
-// also settles a consumer that gave up).
-constexpr int kKeyedSpinUs = 200;
-void wait_round_fold(byteps_server* s, Lane& FL, uint64_t need, int kq_key, uint32_t kq_epoch) {
-  if (FL.done_pub.load(std::memory_order_acquire) >= need) return;
-  if (kq_key >= 0 && kq_epoch) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      for (int i = 0; i < 32; ++i) {
-        if (keyq_key_done(s->kq, kq_key, kq_epoch)) return;
-        if (FL.done_pub.load(std::memory_order_acquire) >= need) return;
-        __builtin_ia32_pause();
-      }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kKeyedSpinUs)) break;
-    }
-  }
-  wait_lane_done(FL, need);
-}
-// The pull copy service for a blocking pull of `len` bytes into `out`, when
-// `out` is this device's memory (the service's release covers this device
-// only) and the pull is small enough that a lane copy's launch cost matters.
-constexpr size_t kServiceMaxPull = 16u << 20;
-CopyService* service_get(byteps_server* s) {
-  std::lock_guard<std::mutex> g(s->svc_mu);
-  if (!s->svc && !s->svc_tried) {
-    s->svc_tried = true;
-    if (force_device(s) || copysvc_create(s->cfg.device, &s->svc)) s->svc = nullptr;  // lane copies then
-  }
-  // a service that gave up (a job not served in time) takes no more pulls:
-  // they ride lane copies, as with BPSR_SERVER_PULL_SERVICE=0
-  return s->svc && !copysvc_broken(s->svc) ? s->svc : nullptr;
-}
-bool on_this_device(const byteps_server* s, const void* p) {
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return a.type == hipMemoryTypeDevice && a.device == s->cfg.device;
-}
-CopyService* service_for(byteps_server* s, void* out, size_t len) {
-  if (!s->pull_service || len == 0 || len > kServiceMaxPull) return nullptr;
-  if (!on_this_device(s, out)) return nullptr;
-  return service_get(s);
-}
-// A blocking push's source for the service's copiers: this device's memory;
-// nullptr when the push takes the lane path.  Host sources stay on the lane
-// path: the copiers reading pinned host memory over PCIe made config 1's
-// host-resident rounds slower than the lanes' SDMA copies (r04s35: 28 vs 31.6
-// GiB/s with views, 23 vs 30.6 with copying pulls).
-const void* service_src(byteps_server* s, const void* data, size_t len, int location) {
-  if (!s->pull_service || !s->combine || s->cfg.async_mode || t_responder || len == 0 ||
-      len > kServiceMaxPull || location != BYTEPS_SERVER_DEVICE)
-    return nullptr;
-  return on_this_device(s, data) ? data : nullptr;
-}
-// A service copy that failed because the service gave up (a job not served
-// in time): the same bytes through the key lane's d2h stream instead, so the
-// call still completes (later calls take the lanes: service_get).
-int fallback_copy(byteps_server* s, KeyState* ks, void* dst, const void* src, size_t len) {
-  Lane& L = *s->lanes[ks->lane];
-  hipError_t e = hipMemcpyAsync(dst, src, len, hipMemcpyDeviceToDevice, L.d2h);
-  if (e == hipSuccess) e = hipStreamSynchronize(L.d2h);
-  return e == hipSuccess ? 0 : hip_fail(e, "copy (after the copy service gave up)");
-}
-// The events given to byteps_server_order_after so far, waited for on the
-// host before a service copy (the service copies on no stream of ours).
-int wait_order_gate(byteps_server* s) {
-  const uint64_t gseq = s->gate_seq.load(std::memory_order_acquire);
-  if (gseq <= s->gate_done.load(std::memory_order_acquire)) return 0;
-  hipEvent_t gev;
-  {
-    std::lock_guard<std::mutex> g(s->gate_mu);
-    gev = s->gate_ev;
-  }
-  // the event's latest record covers every gate recorded up to gseq
-  hipError_t e = hipEventSynchronize(gev);
-  if (e != hipSuccess) return hip_fail(e, "order_after gate sync");
-  uint64_t d = s->gate_done.load(std::memory_order_relaxed);
-  while (d < gseq && !s->gate_done.compare_exchange_weak(d, gseq)) {
-  }
-  return 0;
-}
-// A blocking pull through the copy service: wait for the round's fold as a
-// device view does (its completer's published sequence, no HIP call), then
-// one service copy; count the pull after the copy, as the lane path does.
-// Sync mode keeps the store still meanwhile: the next round needs this
-// worker's next push, which follows this pull.
-int service_pull(byteps_server* s, CopyService* svc, KeyState* ks, void* out, size_t len) {
-  std::unique_lock<std::mutex> lk(ks->mu);
-  if (len > ks->len) return fail(BYTEPS_REDUCE_EARGS, "pull of %zu bytes > key len %zu", len, ks->len);
-  ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
-  if (ks->error) return key_error(ks);
-  const bool has = ks->has_done;
-  hipEvent_t ev = ks->fold_ev;
-  const uint64_t need = ks->fold_seq;
-  const int fl = ks->fold_lane;
-  const void* store = ks->store;
-  const int kq_key = fl < 0 ? ks->kq_key.load() : -1;
-  const uint32_t kq_epoch = ks->kq_round_epoch;
-  lk.unlock();
-  if (need) {
-    wait_round_fold(s, fl < 0 ? *s->klane : *s->lanes[fl], need, kq_key, kq_epoch);
-  } else if (has) {
-    hipError_t e = hipEventSynchronize(ev);
-    if (e != hipSuccess) return hip_fail(e, "store fold sync");
-  }
-  lk.lock();
-  if (ks->error) return key_error(ks);  // a keyed epoch that timed out
-  lk.unlock();
-  if (int rc = wait_order_gate(s)) return rc;
-  int rc = copysvc_copy(svc, out, store, len);
-  if (rc && copysvc_broken(svc)) rc = fallback_copy(s, ks, out, store, len);
-  else if (!rc) s->n_service_pulls.fetch_add(1, std::memory_order_relaxed);
-  if (rc) return rc;
-  s->n_pulls.add();
-  lk.lock();
-  count_pull(s, ks);
-  return BYTEPS_REDUCE_OK;
-}
-// A blocking push through the copy service: once the slot is free (the key's
-// previous fold has completed — the same rule as the lane copy's stream wait),
-// the service copies the data into the worker's slot with no key lock held
-// and no HIP call; then the push arrives as if the transport had written the
-// slot itself (a push_ready: the round needs no copy ordering, and a device
-// release can be a host store).
-int service_push(byteps_server* s, CopyService* svc, uint64_t key, int worker, const void* src,
-                 size_t len, int dtype) {
-  KeyState* ks = get_key(s, key, true);
-  std::unique_lock<std::mutex> lk(ks->mu);
-  int rc = allocate(s, ks, len, dtype);
-  if (rc) return rc;
-  ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-  if (ks->error) return key_error(ks);
-  if (ks->has_done) {
-    const bool keyed = ks->fold_lane < 0;
-    const uint64_t need = ks->fold_seq;
-    const int fl = ks->fold_lane;
-    const int kq_key = keyed ? ks->kq_key.load() : -1;
-    const uint32_t kq_epoch = ks->kq_round_epoch;
-    hipEvent_t ev = ks->fold_ev;
-    lk.unlock();
-    if (need) {
-      wait_round_fold(s, keyed ? *s->klane : *s->lanes[fl], need, kq_key, kq_epoch);
-    } else {
-      const hipError_t e = hipEventSynchronize(ev);
-      if (e != hipSuccess) return hip_fail(e, "slot's last fold");
-    }
-    lk.lock();
-    if (ks->error) return key_error(ks);
-  }
-  lk.unlock();
-  if ((rc = wait_order_gate(s))) return rc;  // the data's producer on the caller's stream
-  if ((rc = copysvc_copy(svc, ks->slot[worker], src, len)) && copysvc_broken(svc))
-    rc = fallback_copy(s, ks, ks->slot[worker], src, len);
-  if (rc) return rc;
-  s->n_service_pushes.fetch_add(1, std::memory_order_relaxed);
-  lk.lock();
-  if (ks->error) return key_error(ks);
-  std::vector<FoldJob> defer;
-  if ((rc = arrive_and_wait_init(s, ks, worker, lk, &defer))) return rc;
-  if (!defer.empty()) {
-    lk.unlock();
-    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return rc;
-    lk.lock();
-  }
-  return 0;
-}
-void sync_push_cb(void* ctx, uint64_t, int, int status) {
-  static_cast<SyncWait*>(ctx)->finish(status);
-}
-// The caller's thread-local message for a status that came back through a callback.
-int sync_status(byteps_server* s, uint64_t key, int status, const char* what) {
-  if (status == 0) return 0;
-  KeyState* ks = get_key(s, key, false);
-  std::string msg = "?";
-  if (ks) {
-    std::lock_guard<std::mutex> g(ks->mu);
-    msg = ks->error_msg;
-  }
-  return fail(status, "key %llu: %s failed: %s", (unsigned long long)key, what, msg.c_str());
-}
-}  // namespace
-}  // namespace bpsr
-
 extern "C" {
 
 int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* data, size_t len,
@@ -2225,7 +1420,7 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
 }  // extern "C"
 
 namespace bpsr {
-namespace {
+inline namespace srv {
 // byteps_server_push_async; with `direct`, a blocking push's issuer-batched
 // copy reports to its waiter instead of the responder (cb/ctx serve the
 // other paths, answered through the responder as for any non-blocking push).
@@ -2304,7 +1499,7 @@ int push_async_impl(byteps_server* s, uint64_t key, int worker, const void* data
   }
   return BYTEPS_REDUCE_OK;
 }
-}  // namespace
+}  // namespace srv
 }  // namespace bpsr
 
 extern "C" {
@@ -2578,390 +1773,7 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
   return ks->error ? key_error(ks) : BYTEPS_REDUCE_OK;
 }
 
-// ------------------------------------------------------- batched calls --
-
-int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n, int worker) {
-  if (!s || (n > 0 && !keys) || n < 0) return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  if (worker < 0 || worker >= s->cfg.num_workers)
-    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
-  int rc = set_device(s);
-  if (rc) return rc;
-  std::vector<FoldJob> defer;
-  for (int i = 0; i < n; ++i) {
-    KeyState* ks = get_key(s, keys[i], false);
-    if (!ks || !ks->allocated) {
-      (void)issue_deferred(s, defer);
-      return fail(BYTEPS_REDUCE_EARGS, "key %llu not initialised", (unsigned long long)keys[i]);
-    }
-    std::unique_lock<std::mutex> lk(ks->mu);
-    if (!can_push(s, ks, worker)) {
-      // never block while holding deferred rounds: others may wait on them
-      lk.unlock();
-      if ((rc = issue_deferred(s, defer))) return rc;
-      lk.lock();
-      ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-    }
-    if (ks->error) {
-      lk.unlock();
-      (void)issue_deferred(s, defer);
-      return key_error(ks);
-    }
-    const bool init_round = !ks->inited;
-    if ((rc = arrive(s, ks, worker, &defer))) {
-      lk.unlock();
-      (void)issue_deferred(s, defer);
-      return rc;
-    }
-    if (init_round && !ks->inited) {
-      lk.unlock();
-      if ((rc = issue_deferred(s, defer))) return rc;
-      lk.lock();
-      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
-      if (ks->error) return key_error(ks);
-    }
-  }
-  return issue_deferred(s, defer);
-}
-
-// A push_many's host copies in flight at most (per call): 4 partitions of
-// BytePS's 4,096,000-B bound.  The transport's calls of different workers then
-// interleave on the link partition by partition, so rounds complete — and are
-// folded and pulled back — while later partitions are still crossing PCIe,
-// instead of one worker's whole batch landing before any other worker's.
-constexpr size_t kHostPushInflight = 16u << 20;
-
-hipEvent_t pool_take(byteps_server* s) {
-  {
-    std::lock_guard<std::mutex> g(s->ev_pool_mu);
-    if (!s->ev_pool.empty()) {
-      hipEvent_t e = s->ev_pool.back();
-      s->ev_pool.pop_back();
-      return e;
-    }
-  }
-  hipEvent_t e = nullptr;
-  return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
-}
-
-void pool_give(byteps_server* s, hipEvent_t e) {
-  std::lock_guard<std::mutex> g(s->ev_pool_mu);
-  s->ev_pool.push_back(e);
-}
-
-// byteps_server_push_many from host memory, in BytePS's order (core_loops.cc:
-// 492-564 issues every partition's ZPush as it comes): key by key, the H2D
-// copy into the slot on the key's lane (its own `copied` event, and the lane's
-// copy mark), then the arrival, whose completed round goes to the issuer at
-// once — with at most kHostPushInflight bytes of this call's copies in flight.
-// Every slot was found free before (the caller's step 1).  Returns once every
-// copy has landed (the blocking contract).
-int push_many_host(byteps_server* s, std::vector<KeyState*>& ks_of, const void* const* datas,
-                   const size_t* lens, int n, int worker) {
-  struct Flight {
-    hipEvent_t ev;
-    size_t bytes;
-  };
-  std::deque<Flight> flight;
-  size_t in_flight = 0;
-  int rc = 0;
-  auto retire = [&](size_t need) -> int {
-    while (!flight.empty() && (need == 0 || in_flight + need > kHostPushInflight)) {
-      const hipError_t e = hipEventSynchronize(flight.front().ev);
-      pool_give(s, flight.front().ev);
-      in_flight -= flight.front().bytes;
-      flight.pop_front();
-      if (e != hipSuccess) return hip_fail(e, "push copy");
-    }
-    return 0;
-  };
-  std::vector<char> lane_ready(s->lanes.size(), 0);
-  std::vector<FoldJob> defer;
-  for (int i = 0; i < n && !rc; ++i) {
-    KeyState* ks = ks_of[i];
-    Lane& L = *s->lanes[ks->lane];
-    if ((rc = retire(lens[i]))) break;
-    hipEvent_t fe = pool_take(s);
-    if (!fe) {
-      rc = fail(BYTEPS_REDUCE_EHIP, "hipEventCreate (push window)");
-      break;
-    }
-    {
-      std::lock_guard<std::mutex> bg(L.batch_mu);
-      hipError_t e = hipSuccess;
-      if (!lane_ready[ks->lane]) {  // once per lane: behind the lane's folds so far
-        lane_ready[ks->lane] = 1;
-        e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
-      }
-      {
-        std::lock_guard<std::mutex> g(ks->mu);
-        // keyed folds run on the consumer's stream, not behind the fold mark
-        if (e == hipSuccess && ks->keyed && ks->has_done)
-          e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
-        if (e == hipSuccess)
-          e = hipMemcpyAsync(ks->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice, L.copy);
-        if (e == hipSuccess) e = hipEventRecord(ks->copied, L.copy);
-      }
-      if (e == hipSuccess) e = hipEventRecord(L.copy_mark, L.copy);
-      if (e == hipSuccess) L.copy_seq.fetch_add(1);
-      if (e == hipSuccess) e = hipEventRecord(fe, L.copy);
-      if (e != hipSuccess) {
-        pool_give(s, fe);
-        rc = hip_fail(e, "push copy");
-        break;
-      }
-    }
-    flight.push_back({fe, lens[i]});
-    in_flight += lens[i];
-    std::unique_lock<std::mutex> lk(ks->mu);
-    ks->round_copied = true;
-    const bool init_round = !ks->inited;
-    if ((rc = arrive(s, ks, worker, &defer))) break;
-    if (init_round && !ks->inited) {  // held until every worker's init push is in
-      lk.unlock();
-      if ((rc = issue_deferred(s, defer))) break;
-      lk.lock();
-      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
-      if (ks->error) {
-        rc = key_error(ks);
-        break;
-      }
-    }
-    lk.unlock();
-    if (!defer.empty() && (rc = issue_deferred(s, defer))) break;
-  }
-  if (!defer.empty()) {
-    const int r2 = issue_deferred(s, defer);
-    if (!rc) rc = r2;
-  }
-  const int r3 = retire(0);
-  return rc ? rc : r3;
-}
-
-int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* const* datas,
-                            const size_t* lens, int n, int worker, int dtype, int location) {
-  if (!s || n < 0 || (n > 0 && (!keys || !datas || !lens)))
-    return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  if (worker < 0 || worker >= s->cfg.num_workers)
-    return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
-  int rc = set_device(s);
-  if (rc) return rc;
-  // 1. every slot free (its previous round folded), then the copies: per lane
-  //    ONE wait for the lane's folds so far, then one batched copy (device
-  //    sources) or a hipMemcpyAsync per key (host sources), then the lane's
-  //    copy mark, which every later fold of the lane waits for
-  std::vector<KeyState*> ks_of(n);
-  std::vector<std::vector<int>> by_lane(s->lanes.size());
-  for (int i = 0; i < n; ++i) {
-    if (!datas[i]) return fail(BYTEPS_REDUCE_EARGS, "null data for key %d", i);
-    KeyState* ks = get_key(s, keys[i], true);
-    ks_of[i] = ks;
-    std::unique_lock<std::mutex> lk(ks->mu);
-    if ((rc = allocate(s, ks, lens[i], dtype))) return rc;
-    ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-    if (ks->error) return key_error(ks);
-    by_lane[ks->lane].push_back(i);
-  }
-  // host data (the default engine, sync mode): copies and arrivals key by key
-  if (location == BYTEPS_SERVER_HOST && s->combine && !s->cfg.async_mode) {
-    if ((rc = push_many_host(s, ks_of, datas, lens, n, worker))) return rc;
-    return BYTEPS_REDUCE_OK;
-  }
-  for (size_t l = 0; l < by_lane.size(); ++l) {
-    if (by_lane[l].empty()) continue;
-    Lane& L = *s->lanes[l];
-    std::lock_guard<std::mutex> bg(L.batch_mu);
-    hipError_t e = hipStreamWaitEvent(L.copy, L.fold_mark, 0);
-    if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-    {  // keyed folds run on the consumer's stream, not behind the fold mark
-      std::vector<hipEvent_t> waits;
-      for (int i : by_lane[l]) {
-        std::lock_guard<std::mutex> g(ks_of[i]->mu);
-        if (ks_of[i]->keyed && ks_of[i]->has_done) waits.push_back(ks_of[i]->fold_ev);
-      }
-      std::sort(waits.begin(), waits.end());
-      waits.erase(std::unique(waits.begin(), waits.end()), waits.end());
-      for (hipEvent_t w : waits)
-        if ((e = hipStreamWaitEvent(L.copy, w, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-    }
-    if (location == BYTEPS_SERVER_HOST) {
-      // each key's own copy event: its round folds once ITS copies have
-      // landed, while the lane's later partitions are still crossing PCIe
-      for (int i : by_lane[l]) {
-        e = hipMemcpyAsync(ks_of[i]->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice,
-                           L.copy);
-        if (e == hipSuccess) {
-          std::lock_guard<std::mutex> g(ks_of[i]->mu);
-          e = hipEventRecord(ks_of[i]->copied, L.copy);
-        }
-        if (e != hipSuccess) return hip_fail(e, "push copy");
-      }
-    } else {
-      std::vector<byteps_bucket_desc> d(by_lane[l].size());
-      for (size_t k = 0; k < by_lane[l].size(); ++k) {
-        const int i = by_lane[l][k];
-        std::memset(&d[k], 0, sizeof(d[k]));
-        d[k].dst = ks_of[i]->slot[worker];
-        d[k].srcs[0] = datas[i];
-        d[k].len = lens[i];
-        d[k].n = 1;
-      }
-      if ((rc = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
-                                  BYTEPS_REDUCE_MODE_REFERENCE, L.copy, L.ring)))
-        return rc;
-    }
-    if ((e = hipEventRecord(L.copy_mark, L.copy)) != hipSuccess)
-      return hip_fail(e, "hipEventRecord");
-    L.copy_seq.fetch_add(1);
-  }
-  // 2. arrivals, with the rounds they complete folded per lane in one launch
-  std::vector<FoldJob> defer;
-  for (int i = 0; i < n; ++i) {
-    KeyState* ks = ks_of[i];
-    std::unique_lock<std::mutex> lk(ks->mu);
-    ks->round_copied = true;
-    if (location != BYTEPS_SERVER_HOST) ks->round_mark_copy = true;
-    const bool init_round = !ks->inited;
-    if ((rc = arrive(s, ks, worker, &defer))) {
-      lk.unlock();
-      (void)issue_deferred(s, defer);
-      return rc;
-    }
-    if (init_round && !ks->inited) {
-      lk.unlock();
-      if ((rc = issue_deferred(s, defer))) return rc;
-      lk.lock();
-      ks->cv.wait(lk, [&] { return ks->inited || ks->error; });
-      if (ks->error) return key_error(ks);
-    }
-  }
-  if ((rc = issue_deferred(s, defer))) return rc;
-  if (s->blocking)  // engine blocking mode: the folds issued above have completed
-    for (size_t l = 0; l < by_lane.size(); ++l)
-      if (!by_lane[l].empty()) {
-        hipError_t e = hipStreamSynchronize(s->lanes[l]->fold);
-        if (e != hipSuccess) return hip_fail(e, "engine blocking: fold sync");
-      }
-  // 3. blocking contract: every source may be reused once the call returns
-  //    (a lane's copy mark, re-recorded since, covers this call's copies too)
-  for (size_t l = 0; l < by_lane.size(); ++l) {
-    if (by_lane[l].empty()) continue;
-    hipError_t e = hipEventSynchronize(s->lanes[l]->copy_mark);
-    if (e != hipSuccess) return hip_fail(e, "push copy");
-  }
-  return BYTEPS_REDUCE_OK;
-}
-
-int byteps_server_pull_many(byteps_server* s, const uint64_t* keys, void* const* outs,
-                            const size_t* lens, int n, int location) {
-  if (!s || n < 0 || (n > 0 && (!keys || !outs || !lens)))
-    return fail(BYTEPS_REDUCE_EARGS, "null argument");
-  int rc = set_device(s);
-  if (rc) return rc;
-  if (s->cfg.async_mode) {
-    // every fold changes the store: each pull keeps the single call's
-    // ordering (copy queued under the key lock, later folds wait for it)
-    for (int i = 0; i < n; ++i)
-      if ((rc = byteps_server_pull(s, keys[i], outs[i], lens[i], location))) return rc;
-    return BYTEPS_REDUCE_OK;
-  }
-  std::vector<KeyState*> ks_of(n, nullptr);
-  std::vector<std::vector<int>> ready(s->lanes.size());  // rounds finished, copies not issued
-  std::vector<char> touched(s->lanes.size(), 0);
-  size_t ready_bytes = 0;
-  // Issue the copies of the keys found ready: per lane ONE wait for the lane's
-  // folds so far (they include every ready key's round: a round is published
-  // after its fold was issued and the mark raised), one batched copy (device
-  // destinations) or a hipMemcpyAsync per key (host), then the d2h mark.
-  auto flush = [&]() -> int {
-    for (size_t l = 0; l < ready.size(); ++l) {
-      if (ready[l].empty()) continue;
-      Lane& L = *s->lanes[l];
-      std::lock_guard<std::mutex> bg(L.batch_mu);
-      hipError_t e = hipStreamWaitEvent(L.d2h, L.fold_mark, 0);
-      if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-      if (location == BYTEPS_SERVER_HOST) {
-        for (int i : ready[l]) {
-          if (void* dv = pull_kernel_dst(outs[i], location)) {
-            if (int rc = byteps_reduce_copy(dv, ks_of[i]->store, lens[i], L.d2h)) return rc;
-            continue;
-          }
-          e = hipMemcpyAsync(outs[i], ks_of[i]->store, lens[i], hipMemcpyDeviceToHost, L.d2h);
-          if (e != hipSuccess) return hip_fail(e, "pull copy");
-        }
-      } else {
-        std::vector<byteps_bucket_desc> d(ready[l].size());
-        for (size_t k = 0; k < ready[l].size(); ++k) {
-          const int i = ready[l][k];
-          std::memset(&d[k], 0, sizeof(d[k]));
-          d[k].dst = outs[i];
-          d[k].srcs[0] = ks_of[i]->store;
-          d[k].len = lens[i];
-          d[k].n = 1;
-        }
-        int r = batched_with_ring(d.data(), (int)d.size(), BYTEPS_REDUCE_UINT8,
-                                  BYTEPS_REDUCE_MODE_REFERENCE, L.d2h, L.ring);
-        if (r) return r;
-      }
-      s->n_pull_launches.fetch_add(1, std::memory_order_relaxed);
-      if ((e = hipEventRecord(L.d2h_mark, L.d2h)) != hipSuccess)
-        return hip_fail(e, "hipEventRecord");
-      touched[l] = 1;
-      ready[l].clear();
-    }
-    return 0;
-  };
-  for (int i = 0; i < n; ++i) {
-    KeyState* ks = key_for_pull(s, keys[i]);
-    if (!ks) {
-      (void)flush();
-      return BYTEPS_REDUCE_EARGS;
-    }
-    ks_of[i] = ks;
-    std::unique_lock<std::mutex> lk(ks->mu);
-    if (lens[i] > ks->len || !outs[i]) {
-      lk.unlock();
-      (void)flush();
-      return fail(BYTEPS_REDUCE_EARGS, "pull %d: bad buffer or %zu bytes > key len %zu", i,
-                  lens[i], ks->len);
-    }
-    if (!pull_ready(s, ks)) {
-      lk.unlock();
-      // let enough ready bytes go while this round finishes; fewer, larger
-      // batched copies otherwise (rounds often complete together)
-      if (ready_bytes >= kPullFlushBytes) {
-        if ((rc = flush())) return rc;
-        ready_bytes = 0;
-      }
-      lk.lock();
-      ks->cv.wait(lk, [&] { return pull_ready(s, ks); });
-    }
-    if (ks->keyed && !ks->error) {  // its epoch published first
-      const uint64_t need = ks->fold_seq;
-      lk.unlock();
-      wait_published(s, ks, need);
-      lk.lock();
-    }
-    if (ks->error) {
-      lk.unlock();
-      (void)flush();
-      return key_error(ks);
-    }
-    ready[ks->lane].push_back(i);
-    ready_bytes += lens[i];
-  }
-  if ((rc = flush())) return rc;
-  for (size_t l = 0; l < touched.size(); ++l) {  // a later record covers this call's copies too
-    if (!touched[l]) continue;
-    hipError_t e = hipEventSynchronize(s->lanes[l]->d2h_mark);
-    if (e != hipSuccess) return hip_fail(e, "pull copy");
-  }
-  for (int i = 0; i < n; ++i) {
-    std::lock_guard<std::mutex> g(ks_of[i]->mu);
-    count_pull(s, ks_of[i]);  // server.cc:105-113
-  }
-  s->n_pulls.add((uint64_t)n);
-  return BYTEPS_REDUCE_OK;
-}
+// ------------------------------------------------------- other calls --
 
 int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, void* event) {
   if (!s || !event || n < 0 || (n > 0 && !keys)) return fail(BYTEPS_REDUCE_EARGS, "null argument");
@@ -3079,3 +1891,4 @@ bool server_key_inited(byteps_server* s, uint64_t key) {
 }
 
 }  // namespace bpsr
+

@@ -1,0 +1,212 @@
+// GPU-resident PS server, device releases (include/bpsr/server.h): one keyed
+// block queue folds every key of an epoch with ONE consumer launch, each key
+// released by its round's last arrival (bpsr_server_state.h).
+#include "bpsr_server_state.h"
+
+namespace bpsr {
+inline namespace srv {
+
+// ------------------------------------------------------ device releases --
+
+// The keyed queue over every allocated key of `dtype` (block order = key
+// order), built once, at the first round completion after the init round
+// (caller holds s->kq_mu and that key's mu).  Keys declared later, and keys
+// of other dtypes, keep the lane launches.
+void build_kq(byteps_server* s, int dtype) {
+  std::vector<KeyState*> keys;
+  {
+    std::shared_lock<std::shared_mutex> g(s->map_mu);
+    for (auto& kv : s->keys) {
+      KeyState* k = kv.second.get();
+      if (k->allocated && k->dtype == dtype) keys.push_back(k);
+    }
+  }
+  if (keys.empty()) return;
+  std::sort(keys.begin(), keys.end(),
+            [](const KeyState* a, const KeyState* b) { return a->key < b->key; });
+  const int N = s->cfg.num_workers;
+  std::vector<byteps_bucket_desc> d(keys.size());
+  for (size_t i = 0; i < keys.size(); ++i) {
+    std::memset(&d[i], 0, sizeof(d[i]));
+    d[i].dst = keys[i]->store;
+    for (int w = 0; w < N; ++w) d[i].srcs[w] = keys[i]->slot[w];
+    d[i].len = keys[i]->len;
+    d[i].n = N;
+  }
+  if (force_device(s) || keyq_create(d.data(), (int)d.size(), dtype, s->kq_timeout_s, &s->kq)) {
+    s->kq = nullptr;  // no queue: every round keeps the lane launches
+    return;
+  }
+  s->kq_keys = keys;
+  for (size_t i = 0; i < keys.size(); ++i) keys[i]->kq_key.store((int)i);
+}
+
+// Is this finished round of `ks` device-released?  Caller holds ks->mu.
+bool keyed_member(byteps_server* s, KeyState* ks) {
+  if (!s->dev_release || s->kq_off.load()) return false;
+  std::lock_guard<std::mutex> g(s->kq_mu);
+  if (!s->kq_tried) {
+    s->kq_tried = true;
+    build_kq(s, ks->dtype);
+  }
+  return ks->kq_key.load() >= 0;
+}
+
+// Release a finished round of a keyed key (caller holds ks->mu): the arrival
+// order and the release word go to the key's block — stored from the host
+// when the round's data is in its slots already (push_ready), or by a one-lane
+// kernel on `stream` behind the round's copies — after the consumer of the
+// block's epoch has been launched (the first release of an epoch launches
+// it).  Then the round is published like an issued fold.  Returns 1 when
+// device releases were turned off meanwhile (the caller folds with a launch).
+int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
+                bool skip) {
+  uint64_t perm = 0;  // position m's worker in bits 4m..4m+3 (16 positions)
+  for (size_t m = 0; m < order.size(); ++m) perm |= (uint64_t)order[m] << (4 * m);
+  if (skip) perm = ((uint64_t)kKeySkip << 32) | kKeySkip;
+  hipEvent_t ev = nullptr;
+  uint64_t seq = 0;
+  const int kk = ks->kq_key.load();
+  uint32_t need = keyq_next_epoch(s->kq, kk);
+  Lane& RL = *s->lanes[ks->lane];
+  if (!s->kq_off.load() && s->kq_pub_epoch.load(std::memory_order_acquire) >= need) {
+    // the epoch's consumer is launched and its slot published: no lock (the
+    // slot cannot be reused before this epoch completes, which needs this key)
+    const int slot = (int)(need % byteps_server::kKqRing);
+    ev = s->kq_ev[slot];
+    seq = s->kq_ev_seq[slot];
+    if (stream) {
+      RL.where = "key_release: wait d2h";
+      // behind the lane's pull copies too (a store is rewritten by the fold)
+      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
+      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+      RL.where = "key_release: release kernel";
+    }
+    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
+  } else {
+    if (stream) RL.where = "key_release: kq_mu";
+    std::lock_guard<std::mutex> g(s->kq_mu);
+    if (stream) RL.where = "key_release: launch";
+    if (s->kq_off.load()) return 1;
+    uint32_t launched = 0;
+    keyq_state(s->kq, kk, &need, &launched);
+    for (; launched < need; launched = keyq_launched(s->kq)) {
+      const uint32_t next = launched + 1;
+      const int slot = (int)(next % byteps_server::kKqRing);
+      if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
+        return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
+                    byteps_server::kKqRing);
+      hipEvent_t& e = s->kq_ev[slot];
+      if (!e) {
+        if (int rc = force_device(s)) return rc;
+        const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (he != hipSuccess) {
+          e = nullptr;
+          return hip_fail(he, "hipEventCreate(consumer)");
+        }
+      }
+      uint32_t got = 0;
+      hipStream_t cs = nullptr;
+      if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
+      s->kq_ev_epoch[slot] = got;
+      s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
+      s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
+      s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
+    }
+    if (stream) {
+      RL.where = "key_release: wait d2h";
+      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
+      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+      RL.where = "key_release: release kernel";
+    }
+    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
+    const int slot = (int)(need % byteps_server::kKqRing);
+    ev = s->kq_ev[slot];
+    seq = s->kq_ev_seq[slot];
+  }
+  if (stream) RL.where = "key_release: publish";
+  if (skip) return 0;  // the round is folded by a lane launch, which publishes it
+  s->n_key_releases.add();
+  ks->kq_round_epoch = need;
+  return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);
+}
+
+// The keyed completer saw epoch `epoch`'s consumer (lane seq `seq`) complete:
+// if a consumer gave up waiting, every key released at that epoch or later
+// fails (its store is not the round's fold) and device releases go off for
+// good; then the epoch is published and the pulls parked on it go to their
+// lanes' issuers (or fail with their key).
+void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
+  std::vector<PullJob> go, keep;
+  std::vector<KeyState*> failed;
+  {
+    std::lock_guard<std::mutex> g(s->kq_mu);
+    if (s->kq && keyq_failed(s->kq)) {
+      if (getenv("BPSR_SERVER_RELEASE_DEBUG")) {
+        fprintf(stderr, "bpsr server: epoch %u timed out: %s\n", epoch, keyq_debug(s->kq).c_str());
+        for (size_t l = 0; l < s->lanes.size(); ++l) {
+          Lane& L = *s->lanes[l];
+          size_t nc = 0, ncp = 0, np = 0;
+          uint64_t iss = 0;
+          {
+            std::lock_guard<std::mutex> dg(L.done_mu);
+            iss = L.issued_seq;
+          }
+          {
+            std::lock_guard<std::mutex> cg(L.comb_mu);
+            nc = L.comb.size();
+            ncp = L.copies.size();
+            np = L.pulls.size();
+          }
+          fprintf(stderr,
+                  "  lane %zu: issued %llu done %llu, queued folds %zu copies %zu pulls %zu, "
+                  "issuer at %s\n",
+                  l, (unsigned long long)iss, (unsigned long long)L.done_pub.load(), nc, ncp, np,
+                  L.where.load());
+        }
+        int rounds_done = 0, pending = 0;
+        for (KeyState* k : s->kq_keys) {
+          if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) ++rounds_done;
+          pending += k->pending;
+        }
+        fprintf(stderr, "  keys released for this epoch %d of %zu, deferred jobs %d\n",
+                rounds_done, s->kq_keys.size(), pending);
+      }
+      s->kq_off.store(true);
+      for (KeyState* k : s->kq_keys)
+        if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
+    }
+    s->kq_done_seq = seq;
+    for (PullJob& j : s->kq_parked) (j.kseq <= seq ? go : keep).push_back(j);
+    s->kq_parked.swap(keep);
+  }
+  for (KeyState* k : failed) {
+    std::lock_guard<std::mutex> g(k->mu);
+    fail(BYTEPS_REDUCE_ETIMEOUT, "device release: a key of the queue was not pushed within %.3f s "
+         "(BPSR_SERVER_RELEASE_TIMEOUT_S); its epoch's folds are void", s->kq_timeout_s);
+    fail_key(s, k, BYTEPS_REDUCE_ETIMEOUT);
+  }
+  for (PullJob& j : go) {
+    int err = 0;
+    {
+      std::lock_guard<std::mutex> g(j.ks->mu);
+      err = j.ks->error;
+    }
+    if (err) {
+      if (j.direct) {
+        j.direct->finish(err);
+      } else {
+        j.resp.status = err;
+        enqueue_response(s, j.resp);
+      }
+      continue;
+    }
+    Lane& L = *s->lanes[j.ks->lane];
+    std::lock_guard<std::mutex> g(L.comb_mu);
+    L.pulls.push_back(j);
+    L.comb_cv.notify_one();
+  }
+}
+
+}  // namespace srv
+}  // namespace bpsr
