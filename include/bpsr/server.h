@@ -180,9 +180,16 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
  * kernel (fetcher + 64 copier workgroups, on a non-blocking high-priority
  * stream of its own) stores once the bytes are visible device-wide — no HIP
  * call and no thread hand-off per pull (≈5–6 µs per small pull from 1 or 8
- * threads).  The kernel exits after 0.5 ms without a job (or
- * after 2 s; the next pull relaunches it), so a device-wide synchronisation
- * waits at most that long for it.  Events given to byteps_server_order_after
+ * threads).  The kernel exits after 0.5 ms without a job, and
+ * at 1 ms of age even while busy (a waiting or posting thread relaunches it
+ * at once), so a device-wide synchronisation elsewhere in the process
+ * (torch.cuda.synchronize, hipDeviceSynchronize, hipFree) waits for it at
+ * most ~1 ms plus one relaunch's age: measured p50 / p99 0.5 / 0.5 ms under 8
+ * threads copying nonstop (profiles/r05s04_copysvc_age_sweep.jsonl; a -m gpu
+ * test asserts median < 4 ms, max < 10 ms).  A job not served within 10 s is
+ * given up: the service raises its stop word, waits for its launch to end
+ * (no copy of it lands afterwards), turns itself off for good, and the call
+ * copies on the key's lane instead.  Events given to byteps_server_order_after
  * are waited for (on the host) before such a copy.  BPSR_SERVER_PULL_SERVICE=0
  * or other destinations: the copy is one of the lane issuer's batched pull
  * copies: the issuer tells the caller which of its launches carries the copy,
@@ -192,8 +199,10 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker);
  * does, so the pulls one round completion answers ride in one launch.  A call
  * made from inside a callback (on the responder thread) copies directly.  The
  * same holds for blocking pushes of device data (byteps_server_push).
- * BPSR_SERVER_SPIN_US=n: such a waiter polls the lane's completion for up to
- * n µs before it sleeps (default 0: it sleeps at once).  Blocking pushes FROM
+ * Copies into pinned host memory are made by the copy kernel through the
+ * memory's device view (beside the pushes' SDMA H2D copies the link then runs
+ * full duplex: 87 GB/s together instead of 55, tools/pcie_probe.py); pageable
+ * memory and device destinations use hipMemcpyAsync.  Blocking pushes FROM
  * this device's memory (up to 16 MiB) take the copy service the same way:
  * once the key's previous fold has completed, the service copies the data
  * into the worker's slot with no key lock held, then the push arrives as a
@@ -268,9 +277,11 @@ int byteps_server_key_info(byteps_server* s, uint64_t key, uint64_t* rounds, int
  * copy out of a store and fold that the lanes of keys[0..n) (n = 0: every
  * lane) issue from now on runs after `event` (a hipEvent_t the caller recorded
  * on the stream that produced a push's data or last touched a pull's
- * destination) — hipStreamWaitEvent on the lanes' streams, no host wait.  The
- * event may be re-recorded or destroyed once the call returns.  Call it before
- * the push / pull calls it orders. */
+ * destination) — hipStreamWaitEvent on the lanes' streams, no host wait.  Work
+ * no lane stream orders waits for the event on the host first: the copy
+ * service's copies, and a device release stored from the host (a push_ready
+ * round with device releases on).  The event may be re-recorded or destroyed
+ * once the call returns.  Call it before the push / pull calls it orders. */
 int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, void* event);
 
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]

@@ -721,7 +721,11 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer,
     ks->order.clear();
     ks->arrived = 0;
     if (!ks->round_copied) {  // the pushes are in their slots already (push_ready)
-      const int rc = key_release(s, ks, order, nullptr);
+      // a release from the host orders nothing on the device: the producers
+      // a caller named with byteps_server_order_after are waited for here
+      // (a no-op without a pending order_after)
+      int rc = wait_order_gate(s);
+      if (!rc) rc = key_release(s, ks, order, nullptr);
       if (rc <= 0) {
         if (rc) fail_key(s, ks, rc);
         return rc;
@@ -1796,12 +1800,15 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
     Lane& L = *s->lanes[l];
     // push copies (and the issuer's), pull copies and mirrors, and the folds
     // of push_ready rounds whose slots the caller wrote on its own stream
+    // (device releases: the gate below, waited for before a host release)
     for (hipStream_t st : {L.copy, L.d2h, L.fold}) {
       const hipError_t e = hipStreamWaitEvent(st, ev, 0);
       if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent(caller event)");
     }
   }
-  if (s->pull_service && s->combine && !s->cfg.async_mode) {  // the copy service's gate
+  // the gate of the work no stream of ours orders: the copy service's copies
+  // and device releases stored from the host
+  if ((s->pull_service || s->dev_release) && s->combine && !s->cfg.async_mode) {
     std::lock_guard<std::mutex> g(s->gate_mu);
     if (!s->gate_stream && (rc = force_device(s))) return rc;
     hipError_t e = hipSuccess;

@@ -1881,6 +1881,53 @@ def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
         assert s1["consumer_launches"] == 0 and s1["key_releases"] == 0
 
 
+def test_order_after_orders_device_released_push_ready(port, monkeypatch):
+    """with device releases a push_ready round is released by a
+    host store, which no lane stream orders.  The transport writes the slots
+    on its own stream behind a long spin, hands the event to order_after and
+    signals the arrivals at once (no host wait): the release waits for the
+    event first, so the consumer folds the written bytes — the oracle's sum —
+    not the slots' previous contents."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    dt, N, n = DType.FLOAT32, 2, 1 << 20
+    key = 91
+    srv = PSServer(N)
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(device=dev)
+    zeros = [torch.zeros(n, device=dev) for _ in range(N)]
+    ts = [threading.Thread(target=srv.push, args=(key, w, zeros[w], dt)) for w in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    ins = [data(dt, n, w, 1, key) for w in range(N)]
+    src = [torch.from_numpy(x).to(dev) for x in ins]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(300_000_000)                  # the producer, still running
+        for w in range(N):
+            GpuReducer().copy(srv.recv_slot(key, w), src[w], n * 4, stream=st)
+        ev = torch.cuda.Event()
+        ev.record(st)
+    srv.order_after(ev, [key])
+    still_running = not st.query()
+    for w in range(N):
+        srv.push_ready(key, w)
+    out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    srv.pull(key, out)
+    got = out.cpu().numpy()
+    want = np.zeros(n * 4, np.uint8)
+    port.sum_n(want, ins, n * 4, dt)      # two fp32 operands: either order, one sum
+    stt = srv.stats()
+    srv.pull(key, out)                    # the round's other pull (it re-arms after N)
+    srv.close()
+    assert still_running, "the producer finished before the releases: nothing was ordered"
+    assert stt["key_releases"] == 1 and stt["consumer_launches"] == 1, stt
+    assert np.array_equal(got, want)
+
+
 def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     """The keyed queue's contract: every key completes one round per epoch.  A
     round in which one key is never pushed makes that epoch's consumer give up
