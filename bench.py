@@ -1192,14 +1192,17 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     for p in parts:
         nparts[p.tensor] = nparts.get(p.tensor, 0) + 1
     arrivals = sorted(range(len(table)), key=lambda i: (-table[i].tensor, table[i].part))
+    from prophet_amd.arena import BucketArena
     gen = torch.Generator(device=dev)
     data, queues, hqueues = [], [], []
     for i in range(sets):
-        w = []
+        # the 8 workers' receive slots and the output: one skewed arena, the
+        # headline's HBM layout (prophet_amd/arena.py; separate allocations
+        # fold 1-1.5 % slower here, profiles/r05s23_overlap_skew.jsonl)
+        *w, out = BucketArena(N + 1, total, dev).slots()
         for k in range(N):
             gen.manual_seed(3000 + 10 * i + k)
-            w.append(torch.randn(total // 2, device=dev, generator=gen).half().view(torch.uint8))
-        out = torch.empty(total, dtype=torch.uint8, device=dev)
+            w[k].copy_(torch.randn(total // 2, device=dev, generator=gen).half().view(torch.uint8))
         data.append((w, out))
         q = red.make_blockq([[(out[toff[p.tensor] + p.offset:][:p.len],
                                [x[toff[p.tensor] + p.offset:][:p.len] for x in w], p.len)
@@ -1216,6 +1219,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
     # never waits behind the spinning consumer (include/bpsr/reduce.h)
     live_s = queues[0].stream()
     rel_s = torch.cuda.Stream(device=dev)
+    overlap_on = [False]
     nb = len(by_block)
     # one scheduler + inline PUSH loop per input set (a loop drives one queue);
     # Z_BATCH_SIZE 64, Z_NET_B 10000, Z_CREDIT 16 MiB, the reference's block
@@ -1245,8 +1249,11 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
             q.release(b, rel_s)
 
     def pre_released(i):
+        # released before the launch: on the launch stream itself without
+        # overlap; with overlap on the release stream (a release queued on a
+        # consumer queue waits there for the consumer before it)
         q = queues[i % sets]
-        q.release(-1, live_s)
+        q.release(-1, rel_s if overlap_on[0] else live_s)
         q.launch(live_s)
 
     def live_host(i):   # the pushes are resident: releases straight from the host
@@ -1268,11 +1275,23 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                         "(one consumer launch per iteration); live = the native PUSH loop "
                         "(Prophet scheduler, stream-ordered release kernels, the release "
                         "groups ready together as one kernel); live_per_block = one "
-                        "release kernel per block"),
+                        "release kernel per block; receive slots in one skewed HBM arena"),
            "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
+    res["overlap"] = ("consecutive launches overlap (byteps_reduce_blockq_overlap: the two "
+                      "consumer queues alternate, a launch dispatched once every workgroup of "
+                      "the previous one has started); *_no_overlap: one stream-ordered queue")
     rel_kernels = {"live_per_block": nb, "pre_released": 1, "live_host_releases": 0}
-    for name, fn in (("live", live), ("live_per_block", live_per_block),
-                     ("pre_released", pre_released), ("live_host_releases", live_host)):
+
+    def set_overlap(on):
+        overlap_on[0] = on
+        for q in queues + hqueues:
+            q.overlap(on)
+
+    variants = (("live", live, True), ("live_per_block", live_per_block, True),
+                ("pre_released", pre_released, True), ("live_host_releases", live_host, True),
+                ("live_no_overlap", live, False), ("pre_released_no_overlap", pre_released, False))
+    for name, fn, ov in variants:
+        set_overlap(ov)
         for i in range(30):
             fn(i)
         torch.cuda.synchronize()
@@ -1286,6 +1305,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
             for i in range(iters):
                 fn(i)
             hs.append((time.perf_counter() - t0) / iters * 1e6)
+            queues[0].join(live_s)      # both consumer queues' last launches
             e1.record(live_s)
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) / iters)
@@ -1294,10 +1314,12 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                      "spread": round((max(ts) - min(ts)) / ms, 4),
                      "frac_of_roofline": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "host_us_per_iter": round(statistics.median(hs), 1)}
-        if name == "live":
+        base = name.replace("_no_overlap", "")
+        if base == "live":
             rel_kernels[name] = round((sum(lp.release_calls() for lp in loops) - c0)
                                       / (reps * iters), 2)
-        res[name]["release_kernels_per_iter"] = rel_kernels[name]
+        res[name]["release_kernels_per_iter"] = rel_kernels.get(name, rel_kernels[base])
+    set_overlap(True)
     for q in queues + hqueues:
         q.status(live_s)
     ok = True

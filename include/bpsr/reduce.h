@@ -233,6 +233,20 @@ int byteps_reduce_blockq_host_releases(byteps_reduce_blockq* q, int on);
 int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int count);
 /* The device's consumer stream (see above); owned by the library. */
 int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream);
+/* Overlap (on = 1; dispatch-ordered consumer only, EARGS otherwise):
+ * consecutive launches may run at once, so one iteration's first blocks fold
+ * while the previous one's last tiles drain.  A launch goes to whichever of
+ * the device's two consumer queues the device's previous block-queue launch
+ * did not use, and its first workgroup is dispatched only after every
+ * workgroup of that previous launch has started (so waiting workgroups never
+ * hold the slots an earlier launch still needs).  The launch
+ * forks from `stream` unless `stream` is a consumer queue, and does NOT order
+ * `stream` after the fold: byteps_reduce_blockq_join(q, s) makes s wait, on
+ * the device, for every block-queue launch of the device so far (status
+ * joins first).  Read outputs, or rewrite inputs, only after a join.  on = 0
+ * restores the default for later launches. */
+int byteps_reduce_blockq_overlap(byteps_reduce_blockq* q, int on);
+int byteps_reduce_blockq_join(byteps_reduce_blockq* q, void* stream);
 /* Debug (synchronises the device): out = launch epoch, nblocks, the sticky
  * error word, the host's release epoch per block, the device release words,
  * the device block_first table (nblocks + 1), and 1 if the device tile table

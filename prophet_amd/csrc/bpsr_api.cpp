@@ -676,7 +676,10 @@ struct byteps_reduce_blockq {
   // pooled high- and normal-priority streams shared one for some pool
   // indices, tools/pushloop_diag.py).
   bool own_queue = true;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  // Overlap (byteps_reduce_blockq_overlap): launches
+  // alternate between the device's two consumer queues and do not join back.
+  bool overlap = false;
+  hipEvent_t fork_ev = nullptr;
   // Host releases (byteps_reduce_blockq_host_releases): pinned, coherent
   // words the host writes and the launch's helper workgroup forwards.
   uint32_t* hflags = nullptr;
@@ -697,37 +700,114 @@ struct byteps_reduce_blockq {
   uint32_t* khdone_dev = nullptr;
 };
 
-// One consumer stream per device, created on first use, never destroyed:
-// every block queue's consumer on a device runs on it (in launch order).
+// Per device, created on first use, never destroyed: two consumer queues
+// (all-CU-masked streams, each a hardware queue of its own; queue 0 is
+// byteps_reduce_blockq_stream, where every launch without overlap runs, in
+// launch order) and the dispatch sequence every block-queue launch outside a
+// capture takes part in: sequence numbers, the
+// started-workgroup counter and its target, the signal word, the stream of the
+// latest launch, and per stream the completion event of its latest launch
+// (what byteps_reduce_blockq_join waits for).
+struct ConsumerDev {
+  std::mutex mu;                        // sequence order = enqueue order
+  hipStream_t q[2] = {nullptr, nullptr};
+  unsigned long long* started = nullptr;  // started counter (device, a line of its own)
+  unsigned long long target = 0;        // counted workgroups of every launch so far
+  hipStream_t last = nullptr;           // stream of the latest launch
+  bool any = false;                     // a launch is in the sequence
+  struct Tail {
+    hipStream_t stream;
+    hipEvent_t ev;
+    bool record;  // the latest launch there carried no stop event: join records one
+  };
+  std::vector<Tail> tails;
+};
 static std::mutex g_consumer_mu;
-static hipStream_t g_consumer[64];
+static ConsumerDev g_cdev[64];
 
-static hipError_t consumer_stream(int device, int cus, hipStream_t* out) {
+static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
   if (device < 0 || device >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> g(g_consumer_mu);
-  if (!g_consumer[device]) {
+  hipStream_t& slot = g_cdev[device].q[which];
+  if (!slot) {
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
     for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
-    hipError_t e = hipExtStreamCreateWithCUMask(&g_consumer[device], (uint32_t)mask.size(),
-                                                mask.data());
+    hipError_t e = hipExtStreamCreateWithCUMask(&slot, (uint32_t)mask.size(), mask.data());
     if (cur != device && cur >= 0) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
-      g_consumer[device] = nullptr;
+      slot = nullptr;
       return e;
     }
   }
-  *out = g_consumer[device];
+  *out = slot;
   return hipSuccess;
 }
 
-static hipError_t blockq_events(byteps_reduce_blockq* q) {
-  hipError_t e = hipSuccess;
-  if (!q->fork_ev) e = hipEventCreateWithFlags(&q->fork_ev, hipEventDisableTiming);
-  if (e == hipSuccess && !q->join_ev) e = hipEventCreateWithFlags(&q->join_ev, hipEventDisableTiming);
+static hipError_t consumer_stream(int device, int cus, hipStream_t* out) {
+  return consumer_queue(device, cus, 0, out);
+}
+
+// D.mu held.  The started counters, once per device.
+static hipError_t seq_init(ConsumerDev& D, int device) {
+  if (D.started) return hipSuccess;
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != device) (void)hipSetDevice(device);
+  const size_t bytes = 256;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e == hipSuccess) e = hipMemset(p, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (cur != device && cur >= 0) (void)hipSetDevice(cur);
+  if (e != hipSuccess) {
+    if (p) (void)hipFree(p);
+    return e;
+  }
+  D.started = static_cast<unsigned long long*>(p);
+  return hipSuccess;
+}
+
+// D.mu held.  The join entry of stream `s`: its event completes with the
+// latest launch on `s` (the launch's stop event), or is recorded on `s` by
+// the next join when that launch carried none (a stop event is an
+// end-of-kernel release: ~5 µs when another kernel follows on its stream,
+// ~2.4 µs of an overlapped iteration; r05s22-23).
+static hipError_t seq_tail(ConsumerDev& D, hipStream_t s, ConsumerDev::Tail** out) {
+  for (auto& t : D.tails)
+    if (t.stream == s) {
+      *out = &t;
+      return hipSuccess;
+    }
+  hipEvent_t e = nullptr;
+  const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  if (r != hipSuccess) return r;
+  D.tails.push_back({s, e, false});
+  *out = &D.tails.back();
+  return hipSuccess;
+}
+
+// D.mu held; before enqueueing the kernel of a launch on `ls`: put it in the
+// sequence and, when the device's previous launch went to another stream,
+// gate `ls` until every workgroup launched so far has started (the gate
+// gives up after gate_ticks).
+static hipError_t seq_prepare(ConsumerDev& D, int device, BlockqLaunch& Q, hipStream_t ls,
+                              uint64_t gate_ticks) {
+  hipError_t e = seq_init(D, device);
+  if (e != hipSuccess) return e;
+  if (D.any && D.last != ls) e = launch_seq_gate(D.started, D.target, gate_ticks, ls);
+  Q.started = D.started;
   return e;
+}
+
+// D.mu held; after the kernel was enqueued.
+static void seq_commit(ConsumerDev& D, const BlockqLaunch& Q, hipStream_t ls) {
+  if (!Q.started) return;
+  D.target += seq_counted(Q.grid);
+  D.last = ls;
+  D.any = true;
 }
 
 static void blockq_free(byteps_reduce_blockq* q) {
@@ -737,7 +817,6 @@ static void blockq_free(byteps_reduce_blockq* q) {
   if (q->kcnt) (void)hipFree(q->kcnt);
   if (q->khdone) (void)hipHostFree(q->khdone);
   if (q->fork_ev) (void)hipEventDestroy(q->fork_ev);
-  if (q->join_ev) (void)hipEventDestroy(q->join_ev);
   if (q->dev_table) (void)hipFree(q->dev_table);
   if (q->flags) (void)hipFree(q->flags);
   if (q->ctl) (void)hipFree(q->ctl);
@@ -825,6 +904,8 @@ int byteps_reduce_blockq_config(byteps_reduce_blockq* q, int wg_per_cu, double t
   if (wg_per_cu > 8) return fail(BYTEPS_REDUCE_EARGS, "wg_per_cu %d > 8", wg_per_cu);
   if (wg_per_cu > 0 && q->host_rel)
     return fail(BYTEPS_REDUCE_EARGS, "host releases need the dispatch-ordered consumer");
+  if (wg_per_cu > 0 && q->overlap)
+    return fail(BYTEPS_REDUCE_EARGS, "overlap needs the dispatch-ordered consumer");
   if (wg_per_cu >= 0) q->occ = wg_per_cu;
   if (timeout_s > 0) q->timeout_s = timeout_s;
   return BYTEPS_REDUCE_OK;
@@ -895,23 +976,78 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     // residency cap through LDS (the kernel's own static LDS included)
     lds = ((kLdsPerCU / (size_t)q->occ) - 256) & ~(size_t)255;
   }
-  // Outside a capture the consumer runs on the queue's own hardware queue,
-  // forked from and joined back into `s` (a captured launch is pre-released
-  // by rule, so it may run on the capturing stream itself).
-  hipStream_t own = nullptr;
-  hipError_t e = hipSuccess;
-  if (q->own_queue && cap != hipStreamCaptureStatusActive) e = consumer_stream(q->device, q->cus, &own);
-  const bool fork = own && s != own;
-  hipStream_t ls = own ? own : s;
-  if (fork) {
-    e = blockq_events(q);
-    if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(own, q->fork_ev, 0);
+  const int pol = cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16);
+  Q.started = nullptr;
+  if (cap == hipStreamCaptureStatusActive) {
+    // pre-released by rule: runs on the capturing stream, outside the sequence
+    const hipError_t e = launch_blockq(Q, q->ti.vpt, pol, lds, gated, q->dtype, q->mode, s);
+    return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
   }
-  if (fork) Q.L.stop = q->join_ev;  // the consumer's own completion joins `s` back
-  if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16), lds, gated, q->dtype, q->mode, ls);
-  if (fork && e == hipSuccess) e = hipStreamWaitEvent(s, q->join_ev, 0);
+  // The consumer runs on a consumer queue of the device (a hardware queue of
+  // its own), forked from `s`; without overlap it runs on queue 0 and joins
+  // back into `s`, with overlap it takes the queue the device's previous
+  // launch did not and does not join (byteps_reduce_blockq_join).
+  ConsumerDev& D = g_cdev[q->device];
+  hipStream_t c0 = nullptr, c1 = nullptr;
+  hipError_t e = hipSuccess;
+  if (q->own_queue) e = consumer_queue(q->device, q->cus, 0, &c0);
+  if (e == hipSuccess && q->own_queue && q->overlap) e = consumer_queue(q->device, q->cus, 1, &c1);
+  if (e != hipSuccess) return hip_fail(e, "consumer stream");
+  std::lock_guard<std::mutex> dg(D.mu);
+  hipStream_t ls = s;
+  if (q->own_queue) ls = q->overlap && D.last == c0 ? c1 : c0;
+  const bool fork = q->own_queue && s != ls && (!q->overlap || (s != c0 && s != c1));
+  if (fork) {
+    if (!q->fork_ev) e = hipEventCreateWithFlags(&q->fork_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(q->fork_ev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ls, q->fork_ev, 0);
+  }
+  // The consumer's own completion completes the join event when `s` joins
+  // back at once; otherwise the next byteps_reduce_blockq_join records it (a
+  // stop event on every overlapped launch cost 2.4 µs per config-3
+  // iteration: 0.0744 vs 0.0720 ms, r05s23).
+  ConsumerDev::Tail* tail = nullptr;
+  if (e == hipSuccess) e = seq_tail(D, ls, &tail);
+  const bool stop = !q->overlap && q->own_queue && s != ls;
+  if (e == hipSuccess) {
+    Q.L.stop = stop ? tail->ev : nullptr;
+    tail->record = !stop;
+  }
+  if (e == hipSuccess) e = seq_prepare(D, q->device, Q, ls, 4 * Q.timeout_ticks);
+  if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, pol, lds, gated, q->dtype, q->mode, ls);
+  if (e == hipSuccess) seq_commit(D, Q, ls);
+  if (e == hipSuccess && q->own_queue && !q->overlap && s != ls) e = hipStreamWaitEvent(s, tail->ev, 0);
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
+}
+
+int byteps_reduce_blockq_overlap(byteps_reduce_blockq* q, int on) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  std::lock_guard<std::mutex> g(q->mu);
+  if (!on) {
+    q->overlap = false;
+    return BYTEPS_REDUCE_OK;
+  }
+  if (q->keyed || q->occ != 0)
+    return fail(BYTEPS_REDUCE_EARGS, "overlap needs the dispatch-ordered consumer "
+                                     "(byteps_reduce_blockq_config wg_per_cu = 0)");
+  q->overlap = true;
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_join(byteps_reduce_blockq* q, void* stream) {
+  if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  hipStream_t s = to_stream(stream);
+  ConsumerDev& D = g_cdev[q->device];
+  std::lock_guard<std::mutex> dg(D.mu);
+  for (auto& t : D.tails) {
+    if (t.stream == s) continue;
+    hipError_t e = hipSuccess;
+    if (t.record) e = hipEventRecord(t.ev, t.stream);
+    t.record = false;
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, t.ev, 0);
+    if (e != hipSuccess) return hip_fail(e, "block queue join");
+  }
+  return BYTEPS_REDUCE_OK;
 }
 
 int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int count,
@@ -1001,6 +1137,10 @@ int byteps_reduce_blockq_release(byteps_reduce_blockq* q, int block, void* strea
 int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
   hipStream_t s = to_stream(stream);
+  if (q->overlap) {  // launches do not join their stream: the status waits for all of them
+    const int rc = byteps_reduce_blockq_join(q, stream);
+    if (rc) return rc;
+  }
   hipError_t e = hipMemcpyAsync(q->host_err, &q->ctl->err, sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -1174,9 +1314,15 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   // each (two fit in 160 KiB, three do not; 44 KiB stay free).
   const Tuning tu = tuning_for_n(q->ti.nmax);
   constexpr size_t kKeyedLds = 58u * 1024u;
-  e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16),
-                    kKeyedLds, true, q->dtype, q->mode, own);
+  Q.started = nullptr;
+  ConsumerDev& D = g_cdev[q->device];
+  std::lock_guard<std::mutex> dg(D.mu);  // in the device's dispatch sequence
+  e = seq_prepare(D, q->device, Q, own, 4 * Q.timeout_ticks);
+  if (e == hipSuccess)
+    e = launch_blockq(Q, q->ti.vpt, cache_pol(tu, (uint64_t)q->ti.tiles * q->ti.vpt * kBlock * 16),
+                      kKeyedLds, true, q->dtype, q->mode, own);
   if (e != hipSuccess) return hip_fail(e, "keyed queue launch");
+  seq_commit(D, Q, own);
   __atomic_store_n(&q->launch_epoch, ep, __ATOMIC_RELEASE);
   if (stream) *stream = own;
   if (epoch) *epoch = ep;

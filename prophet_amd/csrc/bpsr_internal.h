@@ -131,7 +131,19 @@ struct BlockqLaunch {
   // device-wide — a key's store can be read before the whole epoch ends.
   uint32_t* kcnt;
   uint32_t* khdone;          // host words (device view), one per block
+  // Dispatch sequence: each of the launch's last
+  // kSeqLast workgroups (by index) adds one to the device's started counter
+  // on entry; a launch on another stream is gated on the count
+  // (launch_seq_gate).  Null in a captured launch.
+  unsigned long long* started;
 };
+constexpr uint32_t kSeqLast = 8;  // one per XCD: workgroups are dealt round-robin over 8
+inline uint32_t seq_counted(uint32_t grid) { return grid < kSeqLast ? grid : kSeqLast; }
+// One wave on `s`: returns once the counter reaches target (the last
+// workgroups of every launch counted so far have started), or after
+// timeout_ticks of wall_clock64() (a safety net; the count is exact).
+hipError_t launch_seq_gate(const unsigned long long* started, unsigned long long target,
+                           uint64_t timeout_ticks, hipStream_t s);
 // Arrival order of a keyed block: position m's source is worker
 // (perm >> 4m) & 15 — positions 0..7 in the block's word, 8..15 in its second
 // word (wide queues, 9..16 sources); kKeySkip: the round is folded

@@ -139,6 +139,29 @@ hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,
   return hipGetLastError();
 }
 
+// Dispatch-sequence gate: one wave, enqueued on a
+// consumer launch's stream ahead of its kernel, returns once the last
+// workgroups of the device's earlier launches have all started (the counter
+// reaches the target; system-scope polls, the adds are system-scope
+// atomics).  Bounded: past the timeout it returns anyway (the count is exact
+// by construction; this only keeps a mistake from hanging the stream).
+__global__ void seq_gate_kernel(const unsigned long long* started, unsigned long long target,
+                                uint64_t timeout_ticks) {
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    const unsigned long long v =
+        __hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v >= target || wall_clock64() - t0 > timeout_ticks) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+hipError_t launch_seq_gate(const unsigned long long* started, unsigned long long target,
+                           uint64_t timeout_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(seq_gate_kernel, dim3(1), dim3(64), 0, s, started, target, timeout_ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bool g, int dtype,
                          int mode, hipStream_t s) {
   const bool acc = mode == kModeAccumF32;

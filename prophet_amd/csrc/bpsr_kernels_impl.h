@@ -486,8 +486,22 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Dispatch sequence: each of the launch's last
+// kSeqLast workgroups counts itself started on entry, before any wait (one
+// no-return vector atomic; every other workgroup skips it — a counted start
+// costs its wave the atomic's ~1 µs of vmcnt, measured 5 µs per config-3
+// launch when every workgroup counted).  Hardware deals a launch's
+// workgroups round-robin over the 8 XCDs and dispatches each XCD's share in
+// index order, so the last 8 started means every workgroup has.  A launch
+// on another stream is gated on the count (seq_gate_kernel).
+__device__ __forceinline__ void note_started(const BlockqLaunch& Q) {
+  if (Q.started == nullptr || threadIdx.x != 0 || blockIdx.x + kSeqLast < gridDim.x) return;
+  (void)__hip_atomic_fetch_add(Q.started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_kernel(BlockqLaunch Q) {
+  note_started(Q);
   // record slots alternate: iteration i reads slot i&1 and stages the next
   // record into the other one, so no wave overwrites a record still being read
   __shared__ __attribute__((aligned(16))) uint32_t s_rec[2][kRecWords];
@@ -603,6 +617,7 @@ __device__ __forceinline__ void forward_host_releases(const BlockqLaunch& Q) {
 
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_gate_kernel(BlockqLaunch Q) {
+  note_started(Q);
   if (Q.helper && blockIdx.x == 0) {  // dispatched first: resident for the whole launch
     forward_host_releases(Q);
     return;
@@ -753,6 +768,7 @@ __device__ __forceinline__ void key_tile_done(const BlockqLaunch& Q, uint32_t bl
 
 template <class Op, int VPT, int NT>
 __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
+  note_started(Q);
   if (Q.helper && blockIdx.x == 0) {  // dispatched first: resident for the whole launch
     forward_host_keys(Q);
     return;

@@ -268,11 +268,11 @@ class PushLoop:
     def end(self, timeout_s: float = 10.0) -> None:
         """Wait until every block has been released; with the consumer on the
         library's stream, the current torch stream then waits for it (on the
-        device), so later torch work sees the folded outputs."""
+        device, ``BlockQueue.join`` — also with overlapping launches), so
+        later torch work sees the folded outputs."""
         _ck(self._L.byteps_prophet_loop_end(self._h, float(timeout_s)))
         if getattr(self, "_on_library_stream", False):
-            import torch
-            torch.cuda.current_stream().wait_stream(self.blockq.stream())
+            self.blockq.join()      # torch's current stream, after the consumer
 
     def close(self) -> None:
         h = getattr(self, "_h", None)

@@ -52,7 +52,8 @@ EXPORTS = (
     "byteps_reduce_blockq_release", "byteps_reduce_blockq_status", "byteps_reduce_blockq_destroy",
     "byteps_reduce_blockq_debug", "byteps_reduce_blockq_stream",
     "byteps_reduce_blockq_release_range", "byteps_reduce_blockq_host_releases",
-    "byteps_reduce_blockq_release_host",
+    "byteps_reduce_blockq_release_host", "byteps_reduce_blockq_overlap",
+    "byteps_reduce_blockq_join",
 )
 
 
@@ -110,6 +111,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_destroy.argtypes = [_vp]
     L.byteps_reduce_blockq_debug.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint32), _int]
     L.byteps_reduce_blockq_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
+    L.byteps_reduce_blockq_overlap.argtypes = [_vp, _int]
+    L.byteps_reduce_blockq_join.argtypes = [_vp, _vp]
     _LIB = L
     return L
 
@@ -309,6 +312,17 @@ class BlockQueue:
         """Release blocks [first, first + count) from the host: no stream, no
         kernel.  Their data must already be complete and visible to the device."""
         _check(self.lib.byteps_reduce_blockq_release_host(self.handle, int(first), int(count)))
+
+    def overlap(self, on: bool = True) -> None:
+        """Consecutive launches may overlap (byteps_reduce_blockq_overlap):
+        a launch no longer orders its stream after the fold — ``join``
+        before reading the outputs or rewriting the inputs."""
+        _check(self.lib.byteps_reduce_blockq_overlap(self.handle, 1 if on else 0))
+
+    def join(self, stream=None) -> None:
+        """``stream`` (default: torch's current stream) waits on the device
+        for every block-queue launch of the device so far."""
+        _check(self.lib.byteps_reduce_blockq_join(self.handle, _stream_of(self.first, stream)))
 
     def status(self, stream=None) -> None:
         _check(self.lib.byteps_reduce_blockq_status(self.handle, _stream_of(self.first, stream)))

@@ -192,6 +192,8 @@ def test_block_queue_argument_errors_without_gpu():
     assert lib.byteps_reduce_blockq_release(None, 0, None) == reducer.EARGS
     assert lib.byteps_reduce_blockq_status(None, None) == reducer.EARGS
     assert lib.byteps_reduce_blockq_config(None, 0, 1.0) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_overlap(None, 1) == reducer.EARGS
+    assert lib.byteps_reduce_blockq_join(None, None) == reducer.EARGS
     assert lib.byteps_reduce_blockq_destroy(None) == reducer.OK
 
 

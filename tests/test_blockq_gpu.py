@@ -501,3 +501,138 @@ def test_host_releases_rules(red, dev):
     q.host_releases(False)
     q.config(wg_per_cu=1)
     q.close()
+
+
+# ------------------------------------- overlapping launches (round 5) --
+# byteps_reduce_blockq_overlap: consecutive launches alternate between the
+# device's two consumer queues, each dispatched only once every workgroup of
+# the previous launch has started.  The tables below have
+# more tiles than the consumer's resident slots (2 per CU), so a launch is
+# enqueued while its predecessor still has workgroups to dispatch.
+
+
+def _quarter_resnet(dev, dt=DType.FLOAT16):
+    from prophet_amd.buckets import prophet_blocks, resnet50_param_sizes
+    sizes = resnet50_param_sizes()
+    return Table(dev, dt, [[(max(1, sizes[i] // 4), 8, "normal") for i in g]
+                           for g in prophet_blocks(len(sizes))])
+
+
+def test_overlap_releases_after_previous_iteration_no_deadlock(red, dev):
+    """The pattern that deadlocks two freely overlapping launches: iteration
+    k's inputs are rewritten, and its blocks released, on a side stream that
+    first waits for every earlier launch (join) — so k's releases need k - 1
+    to finish.  Launch k is enqueued before them, while k - 1 may still have
+    workgroups to dispatch.  Four iterations of one queue with data changing
+    every iteration, each output copied out after a join: bit-exact, no
+    timeout (1 s)."""
+    tab = _quarter_resnet(dev)
+    q = red.make_blockq(tab.blocks, DType.FLOAT16)
+    q.config(wg_per_cu=0, timeout_s=1.0)
+    q.overlap(True)
+    cons, side, out_s = q.stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    staged, wants, outs = [], [], []
+    for it in range(4):
+        pushes, w = tab.host_inputs(700 + it)
+        staged.append([[p.to(dev) for p in ps] for ps in pushes])
+        wants.append(w)
+    torch.cuda.synchronize()
+    for it in range(4):
+        q.join(side)                     # side: after every launch so far (k - 1)
+        q.launch(cons)                   # k: enqueued before its releases
+        k = 0
+        with torch.cuda.stream(side):
+            for b, blk in enumerate(tab.blocks):
+                for dst, srcs, L in blk:
+                    for s, p in zip(srcs, staged[it][k]):
+                        s.copy_(p, non_blocking=True)
+                    k += 1
+                q.release(b, side)
+        q.join(out_s)
+        with torch.cuda.stream(out_s):
+            outs.append([v[0].clone() for v in tab.views])
+    torch.cuda.synchronize()
+    q.status(cons)
+    for it in range(4):
+        for i, (o, w) in enumerate(zip(outs[it], wants[it])):
+            assert np.array_equal(o.cpu().numpy(), w), (it, i)
+    q.close()
+
+
+def test_overlap_two_queues_live_and_classic_interleaved(red, dev):
+    """Two tables: A overlaps, B does not (its launches stay stream-ordered on
+    consumer queue 0 and wait for A's dispatch when A went to queue 1).  Six
+    rounds of A, B launched back to back with live releases from another
+    stream after each launch, then host releases on A: every output exact."""
+    dt = DType.FLOAT32
+    ta = Table(dev, dt, MIXED, offsets=True)
+    tb = _quarter_resnet(dev)
+    qa = red.make_blockq(ta.blocks, dt)
+    qb = red.make_blockq(tb.blocks, DType.FLOAT16)
+    for q in (qa, qb):
+        q.config(wg_per_cu=0, timeout_s=2.0)
+    qa.overlap(True)
+    pa, wa = ta.host_inputs(41)
+    pb, wb = tb.host_inputs(42)
+    ta.upload(pa)
+    tb.upload(pb)
+    torch.cuda.synchronize()
+    cons, rel = qa.stream(), torch.cuda.Stream()
+    for _ in range(6):
+        for t in (ta, tb):
+            for dst, *_ in t.views:
+                dst.fill_(0x5A)
+        torch.cuda.synchronize()
+        qa.launch(cons)
+        qb.launch(cons)
+        qa.release(-1, rel)
+        qb.release(-1, rel)
+        qa.join()
+        torch.cuda.synchronize()
+        qa.status(cons)
+        qb.status(cons)
+        ta.check(wa)
+        tb.check(wb)
+    qa.host_releases(True)
+    for _ in range(3):
+        qa.launch(cons)
+        qa.release_host(0, len(MIXED))
+    qa.status(cons)
+    torch.cuda.synchronize()
+    ta.check(wa)
+    qa.close()
+    qb.close()
+
+
+def test_overlap_rules(red, dev):
+    """Overlap needs the dispatch-ordered consumer (EARGS for a persistent
+    one, and a persistent config is refused while overlap is on); off again
+    restores stream-ordered launches: the launch stream then sees the
+    output without a join."""
+    from prophet_amd.reducer import EARGS, ReduceError
+    dt = DType.FLOAT32
+    tab = Table(dev, dt, [[(65_536, 4, "normal")], [(4096, 2, "normal")]])
+    q = red.make_blockq(tab.blocks, dt)
+    q.config(wg_per_cu=1)
+    with pytest.raises(ReduceError) as ei:
+        q.overlap(True)
+    assert ei.value.code == EARGS
+    q.config(wg_per_cu=0)
+    q.overlap(True)
+    with pytest.raises(ReduceError) as ei:
+        q.config(wg_per_cu=2)
+    assert ei.value.code == EARGS
+    q.overlap(False)
+    pushes, wants = tab.host_inputs(5)
+    tab.upload(pushes)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    q.release(-1, s)
+    q.launch(s)                          # classic: forks and joins back into s
+    with torch.cuda.stream(s):
+        got = [v[0].clone() for v in tab.views]
+    s.synchronize()
+    q.status(s)
+    for g, w in zip(got, wants):
+        assert np.array_equal(g.cpu().numpy(), w)
+    q.close()
