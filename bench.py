@@ -1667,6 +1667,19 @@ def main(argv=None):
                 line["server_cfg1"] = {"error": repr(e)}
         elif not args.no_server:
             line["server_cfg1"] = {"skipped": "the PS server needs a GPU (--device cpu)"}
+        # Hardware-queue placement (DESIGN.md §4.4 "placement"): the order in
+        # which legs make their streams decides which queues share hardware,
+        # and a stream that lands badly is slow: the host-resident server made
+        # after the consumer queues exist (4.3 vs 3.1 ms per round, r05s42),
+        # config 3's stream releases made after other legs churned streams
+        # (per-block releases 0.081 -> 2.4 ms per iteration, r05s33/s40).
+        # Config 3 right after the server measured clean for both (r05s42).
+        if world == 1 and cuda and not args.no_cfg3:
+            leg("cfg3_blockq")
+            try:
+                line["cfg3_blockq"] = cfg3_leg(dev, red)
+            except Exception as e:  # report, never hide
+                line["cfg3_blockq"] = {"error": repr(e)}
         if cuda and not args.no_e2e:
             leg("e2e_cfg5")
             try:
@@ -1682,11 +1695,6 @@ def main(argv=None):
                 line["fp16"] = fp16_leg(dev, red, N, B, args.steps)
             except Exception as e:  # report, never hide
                 line["fp16"] = {"error": repr(e)}
-        if cuda and not args.no_cfg3:
-            try:
-                line["cfg3_blockq"] = cfg3_leg(dev, red)
-            except Exception as e:  # report, never hide
-                line["cfg3_blockq"] = {"error": repr(e)}
         if cuda and not args.no_cfg3 and not args.no_server:
             try:
                 line["server_cfg3"] = server_cfg3_leg(dev)

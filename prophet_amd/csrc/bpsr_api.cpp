@@ -725,24 +725,32 @@ struct ConsumerDev {
 static std::mutex g_consumer_mu;
 static ConsumerDev g_cdev[64];
 
+// which: 0 or 1.  Both consumer queues are made together, one after the
+// other, the first time either is asked for.
 static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
   if (device < 0 || device >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> g(g_consumer_mu);
-  hipStream_t& slot = g_cdev[device].q[which];
-  if (!slot) {
+  ConsumerDev& D = g_cdev[device];
+  if (!D.q[0]) {
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
     for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
-    hipError_t e = hipExtStreamCreateWithCUMask(&slot, (uint32_t)mask.size(), mask.data());
+    hipStream_t made[2] = {nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+      e = hipExtStreamCreateWithCUMask(&made[i], (uint32_t)mask.size(), mask.data());
     if (cur != device && cur >= 0) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
-      slot = nullptr;
+      for (hipStream_t m : made)
+        if (m) (void)hipStreamDestroy(m);
       return e;
     }
+    D.q[0] = made[0];
+    D.q[1] = made[1];
   }
-  *out = slot;
+  *out = D.q[which];
   return hipSuccess;
 }
 

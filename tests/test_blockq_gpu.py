@@ -524,8 +524,8 @@ def test_overlap_releases_after_previous_iteration_no_deadlock(red, dev):
     first waits for every earlier launch (join) — so k's releases need k - 1
     to finish.  Launch k is enqueued before them, while k - 1 may still have
     workgroups to dispatch.  Four iterations of one queue with data changing
-    every iteration, each output copied out after a join: bit-exact, no
-    timeout (1 s)."""
+    every iteration, each output copied out after a join (and the next
+    iteration's releases after that copy): bit-exact, no timeout (1 s)."""
     tab = _quarter_resnet(dev)
     q = red.make_blockq(tab.blocks, DType.FLOAT16)
     q.config(wg_per_cu=0, timeout_s=1.0)
@@ -551,6 +551,9 @@ def test_overlap_releases_after_previous_iteration_no_deadlock(red, dev):
         q.join(out_s)
         with torch.cuda.stream(out_s):
             outs.append([v[0].clone() for v in tab.views])
+        # the caller's side of the contract: the next iteration's releases
+        # (which let its tiles rewrite the outputs) only after this read
+        side.wait_stream(out_s)
     torch.cuda.synchronize()
     q.status(cons)
     for it in range(4):

@@ -1,0 +1,61 @@
+"""Probe (not product code): config 3's block-queue variants (bench.cfg3_leg)
+measured alone and again after another bench leg ran in the same process —
+`--after` picks the leg (pcie, server_cfg1, e2e, group_idle: a server group
+made and closed with no rounds), or `--seq` runs a comma-separated sequence
+of legs (cfg3 measures).  Prints one line per measurement."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--after", default="server_cfg1")
+    ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--seq", default="")
+    a = ap.parse_args()
+    import torch
+    import bench
+    from prophet_amd.reducer import GpuReducer
+    dev = torch.device("cuda:0")
+    red = GpuReducer(0)
+
+    def show(tag):
+        r = bench.cfg3_leg(dev, red, iters=a.iters, reps=3)
+        print(tag, {k: (v["ms_per_iter"], v["frac_of_roofline"]) for k, v in r.items()
+                    if isinstance(v, dict)}, flush=True)
+
+    if a.seq:
+        link = None
+        for i, leg in enumerate(a.seq.split(",")):
+            if leg == "cfg3":
+                show(f"{i}:cfg3")
+            elif leg == "pcie":
+                link = bench.pcie_leg(dev, red)
+            elif leg == "server_cfg1":
+                r = bench.server_group_leg(dev, 1, 0, link=link)
+                print(f"{i}:server_cfg1", r["round_ms"], r.get("frac_of_link"),
+                      r["copying_pulls"]["round_ms"], flush=True)
+            elif leg == "e2e":
+                r = bench.e2e_leg(dev, 1, 0, link=link)
+                print(f"{i}:e2e", r["ms"], r.get("frac_of_link"), flush=True)
+            elif leg == "headline":
+                bench.main_headline_for_probe(dev) if hasattr(bench, "main_headline_for_probe") else None
+        return
+    show("alone")
+    link = bench.pcie_leg(dev, red)
+    if a.after == "server_cfg1":
+        bench.server_group_leg(dev, 1, 0, link=link)
+    elif a.after == "e2e":
+        bench.e2e_leg(dev, 1, 0, link=link)
+    elif a.after == "group_idle":
+        from prophet_amd.server import PSServerGroup
+        g = PSServerGroup(2, devices=[0], engine_lanes=4, split="hash")
+        g.close()
+    show(f"after_{a.after}")
+
+
+if __name__ == "__main__":
+    main()
