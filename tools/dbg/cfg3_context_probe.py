@@ -15,12 +15,26 @@ def main():
     ap.add_argument("--after", default="server_cfg1")
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--seq", default="")
+    ap.add_argument("--persistent", type=int, default=0,
+                    help="> 0: block queues use that many persistent workgroups per CU "
+                         "(no stalled dispatch; overlap requests ignored)")
     a = ap.parse_args()
     import torch
     import bench
     from prophet_amd.reducer import GpuReducer
     dev = torch.device("cuda:0")
     red = GpuReducer(0)
+    if a.persistent:
+        from prophet_amd import reducer as _r
+        _cfg, _ov = _r.BlockQueue.config, _r.BlockQueue.overlap
+        _r.BlockQueue.config = lambda q, wg_per_cu=-1, timeout_s=0.0: _cfg(q, a.persistent, timeout_s)
+        _r.BlockQueue.overlap = lambda q, on=True: None
+        _hr = _r.BlockQueue.host_releases
+
+        def host_releases(q, on=True):   # host releases need the dispatch-ordered consumer
+            _cfg(q, 0, 0.0)
+            _hr(q, on)
+        _r.BlockQueue.host_releases = host_releases
 
     def show(tag):
         r = bench.cfg3_leg(dev, red, iters=a.iters, reps=3)
