@@ -725,32 +725,26 @@ struct ConsumerDev {
 static std::mutex g_consumer_mu;
 static ConsumerDev g_cdev[64];
 
-// which: 0 or 1.  Both consumer queues are made together, one after the
-// other, the first time either is asked for.
+// which: 0 (every launch without overlap) or 1 (made at the first
+// overlapped launch: a queue that is never used is not made).
 static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
   if (device < 0 || device >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> g(g_consumer_mu);
-  ConsumerDev& D = g_cdev[device];
-  if (!D.q[0]) {
+  hipStream_t& slot = g_cdev[device].q[which];
+  if (!slot) {
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
     for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
     int cur = -1;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
-    hipStream_t made[2] = {nullptr, nullptr};
-    hipError_t e = hipSuccess;
-    for (int i = 0; i < 2 && e == hipSuccess; ++i)
-      e = hipExtStreamCreateWithCUMask(&made[i], (uint32_t)mask.size(), mask.data());
+    hipError_t e = hipExtStreamCreateWithCUMask(&slot, (uint32_t)mask.size(), mask.data());
     if (cur != device && cur >= 0) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
-      for (hipStream_t m : made)
-        if (m) (void)hipStreamDestroy(m);
+      slot = nullptr;
       return e;
     }
-    D.q[0] = made[0];
-    D.q[1] = made[1];
   }
-  *out = D.q[which];
+  *out = slot;
   return hipSuccess;
 }
 
