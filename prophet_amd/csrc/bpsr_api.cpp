@@ -989,6 +989,7 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   // its own), forked from `s`; without overlap it runs on queue 0 and joins
   // back into `s`, with overlap it takes the queue the device's previous
   // launch did not and does not join (byteps_reduce_blockq_join).
+  if (q->device < 0 || q->device >= 64) return fail(BYTEPS_REDUCE_EARGS, "device %d", q->device);
   ConsumerDev& D = g_cdev[q->device];
   hipStream_t c0 = nullptr, c1 = nullptr;
   hipError_t e = hipSuccess;
@@ -1005,12 +1006,14 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
     if (e == hipSuccess) e = hipStreamWaitEvent(ls, q->fork_ev, 0);
   }
   // The consumer's own completion completes the join event when `s` joins
-  // back at once; otherwise the next byteps_reduce_blockq_join records it (a
-  // stop event on every overlapped launch cost 2.4 µs per config-3
-  // iteration: 0.0744 vs 0.0720 ms, r05s23).
+  // back at once, or when the launch stream is the caller's (a join must not
+  // record on a stream the caller may have destroyed since); otherwise the
+  // next byteps_reduce_blockq_join records it on the consumer queue (a stop
+  // event on every overlapped launch cost 2.4 µs per config-3 iteration:
+  // 0.0744 vs 0.0720 ms, r05s23).
   ConsumerDev::Tail* tail = nullptr;
   if (e == hipSuccess) e = seq_tail(D, ls, &tail);
-  const bool stop = !q->overlap && q->own_queue && s != ls;
+  const bool stop = !q->own_queue || (!q->overlap && s != ls);
   if (e == hipSuccess) {
     Q.L.stop = stop ? tail->ev : nullptr;
     tail->record = !stop;
@@ -1032,12 +1035,14 @@ int byteps_reduce_blockq_overlap(byteps_reduce_blockq* q, int on) {
   if (q->keyed || q->occ != 0)
     return fail(BYTEPS_REDUCE_EARGS, "overlap needs the dispatch-ordered consumer "
                                      "(byteps_reduce_blockq_config wg_per_cu = 0)");
+  if (q->device < 0 || q->device >= 64) return fail(BYTEPS_REDUCE_EARGS, "device %d", q->device);
   q->overlap = true;
   return BYTEPS_REDUCE_OK;
 }
 
 int byteps_reduce_blockq_join(byteps_reduce_blockq* q, void* stream) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
+  if (q->device < 0 || q->device >= 64) return fail(BYTEPS_REDUCE_EARGS, "device %d", q->device);
   hipStream_t s = to_stream(stream);
   ConsumerDev& D = g_cdev[q->device];
   std::lock_guard<std::mutex> dg(D.mu);
