@@ -73,8 +73,11 @@ def test_bench_one_gpu_line_has_every_object():
     c3 = line["cfg3_blockq"]
     assert "error" not in c3, c3
     assert c3["exact_vs_torch_fold"] is True
-    for k in ("live", "pre_released"):
-        assert 0 < c3[k]["frac_of_roofline"] < 1
+    for k in ("live", "pre_released", "live_no_overlap", "pre_released_no_overlap",
+              "live_host_releases", "live_per_block"):
+        assert 0 < c3[k]["frac_of_roofline"] < 1, k
+    assert "overlap" in c3 and c3["live"]["release_kernels_per_iter"] > 0
+    assert line["scaling"] == "weak" and "no collective" in line["scaling_note"]
     s3 = line["server_cfg3"]             # config 3's keys through the server, two ways
     assert "error" not in s3, s3
     for k in ("launch", "device_releases"):
