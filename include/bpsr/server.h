@@ -69,11 +69,9 @@ typedef struct byteps_server_config {
                           round, as in the reference.  0 = the default engine */
   int release;         /* byteps_server_release: how a finished round is folded
                           — LAUNCH (0): the lane issuers' batched fold
-                          launches; DEVICE (1): device releases (below).
-                          byteps_server_config_from_env picks DEVICE, the
-                          dedicated server process of server.cc:339-400 where
-                          nothing else runs on the GPU (BPSR_SERVER_RELEASE=
-                          launch|device overrides either way)               */
+                          launches; DEVICE (1): device releases (below), for
+                          pushes that land in HBM.  BPSR_SERVER_RELEASE=
+                          launch|device overrides either way              */
 } byteps_server_config;
 
 typedef struct byteps_server byteps_server;
@@ -83,12 +81,18 @@ typedef struct byteps_server byteps_server;
  * (here "1" means asynchronous; the reference reads the flag inverted,
  * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
  * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0, and
- * release = DEVICE: the server process that byteps_server() (server.cc:
- * 339-400) starts does nothing else on its GPU, so device releases' one rule
- * for other GPU users of the process — no device-wide wait while an epoch is
- * open — holds; config 3's keys from one receive thread then fold at 0.50 of
- * the HBM roofline instead of 0.25-0.35 (the bench line's server_cfg3).  The
- * rounds that cannot be device-released fall back by themselves (see below). */
+ * release = LAUNCH.  Not DEVICE, although the server process byteps_server()
+ * (server.cc:339-400) starts does nothing else on its GPU: that process
+ * receives its pushes into host memory (ps-lite's buffers, server.cc:
+ * 174-218), so its rounds are copied rounds, which device releases cannot
+ * fold — they fold with launches anyway and the epoch's consumer only adds
+ * its residency and its waiting: config 1 from host memory took 11.5-13.3
+ * ms per round with device releases against 3.1 with launches (DESIGN.md §9
+ * round 5).  Device releases pay when the pushes land in HBM
+ * (byteps_server_push_ready after an RDMA write into GPU memory): config 3's
+ * keys from one receive thread at 0.49 of the HBM roofline instead of
+ * 0.21-0.28 (the bench line's server_cfg3) — set BPSR_SERVER_RELEASE=device
+ * (or release = DEVICE) for that shape. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
 /* Device releases (release = DEVICE or BPSR_SERVER_RELEASE=device; sync mode,

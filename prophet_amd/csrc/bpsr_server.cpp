@@ -1184,7 +1184,7 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   const char* eb = getenv("BYTEPS_SERVER_ENGINE_BLOCKING");  // server.cc:324
   cfg->engine_blocking = (eb && atoi(eb) != 0) ? 1 : 0;
   // the dedicated server process: nothing else waits on its GPU (server.h)
-  cfg->release = BYTEPS_SERVER_RELEASE_DEVICE;
+  cfg->release = BYTEPS_SERVER_RELEASE_LAUNCH;  // server.h: why not DEVICE
   return BYTEPS_REDUCE_OK;
 }
 

@@ -1823,16 +1823,17 @@ def test_device_release_rounds_bit_exact(port, N, dt, monkeypatch):
     assert 1 <= st["fold_launches"] - st0["fold_launches"] <= copied * len(keys)
 
 
-@pytest.mark.parametrize("release", [None, "launch"], ids=["env-default", "launch"])
+@pytest.mark.parametrize("release", [None, "device"], ids=["env-default", "device"])
 def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
     """The dedicated server process (server.cc:339-400) builds its server from
-    the environment (byteps_server_config_from_env): device releases by
-    default — one consumer launch per round, no fold launches — and
-    BPSR_SERVER_RELEASE=launch turns them off.  4 workers, push_ready rounds
-    from the slots, pulls into device memory: bit-exact with the oracle's left
-    fold in the recorded order either way."""
+    the environment (byteps_server_config_from_env): launches by default (its
+    pushes land in host memory, server.h), and BPSR_SERVER_RELEASE=device
+    turns device releases on — one consumer launch per round, no fold
+    launches.  4 workers, push_ready rounds from the slots, pulls into device
+    memory: bit-exact with the oracle's left fold in the recorded order either
+    way."""
     from prophet_amd.reducer import GpuReducer
-    from prophet_amd.server import RELEASE_DEVICE, PSServer
+    from prophet_amd.server import RELEASE_LAUNCH, PSServer
     monkeypatch.delenv("BPSR_SERVER_RELEASE", raising=False)
     if release:
         monkeypatch.setenv("BPSR_SERVER_RELEASE", release)
@@ -1842,7 +1843,7 @@ def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
     keys = [11, 12, 13]
     es = elem_size(dt)
     srv = PSServer.from_env()
-    assert srv.cfg.release == RELEASE_DEVICE and srv.cfg.num_workers == N
+    assert srv.cfg.release == RELEASE_LAUNCH and srv.cfg.num_workers == N
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(device=dev)      # never the legacy NULL stream (server.h)
     with torch.cuda.stream(st):
@@ -1874,7 +1875,7 @@ def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
                 st0 = srv.stats()
     s1 = srv.stats()
     srv.close()
-    if release is None:
+    if release == "device":
         assert s1["consumer_launches"] == R and s1["key_releases"] == R * len(keys)
         assert s1["fold_launches"] == st0["fold_launches"]
     else:
