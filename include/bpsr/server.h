@@ -82,15 +82,17 @@ typedef struct byteps_server byteps_server;
  * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
  * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0, and
  * release = LAUNCH.  Not DEVICE, although the server process byteps_server()
- * (server.cc:339-400) starts does nothing else on its GPU: that process
- * receives its pushes into host memory (ps-lite's buffers, server.cc:
- * 174-218), so its rounds are copied rounds, which device releases cannot
- * fold — they fold with launches anyway and the epoch's consumer only adds
- * its residency and its waiting: config 1 from host memory took 11.5-13.3
- * ms per round with device releases against 3.1 with launches (DESIGN.md §9
- * round 5).  Device releases pay when the pushes land in HBM
- * (byteps_server_push_ready after an RDMA write into GPU memory): config 3's
- * keys from one receive thread at 0.49 of the HBM roofline instead of
+ * (server.cc:339-400) starts does nothing else on its GPU, for two reasons.
+ * That process receives its pushes into host memory (ps-lite's buffers,
+ * server.cc:174-218), so its rounds are copied rounds, which device releases
+ * cannot fold: such a server builds no keyed queue (below) and folds with
+ * launches either way (config 1: 3.13-3.17 ms per round with DEVICE set,
+ * 3.1 with LAUNCH; 11.5-13.3 ms before it skipped the queue — DESIGN.md §9
+ * round 5).  And DEVICE adds a contract the reference does not have: every
+ * key completes one round per epoch, or the epoch fails with
+ * BYTEPS_REDUCE_ETIMEOUT (below).  Device releases pay when the pushes land in
+ * HBM (byteps_server_push_ready after an RDMA write into GPU memory): config
+ * 3's keys from one receive thread at 0.49 of the HBM roofline instead of
  * 0.21-0.28 (the bench line's server_cfg3) — set BPSR_SERVER_RELEASE=device
  * (or release = DEVICE) for that shape. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
@@ -98,7 +100,10 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
 /* Device releases (release = DEVICE or BPSR_SERVER_RELEASE=device; sync mode,
  * fused policy, the default engine, num_workers <= 16 — otherwise the server
  * folds with launches): at the first round completion after the
- * init round the server builds ONE keyed block queue over every declared key
+ * init round — when that round came through the slots (push_ready, or
+ * blocking pushes of device data); a first round of copied pushes (host data,
+ * non-blocking pushes) leaves the server on launches for good — the server
+ * builds ONE keyed block queue over every declared key
  * of that key's dtype (each key's receive slots in worker order and its
  * store).  From then on a round's last arrival issues no launch: it stores
  * the key's arrival order and release word from the host when the pushes are

@@ -42,11 +42,18 @@ void build_kq(byteps_server* s, int dtype) {
 }
 
 // Is this finished round of `ks` device-released?  Caller holds ks->mu.
+// The first round finished after the init round decides: pushes already in
+// their slots (push_ready, or device data the copy service landed) build the
+// keyed queue; a round the lanes copied (host data: the ps-lite shape) means
+// the pushes land in host memory, where device releases only add the
+// consumer (config 1: 11.5-13.3 ms per round against 3.1 with launches,
+// r05s55), so the server keeps launches for good.
 bool keyed_member(byteps_server* s, KeyState* ks) {
   if (!s->dev_release || s->kq_off.load()) return false;
   std::lock_guard<std::mutex> g(s->kq_mu);
   if (!s->kq_tried) {
     s->kq_tried = true;
+    if (ks->round_copied) return false;  // no queue: launches from here on
     build_kq(s, ks->dtype);
   }
   return ks->kq_key.load() >= 0;

@@ -1929,28 +1929,77 @@ def test_order_after_orders_device_released_push_ready(port, monkeypatch):
     assert np.array_equal(got, want)
 
 
+def test_device_release_server_with_copied_rounds_keeps_launches(port, monkeypatch):
+    """Device releases on, but the first round after the init round is copied
+    (pushes from host memory, the ps-lite shape): the server builds no keyed
+    queue and folds every round with launches — no consumer waits beside the
+    lanes (config 1 took 4x longer with one, r05s55) — and the later
+    push_ready rounds stay on launches too; every pull exact."""
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    dt, N, n = DType.FLOAT32, 2, 70_001
+    srv = PSServer(N)
+    dev = torch.device("cuda:0")
+    out = np.zeros(n * 4, np.uint8)
+    for r in range(4):
+        for k in (1, 2):
+            if r < 2:                                        # init round + a copied round
+                ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, n, w, r, k), dt))
+                      for w in range(N)]
+                for t in ts:
+                    t.start()
+                for t in ts:
+                    t.join(timeout=60)
+            else:                                            # then push_ready rounds
+                for w in range(N):                           # (no consumer runs: a NULL-
+                    x = torch.from_numpy(data(dt, n, w, r, k)).to(dev)   # stream copy is fine)
+                    _ptr_copy(srv.recv_slot(k, w), x)
+                    torch.cuda.current_stream(dev).synchronize()
+                    srv.push_ready(k, w)
+        if r == 0:                                           # the init round has no pulls
+            continue
+        for k in (1, 2):
+            want = np.zeros(n * 4, np.uint8)
+            port.sum_n(want, [data(dt, n, w, r, k) for w in srv.key_info(k)[2]], n * 4, dt)
+            for w in range(N):
+                srv.pull(k, out)
+                assert np.array_equal(out, want), (r, k, w)
+    st = srv.stats()
+    srv.close()
+    assert st["consumer_launches"] == 0 and st["key_releases"] == 0
+
+
 def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     """The keyed queue's contract: every key completes one round per epoch.  A
     round in which one key is never pushed makes that epoch's consumer give up
     after BPSR_SERVER_RELEASE_TIMEOUT_S: the key released in it fails with
     ETIMEOUT (no stale data), the server turns device releases off, and the
-    late key's round then folds with a launch, exactly.  Rounds 0-1 are
-    copied pushes (host data): they fold with lane launches while the
-    consumer passes their keys."""
+    late key's round then folds with a launch, exactly.  Round 0 (init) is
+    copied pushes; round 1 is push_ready, so the first finished round builds
+    the keyed queue (a server whose first round is copied keeps launches:
+    test_device_release_server_with_copied_rounds_keeps_launches)."""
     from prophet_amd.reducer import ETIMEOUT, ReduceError
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
     monkeypatch.setenv("BPSR_SERVER_RELEASE_TIMEOUT_S", "0.5")
     dt, N, n = DType.FLOAT32, 2, 50_003
     srv = PSServer(N)
-    for r in range(2):                                   # init round + round 1, both keys
-        for k in (1, 2):                                 # (an init push waits for the others)
-            ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, n, w, r, k), dt))
-                  for w in range(N)]
-            for t in ts:
-                t.start()
-            for t in ts:
-                t.join(timeout=60)
+    for k in (1, 2):                                     # init round, both keys
+        ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, n, w, 0, k), dt))
+              for w in range(N)]                         # (an init push waits for the others)
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+    dev = torch.device("cuda:0")
+    for k in (1, 2):                                     # round 1: push_ready, both keys; every
+        for w in range(N):                               # slot written before the first release
+            x = torch.from_numpy(data(dt, n, w, 1, k)).to(dev)   # (the epoch's consumer then
+            _ptr_copy(srv.recv_slot(k, w), x)                   # runs; work on this NULL
+    torch.cuda.current_stream(dev).synchronize()                # stream would wait for it)
+    for k in (1, 2):
+        for w in range(N):
+            srv.push_ready(k, w)
     out = np.zeros(n * 4, np.uint8)
     for k in (1, 2):
         for w in range(N):
@@ -1959,7 +2008,6 @@ def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
     # released from the host (push_ready) — a device-released round; key 2
     # never comes.  (Copied pushes would fold with a lane launch and pass the
     # consumer with a skip word, so they could not show the timeout.)
-    dev = torch.device("cuda:0")
     for w in range(N):
         x = torch.from_numpy(data(dt, n, w, 2, 1)).to(dev)
         _ptr_copy(srv.recv_slot(1, w), x)
