@@ -194,9 +194,25 @@ int byteps_reduce_plan_destroy(byteps_reduce_plan* plan);
  * it, e.g. on an event recorded there); launching on any other stream forks
  * onto it and joins back
  * (two events — ~0.14 ms per iteration at config 3, so launch on the consumer
- * stream when iterations run back to back).  A launch inside a hipGraph
+ * stream when iterations run back to back).  The join-back is queued on the
+ * launch stream once EVERY block of the launch's epoch has been released (by
+ * the release call that completes the epoch, stream or host), or at
+ * byteps_reduce_blockq_join / status, whichever comes first (round 6): a wait
+ * for the consumer queued at launch time would sit in the launch stream's
+ * in-order hardware queue, which HIP shares with other streams, ahead of any
+ * release (or the copies before it) queued later on one of them — the
+ * consumer would wait for a release that waits for the consumer, until the
+ * timeout (false dependencies).  So work queued on the launch
+ * stream after the launch is ordered after the fold only once the epoch is
+ * fully released; call join before that if it must be.  The launch stream
+ * must outlive that point.  A launch inside a hipGraph
  * capture stays on the capturing stream (pre-released by rule).  Releases on
  * the launch stream itself, before the launch, are always safe.
+ * The consumer queues are blocking streams (HIP gives an explicit CU mask only
+ * to those), so work on the legacy NULL stream waits for a running consumer —
+ * and holds back every stream sharing the NULL stream's hardware queue: do not
+ * queue work on the NULL stream between a live launch and its last release
+ * (torch: make the current stream a non-default one).
  * Likewise on the host: between a live launch and its last release, the
  * thread that issues the releases must not block on the device
  * (hipDeviceSynchronize, hipFree — including byteps_reduce_blockq_destroy or

@@ -680,6 +680,21 @@ struct byteps_reduce_blockq {
   // alternate between the device's two consumer queues and do not join back.
   bool overlap = false;
   hipEvent_t fork_ev = nullptr;
+  // Deferred join-back (round 6, DESIGN.md §4.4 "false dependencies"): a
+  // launch forked from the caller's stream `s` (no overlap) makes `s` wait
+  // for its consumer only once every block of its epoch has been released
+  // (or at join / status).  A wait queued on `s` at launch time sits in the
+  // in-order hardware queue `s` shares with other streams, and a release (or
+  // the copies before it) queued on one of those streams would then wait
+  // behind the very consumer it releases: a stall until the timeout (r05s76,
+  // measured r06s02).  Each such launch completes an event of its own.
+  struct PendingJoin {
+    hipStream_t s;
+    hipEvent_t ev;
+    uint32_t epoch;
+  };
+  std::vector<PendingJoin> pend_join;  // under mu
+  std::vector<hipEvent_t> join_evs;    // free events (under mu)
   // Host releases (byteps_reduce_blockq_host_releases): pinned, coherent
   // words the host writes and the launch's helper workgroup forwards.
   uint32_t* hflags = nullptr;
@@ -700,17 +715,19 @@ struct byteps_reduce_blockq {
   uint32_t* khdone_dev = nullptr;
 };
 
-// Per device, created on first use, never destroyed: two consumer queues
+// Per device, created on first use, never destroyed: three consumer queues
 // (all-CU-masked streams, each a hardware queue of its own; queue 0 is
 // byteps_reduce_blockq_stream, where every launch without overlap runs, in
-// launch order) and the dispatch sequence every block-queue launch outside a
+// launch order; queue 1 the overlapped launches' second queue; queue 2 the
+// PS server's keyed consumers, so that a block-queue join never waits for a
+// keyed epoch that waits for host releases) and the dispatch sequence every block-queue launch outside a
 // capture takes part in: sequence numbers, the
 // started-workgroup counter and its target, the signal word, the stream of the
 // latest launch, and per stream the completion event of its latest launch
 // (what byteps_reduce_blockq_join waits for).
 struct ConsumerDev {
   std::mutex mu;                        // sequence order = enqueue order
-  hipStream_t q[2] = {nullptr, nullptr};
+  hipStream_t q[3] = {nullptr, nullptr, nullptr};
   unsigned long long* started = nullptr;  // started counter (device, a line of its own)
   unsigned long long target = 0;        // counted workgroups of every launch so far
   hipStream_t last = nullptr;           // stream of the latest launch
@@ -725,8 +742,8 @@ struct ConsumerDev {
 static std::mutex g_consumer_mu;
 static ConsumerDev g_cdev[64];
 
-// which: 0 (every launch without overlap) or 1 (made at the first
-// overlapped launch: a queue that is never used is not made).
+// which: 0 (every launch without overlap), 1 (made at the first overlapped
+// launch: a queue that is never used is not made) or 2 (keyed consumers).
 static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
   if (device < 0 || device >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> g(g_consumer_mu);
@@ -783,6 +800,21 @@ static hipError_t seq_tail(ConsumerDev& D, hipStream_t s, ConsumerDev::Tail** ou
       *out = &t;
       return hipSuccess;
     }
+  // Callers' streams (launches without a queue of their own) come and go:
+  // drop entries whose launch has completed and that need no record, so the
+  // list stays bounded by the launches still in flight.
+  if (D.tails.size() >= 16) {
+    size_t k = 0;
+    for (auto& t : D.tails) {
+      const bool own = t.stream == D.q[0] || t.stream == D.q[1] || t.stream == D.q[2];
+      if (!own && !t.record && hipEventQuery(t.ev) == hipSuccess) {
+        (void)hipEventDestroy(t.ev);
+        continue;
+      }
+      D.tails[k++] = t;
+    }
+    D.tails.resize(k);
+  }
   hipEvent_t e = nullptr;
   const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
   if (r != hipSuccess) return r;
@@ -812,7 +844,37 @@ static void seq_commit(ConsumerDev& D, const BlockqLaunch& Q, hipStream_t ls) {
   D.any = true;
 }
 
+// q->mu held.  Every block released for `epoch` (host call order).
+static bool epoch_released(const byteps_reduce_blockq* q, uint32_t epoch) {
+  for (uint32_t r : q->rel_epoch)
+    if (!epoch_reached(r, epoch)) return false;
+  return true;
+}
+
+// q->mu held.  Issue the deferred join-backs whose epochs are fully released
+// (all of them when `all`): the caller's stream waits for that launch.
+static hipError_t flush_joins(byteps_reduce_blockq* q, bool all) {
+  hipError_t e = hipSuccess;
+  size_t k = 0;
+  for (auto& p : q->pend_join) {
+    if (e == hipSuccess && (all || epoch_released(q, p.epoch))) {
+      e = hipStreamWaitEvent(p.s, p.ev, 0);
+      q->join_evs.push_back(p.ev);  // the wait holds the event's state at this call
+      continue;
+    }
+    q->pend_join[k++] = p;
+  }
+  q->pend_join.resize(k);
+  return e;
+}
+
 static void blockq_free(byteps_reduce_blockq* q) {
+  // a launch still waiting for releases ends at its timeout at the latest
+  for (auto& p : q->pend_join) {
+    (void)hipEventSynchronize(p.ev);
+    (void)hipEventDestroy(p.ev);
+  }
+  for (hipEvent_t ev : q->join_evs) (void)hipEventDestroy(ev);
   if (q->kwords) (void)hipFree(q->kwords);
   if (q->khwords) (void)hipHostFree(q->khwords);
   if (q->hctl) (void)hipHostFree(q->hctl);
@@ -1011,17 +1073,34 @@ int byteps_reduce_blockq_launch(byteps_reduce_blockq* q, void* stream) {
   // next byteps_reduce_blockq_join records it on the consumer queue (a stop
   // event on every overlapped launch cost 2.4 µs per config-3 iteration:
   // 0.0744 vs 0.0720 ms, r05s23).
+  // A launch forked from `s` without overlap joins back into `s` once its
+  // epoch is fully released (flush_joins), through a stop event of its own.
   ConsumerDev::Tail* tail = nullptr;
   if (e == hipSuccess) e = seq_tail(D, ls, &tail);
-  const bool stop = !q->own_queue || (!q->overlap && s != ls);
+  const bool join_back = q->own_queue && !q->overlap && s != ls;
+  hipEvent_t jev = nullptr;
+  if (e == hipSuccess && join_back) {
+    if (!q->join_evs.empty()) {
+      jev = q->join_evs.back();
+      q->join_evs.pop_back();
+    } else {
+      e = hipEventCreateWithFlags(&jev, hipEventDisableTiming);
+    }
+  }
   if (e == hipSuccess) {
-    Q.L.stop = stop ? tail->ev : nullptr;
+    const bool stop = !q->own_queue;
+    Q.L.stop = join_back ? jev : stop ? tail->ev : nullptr;
     tail->record = !stop;
   }
   if (e == hipSuccess) e = seq_prepare(D, q->device, Q, ls, 4 * Q.timeout_ticks);
   if (e == hipSuccess) e = launch_blockq(Q, q->ti.vpt, pol, lds, gated, q->dtype, q->mode, ls);
   if (e == hipSuccess) seq_commit(D, Q, ls);
-  if (e == hipSuccess && q->own_queue && !q->overlap && s != ls) e = hipStreamWaitEvent(s, tail->ev, 0);
+  if (e == hipSuccess && join_back) {
+    q->pend_join.push_back({s, jev, epoch});
+    e = flush_joins(q, false);  // a pre-released epoch joins at once
+  } else if (jev) {
+    q->join_evs.push_back(jev);
+  }
   return e == hipSuccess ? BYTEPS_REDUCE_OK : hip_fail(e, "block queue kernel launch");
 }
 
@@ -1044,6 +1123,8 @@ int byteps_reduce_blockq_join(byteps_reduce_blockq* q, void* stream) {
   if (!q) return fail(BYTEPS_REDUCE_EARGS, "null block queue");
   if (q->device < 0 || q->device >= 64) return fail(BYTEPS_REDUCE_EARGS, "device %d", q->device);
   hipStream_t s = to_stream(stream);
+  std::lock_guard<std::mutex> g(q->mu);  // (q->mu before D.mu, as in launch)
+  if (const hipError_t e = flush_joins(q, true)) return hip_fail(e, "block queue join-back");
   ConsumerDev& D = g_cdev[q->device];
   std::lock_guard<std::mutex> dg(D.mu);
   for (auto& t : D.tails) {
@@ -1081,6 +1162,10 @@ int byteps_reduce_blockq_release_range(byteps_reduce_blockq* q, int first, int c
     if (e != hipSuccess) return hip_fail(e, "block release");
     for (int k = b; k < run; ++k) q->rel_epoch[k] = ep;
     b = run;
+  }
+  if (!q->pend_join.empty()) {
+    const hipError_t e = flush_joins(q, false);
+    if (e != hipSuccess) return hip_fail(e, "block queue join-back");
   }
   return BYTEPS_REDUCE_OK;
 }
@@ -1131,6 +1216,10 @@ int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int co
     q->rel_epoch[b] = ep;
     __atomic_store_n(q->hflags + b, ep, __ATOMIC_RELEASE);
   }
+  if (!q->pend_join.empty()) {
+    const hipError_t e = flush_joins(q, false);
+    if (e != hipSuccess) return hip_fail(e, "block queue join-back");
+  }
   return BYTEPS_REDUCE_OK;
 }
 
@@ -1147,6 +1236,9 @@ int byteps_reduce_blockq_status(byteps_reduce_blockq* q, void* stream) {
   if (q->overlap) {  // launches do not join their stream: the status waits for all of them
     const int rc = byteps_reduce_blockq_join(q, stream);
     if (rc) return rc;
+  } else {           // deferred join-backs go out now (their launch streams wait)
+    std::lock_guard<std::mutex> g(q->mu);
+    if (const hipError_t e = flush_joins(q, true)) return hip_fail(e, "block queue join-back");
   }
   hipError_t e = hipMemcpyAsync(q->host_err, &q->ctl->err, sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, s);
@@ -1293,7 +1385,7 @@ int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double 
 int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, uint32_t* epoch) {
   std::lock_guard<std::mutex> g(q->mu);
   hipStream_t own = nullptr;
-  hipError_t e = consumer_stream(q->device, q->cus, &own);
+  hipError_t e = consumer_queue(q->device, q->cus, 2, &own);
   if (e != hipSuccess) return hip_fail(e, "consumer stream");
   const uint32_t ep = q->launch_epoch + 1;
   BlockqLaunch Q;

@@ -29,7 +29,10 @@
 // its caller already reuses).  For the same reason a give-up (a job not served
 // in kTimeoutMs) raises `stop` and waits for the running launch to end before
 // any caller learns that the service is off and copies the bytes another way:
-// the fetcher checks `stop` on every pass and moves nothing after it.
+// the fetcher checks `stop` on every pass and moves nothing after it.  That
+// wait is bounded (kStopWaitMs): a launch that has not ended by then may be
+// wedged and may still write a job's buffer, so the service is then marked
+// wedged — every caller gets a hard error and none falls back to another copy.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -60,6 +63,7 @@ constexpr int kIdleUs = 500, kMaxUs = BPSR_SVC_MAX_US;
 constexpr int kCheckUs = 200;                // a waiter's liveness check period
 constexpr int64_t kExitPollNs = 2000;        // ... while the launch is exiting
 constexpr int kTimeoutMs = 10000;            // a job's give-up (reported, not retried)
+constexpr int kStopWaitMs = 1000;            // a give-up's wait for the launch to end
 }  // namespace
 
 struct CopyService {
@@ -84,13 +88,31 @@ struct CopyService {
   std::atomic<bool> running{false};     // written under mu
   std::atomic<uint32_t> gen{0};         // the current launch's number (written under mu)
   std::atomic<bool> broken{false};      // a job timed out: the service is off for good
+  std::atomic<bool> wedged{false};      // ... and its launch did not end: no fallback either
   std::mutex mu;
   uint64_t scan_from = 0;               // under mu: every job below is done
   std::atomic<uint64_t> launches{0};
   int timeout_ms = kTimeoutMs;
+  int stop_wait_ms = kStopWaitMs;
 };
 
 namespace {
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Polls an event for at most `ms`: true once it has completed.
+bool event_done_within(hipEvent_t ev, int ms) {
+  const int64_t end = now_ns() + (int64_t)ms * 1000000;
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e == hipSuccess;
+    if (now_ns() > end) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
 
 // Live services.  A process that exits without destroying its server must not
 // leave a service kernel polling pinned host memory the runtime is about to
@@ -105,7 +127,7 @@ void stop_live_services() {
   if (!g_live) return;
   for (CopyService* c : *g_live) {
     if (c->stop) __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
-    if (c->running.load()) (void)hipEventSynchronize(c->ev);
+    if (c->running.load() && !c->wedged.load()) (void)event_done_within(c->ev, c->stop_wait_ms);
   }
 }
 
@@ -121,11 +143,6 @@ void register_live(CopyService* c) {
 void unregister_live(CopyService* c) {
   std::lock_guard<std::mutex> g(g_live_mu);
   if (g_live) g_live->erase(c);
-}
-
-int64_t now_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(
-             std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // A slot's done word only grows (its next job is posted after this one is
@@ -154,10 +171,18 @@ bool svc_alive(CopyService* c) {
 // ended (it moves and starts no job after seeing `stop`; copies already under
 // way finish first), and only then mark the service off, so that no caller
 // copies a job's bytes another way while the kernel may still write them.
+// The wait is bounded: a launch still running after stop_wait_ms is wedged —
+// a hard error for this and every later caller, with no fallback copy.
 int svc_give_up(CopyService* c, uint64_t j) {
   __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
   if (c->running.load()) {
-    (void)hipEventSynchronize(c->ev);
+    if (!event_done_within(c->ev, c->stop_wait_ms)) {
+      c->wedged.store(true);
+      return fail(BYTEPS_REDUCE_EHIP,
+                  "copy service: job %llu not served in %d ms, and the launch did not stop "
+                  "within %d ms (it may still write the job's buffer: no fallback copy)",
+                  (unsigned long long)j, c->timeout_ms, c->stop_wait_ms);
+    }
     c->running.store(false);
   }
   c->broken.store(true);
@@ -169,8 +194,11 @@ int svc_give_up(CopyService* c, uint64_t j) {
 // but not yet written count as not done: the fetcher waits for them).
 int svc_launch(CopyService* c) {
   if (c->running.load()) {  // let the old launch finish first (it is stopping)
-    hipError_t e = hipEventSynchronize(c->ev);
-    if (e != hipSuccess) return hip_fail(e, "copy service: old launch");
+    if (!event_done_within(c->ev, c->stop_wait_ms)) {
+      c->wedged.store(true);
+      return fail(BYTEPS_REDUCE_EHIP, "copy service: the exiting launch did not end within %d ms",
+                  c->stop_wait_ms);
+    }
     c->running.store(false);
   }
   const uint64_t posted = c->posted.load();
@@ -221,6 +249,7 @@ int copysvc_create(int device, CopyService** out) {
   if (const char* v = getenv("BPSR_COPYSVC_TEST_STALL_MS")) {
     c->timeout_ms = std::max(1, atoi(v));
     c->stall_ticks = (uint64_t)khz * 3 * c->timeout_ms;
+    c->stop_wait_ms = std::min(kStopWaitMs, 5 * c->timeout_ms);
   }
   c->max_ticks = (uint64_t)khz * kMaxUs / 1000;
   int prio_lo = 0, prio_hi = 0;
@@ -266,7 +295,9 @@ void copysvc_destroy(CopyService* c) {
   if (!c) return;
   unregister_live(c);
   if (c->stop) __atomic_store_n(c->stop, 1u, __ATOMIC_RELEASE);
-  if (c->running.load()) (void)hipEventSynchronize(c->ev);  // exits within one poll
+  // exits within one poll; a wedged launch may still touch the ring and the
+  // job buffers: leak what it can reach rather than free it under the kernel
+  if (c->running.load() && (c->wedged.load() || !event_done_within(c->ev, c->stop_wait_ms))) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->ev) (void)hipEventDestroy(c->ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -280,7 +311,8 @@ void copysvc_destroy(CopyService* c) {
 
 // With mu held, for a job j not done: keep a launch serving, or give up.
 int svc_check(CopyService* c, uint64_t j, int64_t now, int64_t t0) {
-  if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+  if (c->broken.load() || c->wedged.load())
+    return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
   if (!svc_alive(c)) {
     const int rc = svc_launch(c);
     if (rc) {
@@ -319,7 +351,8 @@ int copysvc_post(CopyService* c, void* dst, const void* src, size_t len, uint64_
   if (len == 0) return 0;
   if (((reinterpret_cast<uint64_t>(dst) + len) | (reinterpret_cast<uint64_t>(src) + len)) > kSvcMask)
     return fail(BYTEPS_REDUCE_EARGS, "copy service: address beyond 48 bits");
-  if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+  if (c->broken.load() || c->wedged.load())
+    return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
   const uint64_t n = (len + kChunk - 1) / kChunk;
   const uint64_t first = c->posted.fetch_add(n);
   const int64_t t0 = now_ns();
@@ -339,7 +372,8 @@ int copysvc_post(CopyService* c, void* dst, const void* src, size_t len, uint64_
   const int64_t prev = c->last_post_ns.exchange(t0);
   if (!c->running.load() || t0 - prev > kIdleUs * 500ll || svc_exiting(c)) {
     std::lock_guard<std::mutex> g(c->mu);
-    if (c->broken.load()) return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
+    if (c->broken.load() || c->wedged.load())
+      return fail(BYTEPS_REDUCE_EHIP, "copy service: off after a timeout");
     if (!svc_alive(c) && (rc = svc_launch(c))) {
       c->broken.store(true);
       return rc;
@@ -386,6 +420,8 @@ uint64_t copysvc_launches(CopyService* c) { return c ? c->launches.load() : 0; }
 uint64_t copysvc_posted(CopyService* c) { return c->posted.load(); }
 
 bool copysvc_broken(const CopyService* c) { return c->broken.load(); }
+
+bool copysvc_wedged(const CopyService* c) { return c->wedged.load(); }
 
 void copysvc_set_trace(CopyService* c, uint64_t* dev_trace) {
   std::lock_guard<std::mutex> g(c->mu);

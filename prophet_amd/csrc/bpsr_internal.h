@@ -382,6 +382,8 @@ uint64_t copysvc_launches(CopyService* svc);  // kernel launches so far (0 for n
 // A job timed out or a launch failed: the service takes no more jobs (its
 // callers use another copy path from then on).
 bool copysvc_broken(const CopyService* svc);
+// A give-up whose launch did not end in time: hard errors, no fallback copy.
+bool copysvc_wedged(const CopyService* svc);
 // Probes (tools/dbg/copysvc_probe.cpp): jobs posted so far; a device trace
 // buffer (kSvcRing * 4 words) used from the next launch on.
 uint64_t copysvc_posted(CopyService* svc);

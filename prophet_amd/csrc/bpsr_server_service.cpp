@@ -44,7 +44,7 @@ CopyService* service_get(byteps_server* s) {
   }
   // a service that gave up (a job not served in time) takes no more pulls:
   // they ride lane copies, as with BPSR_SERVER_PULL_SERVICE=0
-  return s->svc && !copysvc_broken(s->svc) ? s->svc : nullptr;
+  return s->svc && !copysvc_broken(s->svc) && !copysvc_wedged(s->svc) ? s->svc : nullptr;
 }
 bool on_this_device(const byteps_server* s, const void* p) {
   hipPointerAttribute_t a{};

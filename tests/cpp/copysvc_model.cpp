@@ -72,6 +72,7 @@ struct Launch {
 };
 std::atomic<int> g_live_launches{0}, g_max_live{0};
 std::atomic<uint64_t> g_late_copies{0};  // copies the model made after a stop was seen
+std::atomic<bool> g_wedge{false};        // copiers hang (a launch that does not end)
 int g_jitter_us = 20;
 
 uint64_t ld(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -138,6 +139,7 @@ void model_copiers(bpsr::SvcArgs a) {
         continue;
       }
       any = true;
+      while (g_wedge.load()) std::this_thread::sleep_for(std::chrono::microseconds(100));
       bool skip = j < a.check_below && ld(a.done + slot * bpsr::kDoneStride) >= j + 1;
       if (!skip && a.stall_ticks) {  // tests: hold the job, drop it on a stop
         const uint64_t t0 = now_ticks();
@@ -358,6 +360,38 @@ void give_up() {
   bpsr::copysvc_destroy(svc);
 }
 
+// The give-up when the launch does not end (a wedged kernel): the copy
+// returns a hard error once the bounded wait for the launch has passed —
+// not ETIMEOUT, and the service reports wedged rather than broken, so no
+// caller copies the bytes another way while the kernel may still write them;
+// later posts fail at once.  Then the launch is let go and ends.
+void wedged_give_up() {
+  setenv("BPSR_COPYSVC_TEST_STALL_MS", "40", 1);
+  bpsr::CopyService* svc = nullptr;
+  CHECK(bpsr::copysvc_create(0, &svc) == 0);
+  unsetenv("BPSR_COPYSVC_TEST_STALL_MS");
+  if (!svc) return;
+  std::vector<unsigned char> src(5000, 7), dst(5000, 0);
+  g_wedge.store(true);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = bpsr::copysvc_copy(svc, dst.data(), src.data(), src.size());
+  const double ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  CHECK(rc == BYTEPS_REDUCE_EHIP);
+  CHECK(ms >= 40 + 200 && ms < 40 + 200 + 150);  // the give-up, then the bounded wait (5 x 40 ms)
+  CHECK(bpsr::copysvc_wedged(svc));
+  CHECK(!bpsr::copysvc_broken(svc));  // no fallback copy
+  CHECK(g_live_launches.load() == 1);
+  CHECK(bpsr::copysvc_copy(svc, dst.data(), src.data(), 16) == BYTEPS_REDUCE_EHIP);
+  g_wedge.store(false);
+  for (int i = 0; i < 200 && g_live_launches.load(); ++i)
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  CHECK(g_live_launches.load() == 0);
+  CHECK(g_late_copies.load() == 0);
+  printf("wedged_give_up ms=%.1f\n", ms);
+  bpsr::copysvc_destroy(svc);  // leaks the wedged service's buffers by design
+}
+
 }  // namespace
 
 int main() {
@@ -367,6 +401,7 @@ int main() {
   racing_posters(4, 300, 0);
   g_jitter_us = 20;
   give_up();
+  wedged_give_up();
   printf("fails=%d\n", g_fails.load());
   return g_fails.load() ? 1 : 0;
 }

@@ -7,6 +7,8 @@ released (all up front, one by one from another stream after their pushes
 land by DMA, from a captured hipGraph), and a launch whose releases never come
 stops by itself and reports BYTEPS_REDUCE_ETIMEOUT.
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -639,3 +641,30 @@ def test_overlap_rules(red, dev):
     for g, w in zip(got, wants):
         assert np.array_equal(g.cpu().numpy(), w)
     q.close()
+
+
+def test_releases_on_streams_sharing_the_launch_streams_hardware_queue():
+    """Round 6 (false dependencies): with GPU_MAX_HW_QUEUES=1
+    every normal-priority stream — the NULL stream included — shares ONE
+    in-order hardware queue, so a wait for the consumer queued on the launch
+    stream at launch time would sit ahead of every release (and of the copies
+    before it) on any other stream: the r05s76 stall, made deterministic.  A
+    launch now joins back only once its epoch is fully released: each case
+    (a caller-stream launch with copies and a release on another stream, the
+    r05s76 NULL-stream test with mixed stream and host releases, the PUSH loop
+    on caller streams) completes exactly, well inside the 2-s consumer timeout.
+    Runs in a subprocess: the queue count is read when HIP starts."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="1")
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "blockq_shared_hwq_case.py")],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert [x["case"] for x in lines] == ["caller_stream", "null_mixed", "push_loop"], r.stdout
+    for x in lines:
+        assert x["ok"], x
+        assert x["s"] < 1.5, x          # no consumer timeout on the way
+    assert r.stdout.strip().endswith("ok"), r.stdout + r.stderr

@@ -4,7 +4,9 @@ age exits, the `exited` word, jobs stranded by an exit) and its give-up,
 against a CPU model of the service kernel's protocol behind a fake HIP runtime
 (tests/cpp/copysvc_model.cpp) — racing posters with every byte checked, never
 two launches at once, and a give-up that returns only after the launch ended
-with no copy after the stop.  Once plain and once under ThreadSanitizer.
+with no copy after the stop, and a give-up whose launch never ends that returns
+a hard error after a bounded wait (no unbounded wait under the
+service lock, no fallback copy while the kernel may still write).  Once plain and once under ThreadSanitizer.
 (VERDICT round 4 asked for this in place of re-running the r04s14 hang on the
 GPU: profiles/README.md records that hang.)"""
 import os
@@ -31,3 +33,4 @@ def test_copy_service_host_logic_against_kernel_model(tmp_path, san):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "fails=0" in r.stdout
     assert "give_up ms=" in r.stdout
+    assert "wedged_give_up ms=" in r.stdout   # a launch that never ends: bounded, no fallback
