@@ -1216,9 +1216,16 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
         hq.host_releases(True)
         hqueues.append(hq)
     # the library's consumer stream: a hardware queue of its own, so a release
-    # never waits behind the spinning consumer (include/bpsr/reduce.h)
+    # never waits behind the spinning consumer (include/bpsr/reduce.h); the
+    # stream releases on the library's release stream, a queue on a compute
+    # pipe no consumer queue uses (DESIGN.md §4.4 "pipes": a torch stream
+    # that lands on a running consumer's pipe runs its release kernels ~2x
+    # slower).  BPSR_BENCH_REL_STREAM=torch: a torch stream (measurement only)
     live_s = queues[0].stream()
-    rel_s = torch.cuda.Stream(device=dev)
+    if os.environ.get("BPSR_BENCH_REL_STREAM") == "torch":
+        rel_s = torch.cuda.Stream(device=dev)
+    else:
+        rel_s = queues[0].release_stream()
     overlap_on = [False]
     nb = len(by_block)
     # one scheduler + inline PUSH loop per input set (a loop drives one queue);
@@ -1276,7 +1283,9 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                         "(Prophet scheduler, stream-ordered release kernels, the release "
                         "groups ready together as one kernel); live_per_block = one "
                         "release kernel per block; receive slots in one skewed HBM arena"),
-           "alg_bytes_per_iter": alg, "iters": iters, "reps": reps}
+           "alg_bytes_per_iter": alg, "iters": iters, "reps": reps,
+           "release_stream": ("torch" if os.environ.get("BPSR_BENCH_REL_STREAM") == "torch"
+                              else "library (byteps_reduce_blockq_release_stream)")}
     res["overlap"] = ("consecutive launches overlap (byteps_reduce_blockq_overlap: the two "
                       "consumer queues alternate, a launch dispatched once every workgroup of "
                       "the previous one has started); *_no_overlap: one stream-ordered queue")
@@ -1334,6 +1343,7 @@ def cfg3_leg(dev, red, iters: int = 200, reps: int = 5, sets: int = 3, N: int = 
                 ref.add_(x.view(torch.float16))
             ok = ok and bool(torch.equal(ref.view(torch.uint8), out))
     res["exact_vs_torch_fold"] = ok
+    res["hsa_queue_ids"] = queues[0].queue_ids()   # consumer queues 0-2, release queue
     for lp in loops:
         lp.close()
     for q in queues + hqueues:
@@ -1666,6 +1676,16 @@ def main(argv=None):
                     fold=None if cuda else _torch_fold, comm=comm)
             except Exception as e:  # report, never hide
                 line["local_reduce"] = {"error": repr(e)}
+        # Config 3 before the host-resident server: the order that ran the
+        # server at 0.65 of its link and config 3's per-block releases 30x
+        # slower until round 6 placed the library's queues one per compute pipe
+        # (DESIGN.md §4.4 "pipes"); no leg order is needed any more.
+        if world == 1 and cuda and not args.no_cfg3:
+            leg("cfg3_blockq")
+            try:
+                line["cfg3_blockq"] = cfg3_leg(dev, red)
+            except Exception as e:  # report, never hide
+                line["cfg3_blockq"] = {"error": repr(e)}
         link = None
         if cuda and not (args.no_server and args.no_e2e):
             leg("pcie")
@@ -1683,19 +1703,6 @@ def main(argv=None):
                 line["server_cfg1"] = {"error": repr(e)}
         elif not args.no_server:
             line["server_cfg1"] = {"skipped": "the PS server needs a GPU (--device cpu)"}
-        # Hardware-queue placement (DESIGN.md §4.4 "placement"): the order in
-        # which legs make their streams decides which queues share hardware,
-        # and a stream that lands badly is slow: the host-resident server made
-        # after the consumer queues exist (4.3 vs 3.1 ms per round, r05s42),
-        # config 3's stream releases made after other legs churned streams
-        # (per-block releases 0.081 -> 2.4 ms per iteration, r05s33/s40).
-        # Config 3 right after the server measured clean for both (r05s42).
-        if world == 1 and cuda and not args.no_cfg3:
-            leg("cfg3_blockq")
-            try:
-                line["cfg3_blockq"] = cfg3_leg(dev, red)
-            except Exception as e:  # report, never hide
-                line["cfg3_blockq"] = {"error": repr(e)}
         if cuda and not args.no_e2e:
             leg("e2e_cfg5")
             try:

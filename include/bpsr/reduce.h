@@ -55,8 +55,9 @@ extern "C" {
 #pragma GCC visibility push(default)
 
 /* 3: byteps_server_config.engine_blocking; bpsr/shard.h
- * 4: byteps_server_config.release; byteps_shard_rccl_version */
-#define BYTEPS_REDUCE_ABI_VERSION 4
+ * 4: byteps_server_config.release; byteps_shard_rccl_version
+ * 5: byteps_server_create_sized (a caller states its config's size) */
+#define BYTEPS_REDUCE_ABI_VERSION 5
 
 /* Data type ids: byteps/common/common.h:52-65 (mshadow order), plus bf16 as a
  * build extension (the reference has none). */
@@ -249,6 +250,20 @@ int byteps_reduce_blockq_host_releases(byteps_reduce_blockq* q, int on);
 int byteps_reduce_blockq_release_host(byteps_reduce_blockq* q, int first, int count);
 /* The device's consumer stream (see above); owned by the library. */
 int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream);
+/* The device's release stream (round 6): a hardware queue of its own, owned
+ * by the library, on a different compute pipe than every consumer queue.  A
+ * queue that shares a pipe with a running consumer is served ~2x slower (its
+ * release kernels took 43 us median instead of 5 beside config 3's consumer,
+ * DESIGN.md §4.4 "pipes"), and which pipe a caller's stream lands on is the
+ * runtime's choice; the library places its own queues by their HSA ids.
+ * Queue a block's pushes (e.g. its H2D copies) and its stream release here,
+ * or fork here with an event.  Like the consumer queues it is a blocking
+ * stream (see above: no NULL-stream work between a launch and its last
+ * release). */
+int byteps_reduce_blockq_release_stream(byteps_reduce_blockq* q, void** stream);
+/* Diagnostics: the HSA queue ids of the device's consumer queues 0-2 (0 for one
+ * not made yet) and of its release queue; returns 4 (needs cap >= 4). */
+int byteps_reduce_blockq_queue_ids(byteps_reduce_blockq* q, uint64_t* ids, int cap);
 /* Overlap (on = 1; dispatch-ordered consumer only, EARGS otherwise):
  * consecutive launches may run at once, so one iteration's first blocks fold
  * while the previous one's last tiles drain.  A launch goes to whichever of

@@ -134,6 +134,15 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * (it waits for every blocking stream, the consumer's included) — work on
  * non-blocking streams, and stream or event syncs, are fine. */
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
+/* The same, for a caller that states the size of its config: every version of
+ * byteps_server_config is a prefix of the next (fields are only appended), so
+ * cfg_size picks the version — 28 bytes (ABI 3: up to engine_blocking; release
+ * is LAUNCH) or sizeof(byteps_server_config) (ABI 4 on); any other size is
+ * BYTEPS_REDUCE_EARGS instead of fields read past the caller's struct.
+ * byteps_server_create reads the whole current struct; a binding built
+ * against an older header should call this with its own sizeof. */
+int byteps_server_create_sized(const byteps_server_config* cfg, size_t cfg_size,
+                               byteps_server** out);
 int byteps_server_destroy(byteps_server* s);
 
 /* Optional: allocate a key's slots and store before its first push. */

@@ -728,6 +728,16 @@ struct byteps_reduce_blockq {
 struct ConsumerDev {
   std::mutex mu;                        // sequence order = enqueue order
   hipStream_t q[3] = {nullptr, nullptr, nullptr};
+  // Placement (round 6, DESIGN.md §4.4 "pipes"): the HSA ids of the consumer
+  // queues and of the release queue (byteps_reduce_blockq_release_stream),
+  // and queues made while placing them that did not fit (kept, idle: a
+  // destroyed queue would reshuffle the hardware's queue map).
+  uint64_t qid[3] = {0, 0, 0};
+  hipStream_t rq = nullptr;
+  uint64_t rqid = 0;
+  std::vector<std::pair<hipStream_t, uint64_t>> spare;
+  uint64_t* idw = nullptr;              // pinned word read_queue_id writes (host view)
+  uint64_t* idw_dev = nullptr;          // ... its device view
   unsigned long long* started = nullptr;  // started counter (device, a line of its own)
   unsigned long long target = 0;        // counted workgroups of every launch so far
   hipStream_t last = nullptr;           // stream of the latest launch
@@ -742,27 +752,119 @@ struct ConsumerDev {
 static std::mutex g_consumer_mu;
 static ConsumerDev g_cdev[64];
 
-// which: 0 (every launch without overlap), 1 (made at the first overlapped
-// launch: a queue that is never used is not made) or 2 (keyed consumers).
-static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
+// Queue placement (DESIGN.md §4.4 "pipes", round 6).  The hardware serves
+// its queues through 4 compute pipes, and queue ids map to pipes as id mod 4
+// in every measurement (profiles/r06s01, r06s02, r06s05, r06s07).  A queue on
+// the same pipe as a running consumer answers ~2x slower (43 us median
+// release kernels instead of 5: the r05s34 segment); the two overlapping
+// consumer queues need pipes of their own (on one pipe, overlapped config 3
+// fell from 0.80 to 0.74-0.75, r06s07); and the runtime's own normal-priority
+// queues serve the server's lanes best one per pipe (the host-resident
+// server ran 4.2 ms rounds instead of 3.1 when the library's queues had
+// pushed two of them onto one pipe, r06s08-s09).  So the library makes its
+// four queues together, one per pipe: consumer queues 0 and 1, the keyed
+// consumers' queue 2 and the release queue — its releases never share a pipe
+// with a block-queue consumer, and queues made later keep the runtime's
+// phase.  If another thread made a queue in between (ids not consecutive),
+// the set is completed queue by queue; a queue that does not fit is kept
+// idle for a later placement (a destroyed one could reshuffle the hardware's
+// queue map).
+constexpr uint64_t kPipes = 4;
+
+// g_consumer_mu held, device current.  A new all-CU-masked stream (a hardware
+// queue of its own) and the HSA id of its queue.
+static hipError_t new_cu_queue(ConsumerDev& D, int cus, hipStream_t* out, uint64_t* id) {
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+  for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+  hipError_t e = hipSuccess;
+  if (!D.idw) {
+    e = hipHostMalloc(reinterpret_cast<void**>(&D.idw), 64,
+                      hipHostMallocCoherent | hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&D.idw_dev), D.idw, 0);
+    if (e != hipSuccess) return e;
+  }
+  e = hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+  if (e == hipSuccess) e = read_queue_id(*out, D.idw_dev);
+  if (e == hipSuccess) *id = __atomic_load_n(D.idw, __ATOMIC_ACQUIRE);
+  return e;
+}
+
+// g_consumer_mu held, device current.  A queue whose id satisfies `fits`:
+// an idle spare, or a new one (at most kPipes + 1 tries; the last one made
+// is taken if none fits, i.e. the id-to-pipe model did not hold).
+extern "C++" template <class Fits>
+static hipError_t placed_queue(ConsumerDev& D, int cus, Fits fits, hipStream_t* out, uint64_t* id) {
+  for (size_t i = 0; i < D.spare.size(); ++i)
+    if (fits(D.spare[i].second)) {
+      *out = D.spare[i].first;
+      *id = D.spare[i].second;
+      D.spare.erase(D.spare.begin() + (long)i);
+      return hipSuccess;
+    }
+  for (uint64_t t = 0;; ++t) {
+    hipStream_t s = nullptr;
+    uint64_t qid = 0;
+    const hipError_t e = new_cu_queue(D, cus, &s, &qid);
+    if (e != hipSuccess) return e;
+    if (fits(qid) || t == kPipes) {
+      *out = s;
+      *id = qid;
+      return hipSuccess;
+    }
+    D.spare.push_back({s, qid});
+  }
+}
+
+// The device's four library queues, made together on first use (above):
+// slots 0-2 the consumer queues, slot 3 the release queue.
+static hipError_t queue_set(int device, int cus, ConsumerDev** out) {
   if (device < 0 || device >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> g(g_consumer_mu);
-  hipStream_t& slot = g_cdev[device].q[which];
-  if (!slot) {
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-    for (int c = 0; c < cus; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    if (cur != device) (void)hipSetDevice(device);
-    hipError_t e = hipExtStreamCreateWithCUMask(&slot, (uint32_t)mask.size(), mask.data());
-    if (cur != device && cur >= 0) (void)hipSetDevice(cur);
-    if (e != hipSuccess) {
-      slot = nullptr;
-      return e;
-    }
+  ConsumerDev& D = g_cdev[device];
+  *out = &D;
+  if (D.rq) return hipSuccess;
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (cur != device) (void)hipSetDevice(device);
+  hipStream_t* slot[4] = {&D.q[0], &D.q[1], &D.q[2], &D.rq};
+  uint64_t* sid[4] = {&D.qid[0], &D.qid[1], &D.qid[2], &D.rqid};
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < 4 && e == hipSuccess; ++k) e = new_cu_queue(D, cus, slot[k], sid[k]);
+  // any queue whose pipe an earlier one of the set has: re-placed
+  for (int k = 1; k < 4 && e == hipSuccess; ++k) {
+    auto taken = [&](uint64_t id) {
+      for (int j = 0; j < k; ++j)
+        if (*sid[j] % kPipes == id % kPipes) return true;
+      return false;
+    };
+    if (!taken(*sid[k])) continue;
+    D.spare.push_back({*slot[k], *sid[k]});
+    e = placed_queue(D, cus, [&](uint64_t id) { return !taken(id); }, slot[k], sid[k]);
   }
-  *out = slot;
+  if (cur != device && cur >= 0) (void)hipSetDevice(cur);
+  if (e != hipSuccess) {
+    for (int k = 0; k < 4; ++k) *slot[k] = nullptr;
+    return e;
+  }
   return hipSuccess;
+}
+
+// which: 0 (every launch without overlap), 1 (the overlapped launches'
+// second queue) or 2 (keyed consumers).
+static hipError_t consumer_queue(int device, int cus, int which, hipStream_t* out) {
+  ConsumerDev* D = nullptr;
+  const hipError_t e = queue_set(device, cus, &D);
+  if (e == hipSuccess) *out = D->q[which];
+  return e;
+}
+
+// The device's release queue: a hardware queue on a pipe no consumer queue
+// uses.
+static hipError_t release_queue(int device, int cus, hipStream_t* out) {
+  ConsumerDev* D = nullptr;
+  const hipError_t e = queue_set(device, cus, &D);
+  if (e == hipSuccess) *out = D->rq;
+  return e;
 }
 
 static hipError_t consumer_stream(int device, int cus, hipStream_t* out) {
@@ -1267,6 +1369,25 @@ int byteps_reduce_blockq_stream(byteps_reduce_blockq* q, void** stream) {
   if (e != hipSuccess) return hip_fail(e, "consumer stream");
   *stream = reinterpret_cast<void*>(s);
   return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_release_stream(byteps_reduce_blockq* q, void** stream) {
+  if (!q || !stream) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  hipStream_t s = nullptr;
+  hipError_t e = release_queue(q->device, q->cus, &s);
+  if (e != hipSuccess) return hip_fail(e, "release stream");
+  *stream = reinterpret_cast<void*>(s);
+  return BYTEPS_REDUCE_OK;
+}
+
+int byteps_reduce_blockq_queue_ids(byteps_reduce_blockq* q, uint64_t* ids, int cap) {
+  if (!q || !ids || cap < 4) return fail(BYTEPS_REDUCE_EARGS, "null argument or cap < 4");
+  if (q->device < 0 || q->device >= 64) return fail(BYTEPS_REDUCE_EARGS, "device %d", q->device);
+  std::lock_guard<std::mutex> g(g_consumer_mu);
+  const ConsumerDev& D = g_cdev[q->device];
+  for (int k = 0; k < 3; ++k) ids[k] = D.q[k] ? D.qid[k] : 0;
+  ids[3] = D.rq ? D.rqid : 0;
+  return 4;
 }
 
 int byteps_reduce_blockq_debug(byteps_reduce_blockq* q, uint32_t* out, int cap) {

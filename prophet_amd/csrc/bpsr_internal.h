@@ -291,6 +291,10 @@ hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count
 // null).
 hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,
                               uint64_t* word2_at, uint64_t word2, hipStream_t s);
+// The HSA id of the hardware queue behind stream `s` (a one-wave kernel reads
+// hsa_queue_t::id through its dispatch's queue pointer into `out`, pinned host
+// memory); synchronises `s`.  Queue placement.
+hipError_t read_queue_id(hipStream_t s, uint64_t* out);
 
 // Tile size actually used for a single fold: the tuned vpt, halved while the
 // launch would have fewer than kMinTiles tiles.

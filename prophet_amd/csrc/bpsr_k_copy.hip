@@ -139,6 +139,23 @@ hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,
   return hipGetLastError();
 }
 
+// The HSA id of the queue this dispatch came from: hsa_queue_t::id, at byte 32
+// of the queue (type, features, base_address, doorbell_signal, size,
+// reserved1, id — hsa.h), which the dispatch's queue pointer addresses.
+__global__ void queue_id_kernel(uint64_t* out) {
+  if (threadIdx.x == 0) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>((size_t)__builtin_amdgcn_queue_ptr());
+    __hip_atomic_store(out, q[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t read_queue_id(hipStream_t s, uint64_t* out) {
+  hipLaunchKernelGGL(queue_id_kernel, dim3(1), dim3(64), 0, s, out);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  return e;
+}
+
 // Dispatch-sequence gate: one wave, enqueued on a
 // consumer launch's stream ahead of its kernel, returns once the last
 // workgroups of the device's earlier launches have all started (the counter

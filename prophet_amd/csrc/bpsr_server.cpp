@@ -1188,6 +1188,21 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   return BYTEPS_REDUCE_OK;
 }
 
+int byteps_server_create_sized(const byteps_server_config* cfg, size_t cfg_size,
+                               byteps_server** out) {
+  if (!cfg || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
+  *out = nullptr;
+  constexpr size_t kV3 = offsetof(byteps_server_config, release);  // ABI 3: no release
+  if (cfg_size != kV3 && cfg_size != sizeof(byteps_server_config))
+    return fail(BYTEPS_REDUCE_EARGS,
+                "byteps_server_config of %zu bytes: not a known version (%zu: ABI 3, %zu: ABI 4-5)",
+                cfg_size, kV3, sizeof(byteps_server_config));
+  byteps_server_config c{};  // fields past the caller's version keep their defaults
+  c.release = BYTEPS_SERVER_RELEASE_LAUNCH;
+  std::memcpy(&c, cfg, cfg_size);
+  return byteps_server_create(&c, out);
+}
+
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out) {
   if (!cfg || !out) return fail(BYTEPS_REDUCE_EARGS, "null argument");
   *out = nullptr;
@@ -1535,6 +1550,11 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   if (rc) return rc;
   KeyState* ks = get_key(s, key, false);
   if (!ks || !ks->allocated) return fail(BYTEPS_REDUCE_EARGS, "key not initialised");
+  // the producers named with byteps_server_order_after, before the key lock:
+  // a round released from the host waits for them, and that wait must not
+  // hold the key's other workers and its completer (arrive()
+  // then finds the gate passed)
+  if ((rc = wait_order_gate(s))) return rc;
   std::unique_lock<std::mutex> lk(ks->mu);
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   std::vector<FoldJob> defer;

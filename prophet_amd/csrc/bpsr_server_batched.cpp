@@ -135,6 +135,7 @@ int byteps_server_push_ready_many(byteps_server* s, const uint64_t* keys, int n,
     return fail(BYTEPS_REDUCE_EARGS, "worker %d outside [0, %d)", worker, s->cfg.num_workers);
   int rc = set_device(s);
   if (rc) return rc;
+  if ((rc = wait_order_gate(s))) return rc;  // before any key lock (push_ready)
   std::vector<FoldJob> defer;
   for (int i = 0; i < n; ++i) {
     KeyState* ks = get_key(s, keys[i], false);

@@ -53,7 +53,8 @@ EXPORTS = (
     "byteps_reduce_blockq_debug", "byteps_reduce_blockq_stream",
     "byteps_reduce_blockq_release_range", "byteps_reduce_blockq_host_releases",
     "byteps_reduce_blockq_release_host", "byteps_reduce_blockq_overlap",
-    "byteps_reduce_blockq_join",
+    "byteps_reduce_blockq_join", "byteps_reduce_blockq_release_stream",
+    "byteps_reduce_blockq_queue_ids",
 )
 
 
@@ -113,6 +114,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     L.byteps_reduce_blockq_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
     L.byteps_reduce_blockq_overlap.argtypes = [_vp, _int]
     L.byteps_reduce_blockq_join.argtypes = [_vp, _vp]
+    L.byteps_reduce_blockq_release_stream.argtypes = [_vp, ctypes.POINTER(_vp)]
+    L.byteps_reduce_blockq_queue_ids.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), _int]
     _LIB = L
     return L
 
@@ -334,6 +337,24 @@ class BlockQueue:
         p = _vp()
         _check(self.lib.byteps_reduce_blockq_stream(self.handle, ctypes.byref(p)))
         return torch.cuda.ExternalStream(p.value)
+
+    def release_stream(self):
+        """The device's release stream (byteps_reduce_blockq_release_stream) as
+        a torch ExternalStream: a hardware queue on a compute pipe no consumer
+        queue uses — queue pushes and stream releases here."""
+        import torch
+        p = _vp()
+        _check(self.lib.byteps_reduce_blockq_release_stream(self.handle, ctypes.byref(p)))
+        return torch.cuda.ExternalStream(p.value)
+
+    def queue_ids(self) -> dict:
+        """HSA queue ids of the device's consumer queues and release queue
+        (byteps_reduce_blockq_queue_ids; 0 = not made yet)."""
+        ids = (ctypes.c_uint64 * 4)()
+        n = self.lib.byteps_reduce_blockq_queue_ids(self.handle, ids, 4)
+        if n < 0:
+            _check(n)
+        return {"consumer": [ids[0], ids[1], ids[2]], "release": ids[3]}
 
     def debug(self) -> dict:
         """byteps_reduce_blockq_debug (synchronises the device)."""

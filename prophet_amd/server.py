@@ -18,7 +18,8 @@ FUSED, INCREMENTAL = 0, 1
 HOST, DEVICE = 0, 1
 
 SERVER_EXPORTS = (
-    "byteps_server_config_from_env", "byteps_server_create", "byteps_server_destroy",
+    "byteps_server_config_from_env", "byteps_server_create", "byteps_server_create_sized",
+    "byteps_server_destroy",
     "byteps_server_init_key", "byteps_server_push", "byteps_server_recv_slot",
     "byteps_server_push_ready", "byteps_server_pull", "byteps_server_pull_host_view",
     "byteps_server_pull_async", "byteps_server_push_async", "byteps_server_key_info",

@@ -76,7 +76,7 @@ def test_library_build_applies_the_export_policy():
 
 def test_version_and_dtype_sizes():
     lib = reducer.load_library()
-    assert lib.byteps_reduce_version() == 4
+    assert lib.byteps_reduce_version() == 5
     for dt in ALL_DTYPES:
         assert lib.byteps_reduce_dtype_size(int(dt)) == elem_size(dt)
     assert lib.byteps_reduce_dtype_size(7) == reducer.EDTYPE
@@ -163,6 +163,17 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
     bad = server.ServerConfig(2, 4, 0, 0, 0, 0, 0, 7)  # no such release
     assert lib.byteps_server_create(ctypes.byref(bad), ctypes.byref(h)) == reducer.EARGS
+    # the sized entry point: a caller states its struct's size,
+    # and a size that is no known version is refused before any field is read
+    # past it; an ABI-3 struct (28 B, no release) is read as release = LAUNCH
+    lib.byteps_server_create_sized.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    assert ctypes.sizeof(server.ServerConfig) == 32
+    for size in (0, 20, 30, 36):
+        assert lib.byteps_server_create_sized(ctypes.byref(bad), size, ctypes.byref(h)) == reducer.EARGS
+        assert b"not a known version" in lib.byteps_reduce_last_error()
+    bad = server.ServerConfig(0, 4, 0, 0, 0, 0, 0, 7)   # v3 prefix still validated
+    assert lib.byteps_server_create_sized(ctypes.byref(bad), 28, ctypes.byref(h)) == reducer.EARGS
+    assert b"num_workers" in lib.byteps_reduce_last_error()
     assert lib.byteps_server_pull(None, 1, None, 0, 0) == reducer.EARGS
     assert lib.byteps_server_pull_host_view(None, 1, None, None) == reducer.EARGS
     assert lib.byteps_server_pull_async(None, 1, server.PULL_CB(), None) == reducer.EARGS

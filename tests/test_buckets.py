@@ -63,3 +63,19 @@ def test_cantor_command_roundtrip(req):
         cmd = cantor_command(req, int(dt))
         assert depair_command(cmd) == (req, int(dt))
     assert cantor_command(0, 0) == 0 and cantor_command(0, 2) == 5   # d(d+1)/2 + d
+
+
+def test_arena_skew_classes():
+    """prophet_amd/arena.py: the measured skew classes (profiles/
+    r06s09_s10_arena_skew.jsonl) — 16 KiB up to the headline's 256 MiB
+    bucket, 2 MiB + 16 KiB beyond it — and the stride they give."""
+    import torch
+    from prophet_amd.arena import DEFAULT_SKEW, LARGE_SKEW, BucketArena, default_skew
+    assert default_skew(256 << 20) == DEFAULT_SKEW == 16 << 10
+    assert default_skew((256 << 20) + (64 << 10)) == DEFAULT_SKEW
+    assert default_skew(553_430_176) == LARGE_SKEW == (2 << 20) + (16 << 10)
+    assert default_skew(1 << 30) == LARGE_SKEW
+    a = BucketArena(3, 5000, torch.device("cpu"))          # small: 4 KiB rounding
+    assert a.stride == 8192 + DEFAULT_SKEW
+    assert [s.numel() for s in a.slots()] == [5000] * 3
+    assert a.slot(2).data_ptr() - a.slot(0).data_ptr() == 2 * a.stride

@@ -285,7 +285,13 @@ def test_push_loop_thread_keeps_releasing_while_pusher_frees():
     last push — here it destroys a plan (hipFree synchronises the device)
     while the loop thread still has releases to issue.  The loop thread's
     launches are not held up by the blocked thread, so the consumer completes
-    instead of waiting out its timeout."""
+    instead of waiting out its timeout.  The plan is made before the
+    iteration begins: its table upload is a synchronous hipMemcpy, i.e.
+    legacy NULL-stream work, which waits for the running consumer (a blocking
+    stream) and holds back every stream sharing the NULL stream's hardware
+    queue — the release stream among them, by the runtime's placement
+    (include/bpsr/reduce.h: no NULL-stream work between a launch and its last
+    release; this test once passed by placement alone)."""
     from prophet_amd.dtypes import DType
     from prophet_amd.prophet import PushLoop
     S = _setup(seed=5)
@@ -294,11 +300,11 @@ def test_push_loop_thread_keeps_releasing_while_pusher_frees():
     loop = PushLoop(S["q"], S["bq"], S["block_of"], release_stream=rel, inline=False)
     x, y, z = (torch.zeros(1 << 20, dtype=torch.uint8, device="cuda") for _ in range(3))
     for it in range(3):
+        plan = red.make_plan([(x, [y, z], x.numel())], DType.UINT8)
         torch.cuda.synchronize()
         loop.begin()
         for t, i in S["tasks"]:
             loop.push(t, i)
-        plan = red.make_plan([(x, [y, z], x.numel())], DType.UINT8)
         plan.close()                                  # hipFree while releases are pending
         loop.end(timeout_s=10.0)
         torch.cuda.synchronize()

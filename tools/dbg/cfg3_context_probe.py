@@ -39,7 +39,8 @@ def main():
     def show(tag):
         r = bench.cfg3_leg(dev, red, iters=a.iters, reps=3)
         print(tag, {k: (v["ms_per_iter"], v["frac_of_roofline"]) for k, v in r.items()
-                    if isinstance(v, dict)}, flush=True)
+                    if isinstance(v, dict) and "ms_per_iter" in v},
+              "queues", r.get("hsa_queue_ids"), flush=True)
 
     if a.seq:
         link = None
@@ -55,6 +56,22 @@ def main():
             elif leg == "e2e":
                 r = bench.e2e_leg(dev, 1, 0, link=link)
                 print(f"{i}:e2e", r["ms"], r.get("frac_of_link"), flush=True)
+            elif leg in ("mkq", "tinyq"):
+                # round 6: the block queue's library queues made (mkq: the
+                # consumer and release queues only), or also one small
+                # pre-released launch folded (tinyq)
+                from prophet_amd.dtypes import DType
+                x = [torch.ones(1 << 16, device=dev) for _ in range(3)]
+                q = red.make_blockq([[(x[0], x[1:], 4 << 16)]], DType.FLOAT32)
+                q.stream()
+                q.release_stream()
+                if leg == "tinyq":
+                    q.release(-1)
+                    q.launch()
+                    q.status()
+                torch.cuda.synchronize()
+                q.close()
+                print(f"{i}:{leg}", q.queue_ids() if False else "", flush=True)
             elif leg == "headline":
                 bench.main_headline_for_probe(dev) if hasattr(bench, "main_headline_for_probe") else None
         return
