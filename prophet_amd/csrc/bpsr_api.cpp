@@ -815,6 +815,22 @@ static hipError_t placed_queue(ConsumerDev& D, int cus, Fits fits, hipStream_t* 
   }
 }
 
+// At process exit, before the HIP runtime's own teardown (the handler is
+// registered after the runtime is up, and exit handlers run in reverse):
+// the library's queues are destroyed like any other stream, not left to the
+// runtime's teardown — under rocprofv3 a process holding them at exit faulted
+// inside the profiler's own finalizer (profiles/r06s06_exit_fault_frames.txt).
+static void destroy_queue_sets() {
+  std::lock_guard<std::mutex> g(g_consumer_mu);
+  for (auto& D : g_cdev) {
+    for (auto& q : D.q)
+      if (q) (void)hipStreamDestroy(q), q = nullptr;
+    if (D.rq) (void)hipStreamDestroy(D.rq), D.rq = nullptr;
+    for (auto& sp : D.spare) (void)hipStreamDestroy(sp.first);
+    D.spare.clear();
+  }
+}
+
 // The device's four library queues, made together on first use (above):
 // slots 0-2 the consumer queues, slot 3 the release queue.
 static hipError_t queue_set(int device, int cus, ConsumerDev** out) {
@@ -846,6 +862,8 @@ static hipError_t queue_set(int device, int cus, ConsumerDev** out) {
     for (int k = 0; k < 4; ++k) *slot[k] = nullptr;
     return e;
   }
+  static bool registered = false;
+  if (!registered) registered = std::atexit(destroy_queue_sets) == 0;
   return hipSuccess;
 }
 
