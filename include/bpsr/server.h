@@ -112,8 +112,14 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * with pushes still being copied by the lanes (non-blocking pushes, host
  * data) folds with a lane launch behind its copies, and its key passes the
  * epoch's consumer with a skip word: the consumer never waits for lane-stream
- * work.  One consumer launch per epoch (the
- * epoch's first release launches it) folds every key of the queue, each key's
+ * work.  One consumer launch per epoch folds every key of the queue; it is
+ * launched once the previous epoch has begun (its first release), behind that
+ * epoch's consumer on the keyed queue, so it is resident and polling when its
+ * own first release arrives (an epoch whose consumer was not launched that
+ * way is launched by its first release).  A consumer launched ahead whose
+ * epoch no round begins within 1 ms is retired: its keys get skip words, it
+ * completes, and their next rounds go to the next epoch (byteps_server_stats
+ * out[11]).  The consumer folds each key's
  * tiles as soon as that key is released, in its arrival order (the same bits
  * as the launch path).  Each key's last tile stores the epoch into the key's
  * completion word once the key's bytes are visible device-wide, so device
@@ -132,7 +138,9 @@ int byteps_server_config_from_env(byteps_server_config* cfg);
  * thread that still has to push must not wait for the whole device
  * (hipDeviceSynchronize, hipFree), nor put work on the legacy NULL stream
  * (it waits for every blocking stream, the consumer's included) — work on
- * non-blocking streams, and stream or event syncs, are fine. */
+ * non-blocking streams, and stream or event syncs, are fine.  Between rounds
+ * such a wait costs at most the 1 ms after which an idle consumer launched
+ * ahead is retired. */
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
 /* The same, for a caller that states the size of its config: every version of
  * byteps_server_config is a prefix of the next (fields are only appended), so
@@ -305,10 +313,14 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
  * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
- * push-copy launches, out[6] keyed consumer launches and out[7] rounds
- * released on the device (BPSR_SERVER_RELEASE=device), out[8] blocking pulls
- * served by the pull copy service, out[9] that service's kernel launches and
- * out[10] blocking pushes it served; the first n (<= 11). */
+ * push-copy launches, out[6] keyed consumer epochs a round was released for
+ * and out[7] rounds released on the device (BPSR_SERVER_RELEASE=device),
+ * out[8] blocking pulls served by the pull copy service, out[9] that
+ * service's kernel launches, out[10] blocking pushes it served and out[11]
+ * keyed consumers launched ahead of their epoch and retired because no round
+ * began it within 1 ms (each epoch's consumer is launched once the previous
+ * epoch has begun, so that it is resident when its first round arrives); the
+ * first n (<= 12). */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

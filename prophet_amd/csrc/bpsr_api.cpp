@@ -713,6 +713,7 @@ struct byteps_reduce_blockq {
   uint32_t* kcnt = nullptr;         // device, one tile counter per block
   uint32_t* khdone = nullptr;       // pinned host, one completion word per block
   uint32_t* khdone_dev = nullptr;
+  uint32_t opened = 0;              // highest epoch a round was released for (keyq_opened)
 };
 
 // Per device, created on first use, never destroyed: three consumer queues
@@ -1584,8 +1585,15 @@ void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t
   *launched = keyq_launched(q);
 }
 
-int keyq_release(byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s) {
+int keyq_release(byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s, bool* first) {
   const uint32_t ep = q->rel_epoch[(size_t)key] + 1;
+  {  // a round (folded here, or a skip word for a lane-folded one): the epoch has begun
+    uint32_t o = __atomic_load_n(&q->opened, __ATOMIC_ACQUIRE);
+    while (o < ep && !__atomic_compare_exchange_n(&q->opened, &o, ep, true, __ATOMIC_ACQ_REL,
+                                                  __ATOMIC_ACQUIRE)) {
+    }
+    if (first) *first = o < ep;
+  }
   const uint64_t w = key_word((uint32_t)perm, ep);
   const uint64_t w2 = key_word((uint32_t)(perm >> 32), ep);  // wide: positions 8..15
   const size_t second = (size_t)q->nblocks + (size_t)key;
@@ -1600,6 +1608,18 @@ int keyq_release(byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s)
   }
   __atomic_store_n(&q->rel_epoch[(size_t)key], ep, __ATOMIC_RELEASE);
   return BYTEPS_REDUCE_OK;
+}
+
+uint32_t keyq_opened(const byteps_reduce_blockq* q) {
+  return __atomic_load_n(&q->opened, __ATOMIC_ACQUIRE);
+}
+
+bool keyq_close(byteps_reduce_blockq* q, uint32_t epoch) {
+  uint32_t o = __atomic_load_n(&q->opened, __ATOMIC_ACQUIRE);
+  while (o < epoch)
+    if (__atomic_compare_exchange_n(&q->opened, &o, epoch, true, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+      return true;
+  return false;
 }
 
 bool keyq_key_done(const byteps_reduce_blockq* q, int key, uint32_t epoch) {

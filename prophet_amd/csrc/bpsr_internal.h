@@ -410,7 +410,18 @@ uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
 uint32_t keyq_launched(struct byteps_reduce_blockq* q);
 // Both of the above under one lock.
 void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched);
-int keyq_release(struct byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s);
+// `first` (optional): set when this release is the first one of its epoch
+// (keyq_opened; after keyq_close, none is).
+int keyq_release(struct byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s,
+                 bool* first = nullptr);
+// The highest epoch a key has been released for (a round, or a skip word for
+// a round folded elsewhere) or closed: an epoch at or below it has begun
+// (lock-free host read).
+uint32_t keyq_opened(const struct byteps_reduce_blockq* q);
+// Mark `epoch` begun without a round (an epoch launched ahead is retired):
+// false when a round was released for it first.  Rounds released for it
+// afterwards are folded by its consumer as usual, but are not its first.
+bool keyq_close(struct byteps_reduce_blockq* q, uint32_t epoch);
 bool keyq_failed(struct byteps_reduce_blockq* q);
 // The key's fold for `epoch` is complete and visible device-wide (its block's
 // last tile stored the completion word): a lock-free host read.

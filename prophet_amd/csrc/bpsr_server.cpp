@@ -99,15 +99,37 @@ void completer_main(byteps_server* s, Lane* Lp) {
     if (t.kq_epoch) {
       // a keyed consumer: every pull and view of its epoch waits for this,
       // so poll its event (no other thread makes HIP calls on the device-
-      // release path) for up to 2 ms before a blocking wait — a blocking
-      // event wait wakes tens of microseconds late
-      const auto p0 = std::chrono::steady_clock::now();
+      // release path) for up to 2 ms of a begun epoch before a blocking wait
+      // — a blocking event wait wakes tens of microseconds late.  Once a
+      // round has begun the epoch, the next epoch's consumer is launched
+      // behind it (kq_launch_ahead); an epoch launched so that no round has
+      // begun within kKeyedIdleUs (or at destroy) is retired (kq_retire).
+      const auto i0 = std::chrono::steady_clock::now();
+      auto p0 = i0;
+      bool ahead = false, retired = false;
       while (hipEventQuery(t.ev) == hipErrorNotReady) {
-        if (std::chrono::steady_clock::now() - p0 > std::chrono::milliseconds(2)) {
+        const auto now = std::chrono::steady_clock::now();
+        const bool begun = keyq_opened(s->kq) >= t.kq_epoch;
+        if (begun && !ahead && !retired) {
+          ahead = true;
+          kq_launch_ahead(s, t.kq_epoch);
+          p0 = std::chrono::steady_clock::now();
+          continue;
+        }
+        if (!begun && !retired &&
+            (s->kq_stopping.load(std::memory_order_acquire) ||
+             now - i0 > std::chrono::microseconds(byteps_server::kKeyedIdleUs))) {
+          retired = kq_retire(s, t.kq_epoch);
+          continue;
+        }
+        if (begun && now - p0 > std::chrono::milliseconds(2)) {
           (void)hipEventSynchronize(t.ev);
           break;
         }
-        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+        if (!begun && now - i0 > std::chrono::microseconds(100))
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else
+          for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
       }
       kq_epoch_done(s, t.kq_epoch, t.seq);
     } else {
@@ -1294,6 +1316,7 @@ int byteps_server_destroy(byteps_server* s) {
   (void)hipSetDevice(s->cfg.device);
   destroy_lanes(s);  // queued jobs are issued first (the dispatchers drain)
   if (s->klane) {    // the keyed consumers complete (or time out) and settle their epochs
+    s->kq_stopping.store(true, std::memory_order_release);  // an idle epoch retires at once
     {
       std::lock_guard<std::mutex> g(s->klane->done_mu);
       s->klane->cq_stop = true;
@@ -1849,12 +1872,12 @@ int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
     std::lock_guard<std::mutex> g(s->svc_mu);
     svc_launches = bpsr::copysvc_launches(s->svc);
   }
-  const uint64_t v[11] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+  const uint64_t v[12] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
                           s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
                           s->n_copy_launches.load(), s->n_consumer_launches.load(),
                           s->n_key_releases.load(), s->n_service_pulls.load(), svc_launches,
-                          s->n_service_pushes.load()};
-  for (int i = 0; i < n && i < 11; ++i) out[i] = v[i];
+                          s->n_service_pushes.load(), s->n_consumer_retired.load()};
+  for (int i = 0; i < n && i < 12; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

@@ -59,6 +59,67 @@ bool keyed_member(byteps_server* s, KeyState* ks) {
   return ks->kq_key.load() >= 0;
 }
 
+// Launch the consumers of every epoch up to `need` (caller holds kq_mu):
+// each gets its ring slot's stop event and is tracked by the keyed completer.
+int kq_launch_upto(byteps_server* s, uint32_t need) {
+  for (uint32_t launched = keyq_launched(s->kq); launched < need;
+       launched = keyq_launched(s->kq)) {
+    const uint32_t next = launched + 1;
+    const int slot = (int)(next % byteps_server::kKqRing);
+    if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
+      return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
+                  byteps_server::kKqRing);
+    hipEvent_t& e = s->kq_ev[slot];
+    if (!e) {
+      if (int rc = force_device(s)) return rc;
+      const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      if (he != hipSuccess) {
+        e = nullptr;
+        return hip_fail(he, "hipEventCreate(consumer)");
+      }
+    }
+    uint32_t got = 0;
+    hipStream_t cs = nullptr;
+    if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
+    s->kq_ev_epoch[slot] = got;
+    s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
+    s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
+  }
+  return 0;
+}
+
+// The keyed completer, once epoch `epoch` has begun: launch the next epoch's
+// consumer now, behind this one on the keyed queue, so that it is dispatched
+// the moment this one completes and its tiles are resident, polling their
+// words, before the next round's first push (DESIGN.md §9 "launched ahead").
+// A launch that fails here is left to the next round's first release, which
+// launches as before.
+void kq_launch_ahead(byteps_server* s, uint32_t epoch) {
+  std::lock_guard<std::mutex> g(s->kq_mu);
+  if (s->kq_off.load() || !s->kq || keyq_failed(s->kq)) return;
+  (void)kq_launch_upto(s, epoch + 1);
+}
+
+// Retire an epoch launched ahead that no round has begun: every key not yet
+// released for it gets a skip word (the tiles pass it, nothing is stored), so
+// the consumer completes at once and its keys' next rounds go to the next
+// epoch, launched by their first release as without the launch ahead.  The
+// epoch is closed first (keyq_close), so a round that begins it from then on
+// is not counted as its first; such a round keeps its place in this epoch
+// (key by key, under the key's lock, as its release is) and is folded by it.
+// False: a round had begun the epoch, which is not retired.
+bool kq_retire(byteps_server* s, uint32_t epoch) {
+  if (!keyq_close(s->kq, epoch)) return false;  // a round began it after all
+  const uint64_t skip = ((uint64_t)kKeySkip << 32) | kKeySkip;
+  for (KeyState* k : s->kq_keys) {
+    std::lock_guard<std::mutex> g(k->mu);
+    const int kk = k->kq_key.load();
+    if (kk >= 0 && keyq_next_epoch(s->kq, kk) == epoch) (void)keyq_release(s->kq, kk, skip, nullptr);
+  }
+  s->n_consumer_retired.fetch_add(1, std::memory_order_relaxed);
+  return true;
+}
+
 // Release a finished round of a keyed key (caller holds ks->mu): the arrival
 // order and the release word go to the key's block — stored from the host
 // when the round's data is in its slots already (push_ready), or by a one-lane
@@ -73,6 +134,7 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
   if (skip) perm = ((uint64_t)kKeySkip << 32) | kKeySkip;
   hipEvent_t ev = nullptr;
   uint64_t seq = 0;
+  bool first = false;  // the first round released for its epoch
   const int kk = ks->kq_key.load();
   uint32_t need = keyq_next_epoch(s->kq, kk);
   Lane& RL = *s->lanes[ks->lane];
@@ -89,7 +151,7 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
       if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
       RL.where = "key_release: release kernel";
     }
-    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
+    if (int rc = keyq_release(s->kq, kk, perm, stream, &first)) return rc;
   } else {
     if (stream) RL.where = "key_release: kq_mu";
     std::lock_guard<std::mutex> g(s->kq_mu);
@@ -97,41 +159,20 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
     if (s->kq_off.load()) return 1;
     uint32_t launched = 0;
     keyq_state(s->kq, kk, &need, &launched);
-    for (; launched < need; launched = keyq_launched(s->kq)) {
-      const uint32_t next = launched + 1;
-      const int slot = (int)(next % byteps_server::kKqRing);
-      if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
-        return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
-                    byteps_server::kKqRing);
-      hipEvent_t& e = s->kq_ev[slot];
-      if (!e) {
-        if (int rc = force_device(s)) return rc;
-        const hipError_t he = hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        if (he != hipSuccess) {
-          e = nullptr;
-          return hip_fail(he, "hipEventCreate(consumer)");
-        }
-      }
-      uint32_t got = 0;
-      hipStream_t cs = nullptr;
-      if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
-      s->kq_ev_epoch[slot] = got;
-      s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
-      s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
-      s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
-    }
+    if (int rc = kq_launch_upto(s, need)) return rc;
     if (stream) {
       RL.where = "key_release: wait d2h";
       const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
       if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
       RL.where = "key_release: release kernel";
     }
-    if (int rc = keyq_release(s->kq, kk, perm, stream)) return rc;
+    if (int rc = keyq_release(s->kq, kk, perm, stream, &first)) return rc;
     const int slot = (int)(need % byteps_server::kKqRing);
     ev = s->kq_ev[slot];
     seq = s->kq_ev_seq[slot];
   }
   if (stream) RL.where = "key_release: publish";
+  if (first) s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
   if (skip) return 0;  // the round is folded by a lane launch, which publishes it
   s->n_key_releases.add();
   ks->kq_round_epoch = need;

@@ -348,15 +348,21 @@ struct byteps_server {
   byteps_reduce_blockq* kq = nullptr;
   bool kq_tried = false;
   std::atomic<bool> kq_off{false};
+  std::atomic<bool> kq_stopping{false};  // destroy: retire an idle epoch at once
   std::vector<bpsr::KeyState*> kq_keys;  // block -> key
   static constexpr int kKqRing = 64;
+  // an epoch launched ahead that no round begins within this is retired
+  // (kq_retire): its consumer would otherwise hold two workgroup slots per CU
+  // and keep device-wide waits (hipDeviceSynchronize, NULL-stream copies) open
+  static constexpr int kKeyedIdleUs = 1000;
   hipEvent_t kq_ev[kKqRing] = {};       // stop event of epoch e at e % kKqRing
   uint64_t kq_ev_seq[kKqRing] = {};     // lane-0 seq of that launch
   uint32_t kq_ev_epoch[kKqRing] = {};
   uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
   std::atomic<uint32_t> kq_pub_epoch{0};  // epochs launched with their kq_ev slot written
   std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
-  std::atomic<uint64_t> n_consumer_launches{0};
+  std::atomic<uint64_t> n_consumer_launches{0};  // epochs a round was released for
+  std::atomic<uint64_t> n_consumer_retired{0};   // epochs launched ahead and retired idle
   ShardedCount n_key_releases;
   // Blocking pulls into this device's memory (combine path): served by the
   // pull copy service, created on first use (BPSR_SERVER_PULL_SERVICE=0: the
@@ -415,6 +421,9 @@ void build_kq(byteps_server* s, int dtype);
 bool keyed_member(byteps_server* s, KeyState* ks);
 int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
                 bool skip = false);
+int kq_launch_upto(byteps_server* s, uint32_t need);
+void kq_launch_ahead(byteps_server* s, uint32_t epoch);
+bool kq_retire(byteps_server* s, uint32_t epoch);
 void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq);
 void wait_published(byteps_server* s, KeyState* ks, uint64_t seq);
 int execute(byteps_server* s, const FoldJob& j);

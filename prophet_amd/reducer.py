@@ -136,6 +136,16 @@ def _ptr(x) -> int:
     raise TypeError(f"expected a device pointer or tensor, got {type(x)!r}")
 
 
+def _fits(length: int, *xs) -> None:
+    """Host-side bounds check before a launch: every tensor operand holds at
+    least ``length`` bytes (raw pointers carry no size and are the caller's)."""
+    for x in xs:
+        if hasattr(x, "data_ptr") and hasattr(x, "element_size"):
+            have = int(x.numel()) * int(x.element_size())
+            if int(length) > have:
+                raise ValueError(f"{int(length)}-byte operation on a {have}-byte tensor")
+
+
 def _stream_of(x, stream):
     if stream is not None:
         return int(getattr(stream, "cuda_stream", stream))
@@ -160,18 +170,21 @@ class GpuReducer:
 
     def sum(self, dst, src, length: int, dtype: int, stream=None) -> int:
         """In place ``dst += src`` over ``length`` bytes (cpu_reducer.cc:57-83)."""
+        _fits(length, dst, src)
         _check(self.lib.byteps_reduce_sum(_ptr(dst), _ptr(src), int(length), int(dtype),
                                           _stream_of(dst, stream)))
         return 0
 
     def sum3(self, dst, src1, src2, length: int, dtype: int, stream=None) -> int:
         """``dst = src1 + src2`` (cpu_reducer.cc:130-162)."""
+        _fits(length, dst, src1, src2)
         _check(self.lib.byteps_reduce_sum3(_ptr(dst), _ptr(src1), _ptr(src2), int(length),
                                            int(dtype), _stream_of(dst, stream)))
         return 0
 
     def copy(self, dst, src, length: int, stream=None) -> int:
         """``length``-byte device copy (cpu_reducer.cc:209-220)."""
+        _fits(length, dst, src)
         _check(self.lib.byteps_reduce_copy(_ptr(dst), _ptr(src), int(length),
                                            _stream_of(dst, stream)))
         return 0
@@ -179,6 +192,7 @@ class GpuReducer:
     def sum_n(self, dst, srcs: Sequence, length: int, dtype: int,
               mode: int = MODE_REFERENCE, stream=None) -> int:
         """Left fold ``dst = ((srcs[0] + srcs[1]) + ...)`` in the given order."""
+        _fits(length, dst, *srcs)
         arr = (_vp * len(srcs))(*[_ptr(s) for s in srcs])
         _check(self.lib.byteps_reduce_sum_n(_ptr(dst), arr, len(srcs), int(length),
                                             int(dtype), int(mode), _stream_of(dst, stream)))

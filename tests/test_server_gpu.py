@@ -1823,6 +1823,81 @@ def test_device_release_rounds_bit_exact(port, N, dt, monkeypatch):
     assert 1 <= st["fold_launches"] - st0["fold_launches"] <= copied * len(keys)
 
 
+def test_device_release_epoch_launched_ahead_and_retired(port, monkeypatch):
+    """Device releases launch each epoch's consumer once the previous epoch
+    has begun (kq_launch_ahead), behind it on the keyed queue, so it is
+    resident before the next round's first push; an epoch launched ahead that
+    no round begins within 1 ms is retired (skip words: its tiles pass,
+    nothing is stored) and the next round launches its own.  Rounds back to
+    back and after idle gaps, 4 workers, fp16: every pull equals the oracle's
+    left fold in the recorded order; consumer_launches counts the begun
+    epochs only (one per round), the idle gaps show as retirements; a
+    device-wide sync and destroy with an idle consumer launched ahead return
+    at once instead of waiting for the release timeout."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    monkeypatch.setenv("BPSR_SERVER_RELEASE_TIMEOUT_S", "3")
+    dt, N, R = DType.FLOAT16, 4, 6
+    sizes = [5, 4096 + 1, 100_003]
+    keys = [70, 71, 72]
+    es = elem_size(dt)
+    dev = torch.device("cuda:0")
+    src = {(w, r, j): torch.from_numpy(data(dt, n, w, r, j)).to(dev)
+           for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    torch.cuda.synchronize()
+    srv = PSServer(N, engine_lanes=2)
+    st = torch.cuda.Stream(device=dev)      # never the legacy NULL stream (server.h)
+    closed = False
+    try:
+        with torch.cuda.stream(st):
+            for j, k in enumerate(keys):                 # init round: blocking pushes
+                ts = [threading.Thread(target=srv.push, args=(k, w, src[(w, 0, j)], dt))
+                      for w in range(N)]
+                for t in ts:
+                    t.start()
+                for t in ts:
+                    t.join(timeout=60)
+            for r in range(1, R + 1):
+                for j, k in enumerate(keys):             # the transport writes the slots
+                    for w in range(N):
+                        x = src[(w, r, j)]                   # the key's bytes (uint8)
+                        GpuReducer().copy(srv.recv_slot(k, w), x, x.numel(), stream=st)
+                st.synchronize()
+                if r in (4, 5):
+                    time.sleep(0.01)                     # idle: the epoch launched ahead retires
+                for j, k in enumerate(keys):
+                    for w in range(N):
+                        srv.push_ready(k, w)
+                for j, k in enumerate(keys):
+                    _, _, order = srv.key_info(k)
+                    n = sizes[j] * es
+                    want = np.zeros(n, np.uint8)
+                    port.sum_n(want, [data(dt, sizes[j], w, r, j) for w in order], n, dt)
+                    for w in range(N):
+                        o = torch.empty(n, dtype=torch.uint8, device=dev)
+                        srv.pull(k, o)
+                        assert np.array_equal(o.cpu().numpy(), want), (r, k, w)
+                if r == 1:
+                    st0 = srv.stats()
+        stats = srv.stats()
+        t0 = time.time()
+        torch.cuda.synchronize()          # the epoch launched ahead is idle: it retires
+        sync_s = time.time() - t0
+        t0 = time.time()
+        srv.close()
+        closed = True
+        close_s = time.time() - t0
+    finally:
+        if not closed:
+            srv.close()
+    assert stats["key_releases"] == R * len(keys), stats
+    assert stats["consumer_launches"] == R, stats            # begun epochs only
+    assert stats["consumers_retired"] >= 2, stats             # the two idle gaps at least
+    assert stats["fold_launches"] == st0["fold_launches"], stats  # no lane folds
+    assert sync_s < 1.0 and close_s < 1.0, (sync_s, close_s)
+
+
 @pytest.mark.parametrize("release", [None, "device"], ids=["env-default", "device"])
 def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
     """The dedicated server process (server.cc:339-400) builds its server from
