@@ -680,15 +680,21 @@ __device__ __forceinline__ uint32_t ld_err(const BlockqLaunch& Q) {
 // Workgroup 0: forward the host-written words of this launch's epoch (the
 // epoch's parity slot) into the device words, until every block holds this
 // epoch (or the sticky error / the timeout ends the launch).  A block
-// released by a stream kernel already holds it.  Vector atomics only.
+// released by a stream kernel already holds it.  Vector atomics only.  Its 4
+// waves take 64-key chunks in turn (wave w: chunks w, w + 4, ...), so a sweep
+// costs one chunk's dependent loads (device word, then host word over PCIe)
+// rather than one per chunk: with the epoch's consumer launched ahead, its
+// tiles are waiting when the first push arrives, and the sweep is the delay
+// between a release and its fold.
 __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
-  if (threadIdx.x >= 64) return;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t first = threadIdx.x & ~63u;  // this wave's first chunk
+  if (first >= Q.nblocks) return;
   const uint32_t par = Q.epoch & 1u;
   const uint64_t t0 = wall_clock64();
   for (;;) {
     bool pending = false;
-    for (uint32_t base = 0; base < Q.nblocks; base += 64) {
+    for (uint32_t base = first; base < Q.nblocks; base += kBlock) {
       const uint32_t b = base + lane;
       if (b < Q.nblocks && (uint32_t)ld_agent64(Q.kwords + b) != Q.epoch) {
         const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);

@@ -384,11 +384,11 @@ void fail_key(byteps_server* s, KeyState* ks, int rc) {
 void queue_pull_copies(byteps_server* s, KeyState* ks, const KeyState::WaitingCopy* wcs, size_t n) {
   if (n == 0) return;
   Lane& L = *s->lanes[ks->lane];
-  std::unique_lock<std::mutex> kg(s->kq_mu, std::defer_lock);
+  std::unique_lock<std::mutex> kg(s->kq_park_mu, std::defer_lock);
   bool park = false;
   if (ks->keyed) {  // nothing reads a keyed store before its epoch is published
     kg.lock();
-    park = s->kq_done_seq < ks->fold_seq;
+    park = s->kq_done_seq.load(std::memory_order_relaxed) < ks->fold_seq;
     if (!park) kg.unlock();
   }
   std::unique_lock<std::mutex> g(L.comb_mu, std::defer_lock);
@@ -782,7 +782,11 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer,
   j.ks = ks;
   j.kind = s->cfg.policy == BYTEPS_SERVER_INCREMENTAL ? kFinishIncremental : kFinishFused;
   j.acc = ks->order[0];
-  j.order = ks->order;
+  // the order's buffer travels with the job and comes back through
+  // order_spare once the issuer has published the round (recycle_order):
+  // no allocation here and no free on another thread, per round
+  j.order.swap(ks->order);
+  ks->order.swap(ks->order_spare);
   ks->order.clear();
   ks->arrived = 0;
   // Combining: EVERY finished round goes to the lane's issuer (a fold that
@@ -797,6 +801,12 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer,
   const int rc = submit(s, ks, std::move(j));
   if (q) q->clear_counter(ks->key);  // server.cc:269-271
   return rc;
+}
+
+// A published round's order buffer goes back to its key (caller holds
+// ks->mu), for the next round's arrivals (arrive).
+void recycle_order(KeyState* ks, FoldJob& j) {
+  if (ks->order_spare.capacity() == 0) ks->order_spare.swap(j.order);
 }
 
 // Issue deferred fused folds: per (lane, dtype) ONE batched launch whose
@@ -878,6 +888,7 @@ int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs) {
       ks->pending--;
       const int r2 = rc ? rc : finish_round(s, ks, jobs[k].order, /*mark=*/false, bev, bseq);
       if (r2) fail_key(s, ks, r2);
+      recycle_order(ks, jobs[k]);
       ks->cv.notify_all();
     }
     if (rc && !first_rc) first_rc = rc;
@@ -908,6 +919,7 @@ int issue_one(byteps_server* s, FoldJob& j) {
   ks->pending--;
   const int rc = ks->error ? 0 : execute(s, j);
   if (rc) fail_key(s, ks, rc);
+  recycle_order(ks, j);
   ks->cv.notify_all();
   return rc;
 }
@@ -1325,7 +1337,7 @@ int byteps_server_destroy(byteps_server* s) {
     if (s->klane->completer.joinable()) s->klane->completer.join();
     std::vector<PullJob> parked;
     {
-      std::lock_guard<std::mutex> g(s->kq_mu);
+      std::lock_guard<std::mutex> g(s->kq_park_mu);
       parked.swap(s->kq_parked);
     }
     for (PullJob& j : parked) {  // pulls of epochs that never completed: cancelled
@@ -1443,7 +1455,8 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
   if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
-  std::vector<FoldJob> defer;
+  thread_local std::vector<FoldJob> defer;  // keeps its capacity: no allocation per call
+  defer.clear();
   if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return rc;
   if (!defer.empty()) {
     lk.unlock();
@@ -1580,7 +1593,8 @@ int byteps_server_push_ready(byteps_server* s, uint64_t key, int worker) {
   if ((rc = wait_order_gate(s))) return rc;
   std::unique_lock<std::mutex> lk(ks->mu);
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
-  std::vector<FoldJob> defer;
+  thread_local std::vector<FoldJob> defer;  // keeps its capacity: no allocation per call
+  defer.clear();
   if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return rc;
   if (!defer.empty()) {
     lk.unlock();

@@ -50,11 +50,13 @@ void build_kq(byteps_server* s, int dtype) {
 // r05s55), so the server keeps launches for good.
 bool keyed_member(byteps_server* s, KeyState* ks) {
   if (!s->dev_release || s->kq_off.load()) return false;
+  // decided once: no lock from then on (kq_mu is held across the consumer
+  // launches, and every round's last arrival asks this)
+  if (s->kq_tried.load(std::memory_order_acquire)) return ks->kq_key.load() >= 0;
   std::lock_guard<std::mutex> g(s->kq_mu);
-  if (!s->kq_tried) {
-    s->kq_tried = true;
-    if (ks->round_copied) return false;  // no queue: launches from here on
-    build_kq(s, ks->dtype);
+  if (!s->kq_tried.load(std::memory_order_relaxed)) {
+    if (!ks->round_copied) build_kq(s, ks->dtype);  // copied: no queue, launches from here on
+    s->kq_tried.store(true, std::memory_order_release);
   }
   return ks->kq_key.load() >= 0;
 }
@@ -66,7 +68,7 @@ int kq_launch_upto(byteps_server* s, uint32_t need) {
        launched = keyq_launched(s->kq)) {
     const uint32_t next = launched + 1;
     const int slot = (int)(next % byteps_server::kKqRing);
-    if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq < s->kq_ev_seq[slot])
+    if (s->kq_ev_epoch[slot] != 0 && s->kq_done_seq.load() < s->kq_ev_seq[slot])
       return fail(BYTEPS_REDUCE_EARGS, "device releases: %d epochs in flight",
                   byteps_server::kKqRing);
     hipEvent_t& e = s->kq_ev[slot];
@@ -224,7 +226,10 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
       for (KeyState* k : s->kq_keys)
         if (keyq_next_epoch(s->kq, k->kq_key.load()) > epoch) failed.push_back(k);
     }
-    s->kq_done_seq = seq;
+  }
+  {
+    std::lock_guard<std::mutex> g(s->kq_park_mu);
+    s->kq_done_seq.store(seq);
     for (PullJob& j : s->kq_parked) (j.kseq <= seq ? go : keep).push_back(j);
     s->kq_parked.swap(keep);
   }

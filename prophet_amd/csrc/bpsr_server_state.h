@@ -200,6 +200,7 @@ struct KeyState {
   // current round
   std::vector<char> got;      // worker pushed this round (cleared when the round's fold is issued)
   std::vector<int> order;     // arrival order this round
+  std::vector<int> order_spare;  // a buffer for the next round's order (recycle_order)
   int arrived = 0;
   int init_count = 0;
   int init_last = -1;         // the init round's last arrival (its push initialises the store)
@@ -346,7 +347,7 @@ struct byteps_server {
   std::unique_ptr<bpsr::Lane> klane;  // its completer tracks the consumer launches (no streams)
   std::mutex kq_mu;  // guards the kq_* state below (taken after a key's mu, never before)
   byteps_reduce_blockq* kq = nullptr;
-  bool kq_tried = false;
+  std::atomic<bool> kq_tried{false};  // the keyed queue was built or refused (set once)
   std::atomic<bool> kq_off{false};
   std::atomic<bool> kq_stopping{false};  // destroy: retire an idle epoch at once
   std::vector<bpsr::KeyState*> kq_keys;  // block -> key
@@ -358,9 +359,13 @@ struct byteps_server {
   hipEvent_t kq_ev[kKqRing] = {};       // stop event of epoch e at e % kKqRing
   uint64_t kq_ev_seq[kKqRing] = {};     // lane-0 seq of that launch
   uint32_t kq_ev_epoch[kKqRing] = {};
-  uint64_t kq_done_seq = 0;             // lane-0 seq up to which keyed epochs are published
+  // lane-0 seq up to which keyed epochs are published, and the pulls parked
+  // on later ones: under kq_park_mu (never held together with kq_mu, which a
+  // consumer launch holds), so a round's pulls are never queued behind a launch
+  std::mutex kq_park_mu;
+  std::atomic<uint64_t> kq_done_seq{0};
   std::atomic<uint32_t> kq_pub_epoch{0};  // epochs launched with their kq_ev slot written
-  std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet
+  std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet (kq_park_mu)
   std::atomic<uint64_t> n_consumer_launches{0};  // epochs a round was released for
   std::atomic<uint64_t> n_consumer_retired{0};   // epochs launched ahead and retired idle
   ShardedCount n_key_releases;
@@ -435,6 +440,7 @@ int arrive(byteps_server* s, KeyState* ks, int w, std::vector<FoldJob>* defer = 
 int flush_folds(byteps_server* s, std::vector<FoldJob>& jobs);
 int finish_blocking(byteps_server* s, KeyState* ks, std::unique_lock<std::mutex>& lk);
 int issue_one(byteps_server* s, FoldJob& j);
+void recycle_order(KeyState* ks, FoldJob& j);
 int issue_combined(byteps_server* s, std::vector<FoldJob>& jobs);
 int issue_deferred(byteps_server* s, std::vector<FoldJob>& jobs);
 void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs);

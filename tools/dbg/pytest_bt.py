@@ -7,7 +7,6 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import pytest  # noqa: E402
 
-ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libabrt_bt.so"))
-
-rc = pytest.main(sys.argv[1:] + ["-p", "no:faulthandler"])
-sys.exit(rc)
+if __name__ == "__main__":  # spawned children (multiprocessing) re-import this module
+    ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libabrt_bt.so"))
+    sys.exit(pytest.main(sys.argv[1:] + ["-p", "no:faulthandler"]))
