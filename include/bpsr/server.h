@@ -81,66 +81,63 @@ typedef struct byteps_server byteps_server;
  * (here "1" means asynchronous; the reference reads the flag inverted,
  * server.cc:315), BPSR_SERVER_POLICY (fused|incremental),
  * BYTEPS_SERVER_ENABLE_SCHEDULE, BYTEPS_SERVER_ENGINE_BLOCKING, device 0, and
- * release = LAUNCH.  Not DEVICE, although the server process byteps_server()
- * (server.cc:339-400) starts does nothing else on its GPU, for two reasons.
- * That process receives its pushes into host memory (ps-lite's buffers,
- * server.cc:174-218), so its rounds are copied rounds, which device releases
- * cannot fold: such a server builds no keyed queue (below) and folds with
- * launches either way (config 1: 3.13-3.17 ms per round with DEVICE set,
- * 3.1 with LAUNCH; 11.5-13.3 ms before it skipped the queue — DESIGN.md §9
- * round 5).  And DEVICE adds a contract the reference does not have: every
- * key completes one round per epoch, or the epoch fails with
- * BYTEPS_REDUCE_ETIMEOUT (below).  Device releases pay when the pushes land in
- * HBM (byteps_server_push_ready after an RDMA write into GPU memory): config
- * 3's keys from one receive thread at 0.49 of the HBM roofline instead of
- * 0.21-0.28 (the bench line's server_cfg3) — set BPSR_SERVER_RELEASE=device
- * (or release = DEVICE) for that shape. */
+ * release = DEVICE (round 6; LAUNCH before): the server process
+ * byteps_server() (server.cc:339-400) starts does nothing else on its GPU,
+ * and device releases now cost a server whose pushes are copied nothing —
+ * ps-lite delivers into host memory (server.cc:174-218), such rounds fold
+ * with launches and no consumer runs (below) — while pushes that land in HBM
+ * (byteps_server_push_ready after an RDMA write into GPU memory) fold at 0.54
+ * of the HBM roofline instead of 0.26-0.29 (config 3's keys from one receive
+ * thread, the bench line's server_cfg3).  BPSR_SERVER_RELEASE=launch keeps
+ * launches. */
 int byteps_server_config_from_env(byteps_server_config* cfg);
 
 /* Device releases (release = DEVICE or BPSR_SERVER_RELEASE=device; sync mode,
  * fused policy, the default engine, num_workers <= 16 — otherwise the server
- * folds with launches): at the first round completion after the
- * init round — when that round came through the slots (push_ready, or
- * blocking pushes of device data); a first round of copied pushes (host data,
- * non-blocking pushes) leaves the server on launches for good — the server
- * builds ONE keyed block queue over every declared key
- * of that key's dtype (each key's receive slots in worker order and its
- * store).  From then on a round's last arrival issues no launch: it stores
- * the key's arrival order and release word from the host when the pushes are
- * in their slots already (byteps_server_push_ready, or blocking pushes of
- * device data, which the copy service lands before they arrive).  A round
- * with pushes still being copied by the lanes (non-blocking pushes, host
- * data) folds with a lane launch behind its copies, and its key passes the
- * epoch's consumer with a skip word: the consumer never waits for lane-stream
- * work.  One consumer launch per epoch folds every key of the queue; it is
- * launched once the previous epoch has begun (its first release), behind that
- * epoch's consumer on the keyed queue, so it is resident and polling when its
- * own first release arrives (an epoch whose consumer was not launched that
- * way is launched by its first release).  A consumer launched ahead whose
- * epoch no round begins within 1 ms is retired: its keys get skip words, it
- * completes, and their next rounds go to the next epoch (byteps_server_stats
- * out[11]).  The consumer folds each key's
- * tiles as soon as that key is released, in its arrival order (the same bits
- * as the launch path).  Each key's last tile stores the epoch into the key's
- * completion word once the key's bytes are visible device-wide, so device
- * views and blocking device pulls (the copy service) of a released round are
- * answered as soon as THAT key is folded, while the consumer still folds
- * others; other pulls wait for the epoch's consumer to complete.  A key whose
- * fold completed stays readable even if the epoch later gives up on another
- * key (see below); the keys then fail on their next call.  Contract: every key of the queue
- * completes one round per epoch (BytePS pushes every key once per
- * iteration); a key that is not pushed within BPSR_SERVER_RELEASE_TIMEOUT_S
- * (default 5) seconds makes that epoch's consumer give up: the keys released
- * in it fail with BYTEPS_REDUCE_ETIMEOUT and the server goes back to launches
- * for good.  Keys declared after the queue was built, and keys of another
- * dtype, always use launches.  While an epoch is in progress its consumer
- * waits on the device for the releases, on a hardware queue of its own: a
- * thread that still has to push must not wait for the whole device
- * (hipDeviceSynchronize, hipFree), nor put work on the legacy NULL stream
- * (it waits for every blocking stream, the consumer's included) — work on
- * non-blocking streams, and stream or event syncs, are fine.  Between rounds
- * such a wait costs at most the 1 ms after which an idle consumer launched
- * ahead is retired. */
+ * folds with launches).  The first round that finishes through the slots
+ * (byteps_server_push_ready, or blocking pushes of device data, which the
+ * copy service lands before they arrive) builds ONE keyed block queue over
+ * every declared key of that key's dtype (each key's receive slots in worker
+ * order and its store); rounds of copied pushes (host data, non-blocking
+ * pushes) before it fold with lane launches and build nothing.  From then on
+ * rounds are grouped into epochs — a key's k-th round after the build is in
+ * its k-th epoch, or later (below) — and each epoch's kind is decided once:
+ *   - a consumer epoch (opened by a slot-written round, or launched ahead):
+ *     ONE consumer launch folds every key of the queue, each key's tiles as
+ *     soon as that key's round is released — a round's last arrival issues no
+ *     launch, it stores the key's arrival order and release word from the
+ *     host — in its arrival order (the same bits as the launch path).  A
+ *     copied round in such an epoch folds with a lane launch behind its
+ *     copies and its key passes the consumer with a skip word: the consumer
+ *     never waits for lane-stream work.
+ *   - a lane epoch (opened by a copied round while no consumer was launched
+ *     for it): no consumer runs; every round in it folds with a lane launch.
+ * Once a consumer epoch has a slot-written round, the next epoch's consumer
+ * is launched behind it on the keyed queue, so it is resident and polling
+ * when that epoch's first release arrives; one launched ahead that no round
+ * begins within 1 ms is retired (its keys get skip words, byteps_server_stats
+ * out[11]).  Each key's last tile stores the epoch into the key's completion
+ * word once the key's bytes are visible device-wide, so device views and
+ * blocking device pulls (the copy service) of a released round are answered
+ * as soon as THAT key is folded, while the consumer still folds others; other
+ * pulls wait for the epoch's consumer to complete.  No key has to be pushed
+ * in every epoch: a consumer epoch still open 100 ms after its first release
+ * (or half of BPSR_SERVER_RELEASE_TIMEOUT_S, if less) is closed — its keys
+ * not released yet get skip words and their rounds go to a later epoch
+ * (out[12]) — so a key that skips an iteration or arrives late holds nobody
+ * and fails nothing, as in the reference, where every key folds on its own.
+ * BPSR_SERVER_RELEASE_TIMEOUT_S (default 5 s) is now the device-side safety
+ * net only: a consumer whose release never comes although the host closed the
+ * epoch gives up, the keys released in it fail with BYTEPS_REDUCE_ETIMEOUT and
+ * the server goes back to launches for good.  Keys declared after the queue
+ * was built, and keys of another dtype, always use launches.  While an epoch
+ * is open its consumer waits on the device for the releases, on a hardware
+ * queue of its own: a thread that still has to push should not wait for the
+ * whole device (hipDeviceSynchronize, hipFree) nor put work on the legacy
+ * NULL stream (it waits for every blocking stream, the consumer's included)
+ * — such a wait lasts until the epoch completes or is closed (at most
+ * 100 ms), or, between rounds, until the idle consumer launched ahead retires
+ * (1 ms).  Work on non-blocking streams, and stream or event syncs, are fine. */
 int byteps_server_create(const byteps_server_config* cfg, byteps_server** out);
 /* The same, for a caller that states the size of its config: every version of
  * byteps_server_config is a prefix of the next (fields are only appended), so
@@ -313,14 +310,14 @@ int byteps_server_order_after(byteps_server* s, const uint64_t* keys, int n, voi
 /* Telemetry since create: out[0] fold launches (single and batched), out[1]
  * rounds folded, out[2] pull copy launches, out[3] pulls answered (copies and
  * views), out[4] ns the lane issuer threads spent issuing, out[5] batched
- * push-copy launches, out[6] keyed consumer epochs a round was released for
+ * push-copy launches, out[6] keyed consumer epochs a round was released into
  * and out[7] rounds released on the device (BPSR_SERVER_RELEASE=device),
  * out[8] blocking pulls served by the pull copy service, out[9] that
- * service's kernel launches, out[10] blocking pushes it served and out[11]
+ * service's kernel launches, out[10] blocking pushes it served, out[11]
  * keyed consumers launched ahead of their epoch and retired because no round
- * began it within 1 ms (each epoch's consumer is launched once the previous
- * epoch has begun, so that it is resident when its first round arrives); the
- * first n (<= 12). */
+ * began it within 1 ms, out[12] consumer epochs closed with keys not pushed
+ * (their rounds went to a later epoch) and out[13] lane epochs (opened by a
+ * copied round: no consumer); the first n (<= 14). */
 int byteps_server_stats(byteps_server* s, uint64_t* out, int n);
 
 /* Batched calls for a transport that delivers many keys at once (co-located

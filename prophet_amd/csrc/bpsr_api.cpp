@@ -1576,6 +1576,13 @@ uint32_t keyq_next_epoch(byteps_reduce_blockq* q, int key) {
   return __atomic_load_n(&q->rel_epoch[(size_t)key], __ATOMIC_ACQUIRE) + 1;
 }
 
+bool keyq_advance(byteps_reduce_blockq* q, uint32_t epoch) {
+  std::lock_guard<std::mutex> g(q->mu);
+  if (q->launch_epoch + 1 != epoch) return false;
+  __atomic_store_n(&q->launch_epoch, epoch, __ATOMIC_RELEASE);
+  return true;
+}
+
 uint32_t keyq_launched(byteps_reduce_blockq* q) {
   return __atomic_load_n(&q->launch_epoch, __ATOMIC_ACQUIRE);
 }

@@ -408,6 +408,9 @@ int keyq_launch(struct byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* st
                 uint32_t* epoch);
 uint32_t keyq_next_epoch(struct byteps_reduce_blockq* q, int key);
 uint32_t keyq_launched(struct byteps_reduce_blockq* q);
+// Pass epoch `epoch` without a launch (the next launch consumes epoch + 1):
+// an epoch no consumer folds.  False unless `epoch` is the next one to launch.
+bool keyq_advance(struct byteps_reduce_blockq* q, uint32_t epoch);
 // Both of the above under one lock.
 void keyq_state(byteps_reduce_blockq* q, int key, uint32_t* next_epoch, uint32_t* launched);
 // `first` (optional): set when this release is the first one of its epoch

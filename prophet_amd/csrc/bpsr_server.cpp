@@ -99,21 +99,28 @@ void completer_main(byteps_server* s, Lane* Lp) {
     if (t.kq_epoch) {
       // a keyed consumer: every pull and view of its epoch waits for this,
       // so poll its event (no other thread makes HIP calls on the device-
-      // release path) for up to 2 ms of a begun epoch before a blocking wait
-      // — a blocking event wait wakes tens of microseconds late.  Once a
+      // release path) — a blocking event wait wakes tens of microseconds
+      // late — with short sleeps once the wait is long.  Once a slot-written
       // round has begun the epoch, the next epoch's consumer is launched
-      // behind it (kq_launch_ahead); an epoch launched so that no round has
-      // begun within kKeyedIdleUs (or at destroy) is retired (kq_retire).
-      const auto i0 = std::chrono::steady_clock::now();
-      auto p0 = i0;
-      bool ahead = false, retired = false;
+      // behind it (kq_launch_ahead).  An epoch that no round begins within
+      // kKeyedIdleUs (or at destroy) is retired (kq_retire); a begun one still
+      // open kKeyedCloseMs later is closed (kq_close_epoch).
+      using clk = std::chrono::steady_clock;
+      const auto i0 = clk::now();
+      auto b0 = i0;  // when this completer saw the epoch begun
+      const auto close_after = std::chrono::microseconds(std::min<int64_t>(
+          (int64_t)byteps_server::kKeyedCloseMs * 1000, (int64_t)(s->kq_timeout_s * 5e5)));
+      bool begun = false, ahead = false, retired = false, closed = false;
       while (hipEventQuery(t.ev) == hipErrorNotReady) {
-        const auto now = std::chrono::steady_clock::now();
-        const bool begun = keyq_opened(s->kq) >= t.kq_epoch;
-        if (begun && !ahead && !retired) {
+        const auto now = clk::now();
+        if (!begun && keyq_opened(s->kq) >= t.kq_epoch) {
+          begun = true;
+          b0 = now;
+        }
+        if (begun && !ahead && !retired &&
+            s->kq_slot_epoch.load(std::memory_order_acquire) >= t.kq_epoch) {
           ahead = true;
           kq_launch_ahead(s, t.kq_epoch);
-          p0 = std::chrono::steady_clock::now();
           continue;
         }
         if (!begun && !retired &&
@@ -122,12 +129,14 @@ void completer_main(byteps_server* s, Lane* Lp) {
           retired = kq_retire(s, t.kq_epoch);
           continue;
         }
-        if (begun && now - p0 > std::chrono::milliseconds(2)) {
-          (void)hipEventSynchronize(t.ev);
-          break;
+        if (begun && !closed && !retired &&
+            (s->kq_stopping.load(std::memory_order_acquire) || now - b0 > close_after)) {
+          closed = true;
+          kq_close_epoch(s, t.kq_epoch);
+          continue;
         }
-        if (!begun && now - i0 > std::chrono::microseconds(100))
-          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (now - (begun ? b0 : i0) > std::chrono::microseconds(100))
+          std::this_thread::sleep_for(std::chrono::microseconds(begun ? 5 : 20));
         else
           for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
       }
@@ -1217,8 +1226,10 @@ int byteps_server_config_from_env(byteps_server_config* cfg) {
   cfg->enable_schedule = (sc && atoi(sc) != 0) ? 1 : 0;
   const char* eb = getenv("BYTEPS_SERVER_ENGINE_BLOCKING");  // server.cc:324
   cfg->engine_blocking = (eb && atoi(eb) != 0) ? 1 : 0;
-  // the dedicated server process: nothing else waits on its GPU (server.h)
-  cfg->release = BYTEPS_SERVER_RELEASE_LAUNCH;  // server.h: why not DEVICE
+  // the dedicated server process: nothing else waits on its GPU, and a server
+  // whose rounds are copied (ps-lite's host buffers) never runs a consumer
+  // (server.h)
+  cfg->release = BYTEPS_SERVER_RELEASE_DEVICE;
   return BYTEPS_REDUCE_OK;
 }
 
@@ -1886,12 +1897,13 @@ int byteps_server_stats(byteps_server* s, uint64_t* out, int n) {
     std::lock_guard<std::mutex> g(s->svc_mu);
     svc_launches = bpsr::copysvc_launches(s->svc);
   }
-  const uint64_t v[12] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
+  const uint64_t v[14] = {s->n_fold_launches.load(), s->n_rounds_folded.load(),
                           s->n_pull_launches.load(), s->n_pulls.load(), s->issuer_ns.load(),
                           s->n_copy_launches.load(), s->n_consumer_launches.load(),
                           s->n_key_releases.load(), s->n_service_pulls.load(), svc_launches,
-                          s->n_service_pushes.load(), s->n_consumer_retired.load()};
-  for (int i = 0; i < n && i < 12; ++i) out[i] = v[i];
+                          s->n_service_pushes.load(), s->n_consumer_retired.load(),
+                          s->n_epochs_closed.load(), s->n_lane_epochs.load()};
+  for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
   return BYTEPS_REDUCE_OK;
 }
 

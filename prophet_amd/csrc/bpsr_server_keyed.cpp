@@ -42,20 +42,21 @@ void build_kq(byteps_server* s, int dtype) {
 }
 
 // Is this finished round of `ks` device-released?  Caller holds ks->mu.
-// The first round finished after the init round decides: pushes already in
-// their slots (push_ready, or device data the copy service landed) build the
-// keyed queue; a round the lanes copied (host data: the ps-lite shape) means
-// the pushes land in host memory, where device releases only add the
-// consumer (config 1: 11.5-13.3 ms per round against 3.1 with launches,
-// r05s55), so the server keeps launches for good.
+// The first round finished through the slots (push_ready, or device data the
+// copy service landed) builds the keyed queue; until then copied rounds (host
+// data: the ps-lite shape) fold with lane launches and build nothing, so a
+// server whose pushes all land in host memory never runs a consumer (config 1
+// took 11.5-13.3 ms per round with one beside its lanes against 3.1, r05s55).
+// Once the queue exists, each epoch's kind decides (key_release).
 bool keyed_member(byteps_server* s, KeyState* ks) {
   if (!s->dev_release || s->kq_off.load()) return false;
   // decided once: no lock from then on (kq_mu is held across the consumer
   // launches, and every round's last arrival asks this)
   if (s->kq_tried.load(std::memory_order_acquire)) return ks->kq_key.load() >= 0;
+  if (ks->round_copied) return false;  // no queue yet: a lane launch
   std::lock_guard<std::mutex> g(s->kq_mu);
   if (!s->kq_tried.load(std::memory_order_relaxed)) {
-    if (!ks->round_copied) build_kq(s, ks->dtype);  // copied: no queue, launches from here on
+    build_kq(s, ks->dtype);
     s->kq_tried.store(true, std::memory_order_release);
   }
   return ks->kq_key.load() >= 0;
@@ -85,7 +86,9 @@ int kq_launch_upto(byteps_server* s, uint32_t need) {
     if (int rc = keyq_launch(s->kq, e, &cs, &got)) return rc;
     s->kq_ev_epoch[slot] = got;
     s->kq_ev_seq[slot] = track_keyed(*s->klane, e, got);
-    s->kq_pub_epoch.store(got, std::memory_order_release);  // the fast path may use it now
+    s->kq_pub_epoch.store(got, std::memory_order_release);
+    s->kq_kind[slot] = byteps_server::kConsumerEpoch;
+    s->kq_decided.store(got, std::memory_order_release);  // the fast path may use it now
   }
   return 0;
 }
@@ -102,80 +105,103 @@ void kq_launch_ahead(byteps_server* s, uint32_t epoch) {
   (void)kq_launch_upto(s, epoch + 1);
 }
 
-// Retire an epoch launched ahead that no round has begun: every key not yet
-// released for it gets a skip word (the tiles pass it, nothing is stored), so
-// the consumer completes at once and its keys' next rounds go to the next
-// epoch, launched by their first release as without the launch ahead.  The
-// epoch is closed first (keyq_close), so a round that begins it from then on
-// is not counted as its first; such a round keeps its place in this epoch
-// (key by key, under the key's lock, as its release is) and is folded by it.
-// False: a round had begun the epoch, which is not retired.
-bool kq_retire(byteps_server* s, uint32_t epoch) {
-  if (!keyq_close(s->kq, epoch)) return false;  // a round began it after all
+// Skip words for every key not yet released for `epoch` (each under its
+// key's lock, as a release is): the epoch's consumer passes them and
+// completes, and those keys' next rounds go to the next epoch.
+static void skip_unreleased(byteps_server* s, uint32_t epoch) {
   const uint64_t skip = ((uint64_t)kKeySkip << 32) | kKeySkip;
   for (KeyState* k : s->kq_keys) {
     std::lock_guard<std::mutex> g(k->mu);
     const int kk = k->kq_key.load();
     if (kk >= 0 && keyq_next_epoch(s->kq, kk) == epoch) (void)keyq_release(s->kq, kk, skip, nullptr);
   }
+}
+
+// Retire an epoch launched ahead that no round has begun (skip_unreleased),
+// so its consumer does not hold its workgroup slots while the caller is idle.
+// The epoch is closed first (keyq_close), so a round that begins it from then
+// on is not counted as its first; such a round keeps its place in this epoch
+// and is folded by it.  False: a round had begun the epoch, which is not
+// retired.
+bool kq_retire(byteps_server* s, uint32_t epoch) {
+  if (!keyq_close(s->kq, epoch)) return false;  // a round began it after all
+  skip_unreleased(s, epoch);
   s->n_consumer_retired.fetch_add(1, std::memory_order_relaxed);
   return true;
 }
 
-// Release a finished round of a keyed key (caller holds ks->mu): the arrival
+// Close a begun epoch whose keys have not all come (kKeyedCloseMs after its
+// first release): the reference folds every key on its own, so a key that
+// skips an iteration — or arrives late — must not hold the others' epoch, nor
+// fail.  Its round, when it comes, is folded by a later epoch.
+void kq_close_epoch(byteps_server* s, uint32_t epoch) {
+  skip_unreleased(s, epoch);
+  s->n_epochs_closed.fetch_add(1, std::memory_order_relaxed);
+}
+
+// Release a finished round of a keyed key (caller holds ks->mu).  The
+// round's epoch is its key's next; its kind is decided by the epoch's first
+// release (or its consumer's launch ahead): a slot-written round opening an
+// epoch launches its consumer, a copied round (`skip`) opening one with no
+// consumer launched makes it a lane epoch.  In a consumer epoch the arrival
 // order and the release word go to the key's block — stored from the host
-// when the round's data is in its slots already (push_ready), or by a one-lane
-// kernel on `stream` behind the round's copies — after the consumer of the
-// block's epoch has been launched (the first release of an epoch launches
-// it).  Then the round is published like an issued fold.  Returns 1 when
-// device releases were turned off meanwhile (the caller folds with a launch).
+// when the round's data is in its slots already (push_ready), or by a
+// one-lane kernel on `stream` behind the round's copies — and the round is
+// published like an issued fold; a copied round passes the consumer with a
+// skip word.  In a lane epoch every round gets a skip word and folds with a
+// lane launch.  Returns 1 when the caller must fold the round with a launch
+// (a lane epoch, or device releases turned off meanwhile).
 int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
                 bool skip) {
   uint64_t perm = 0;  // position m's worker in bits 4m..4m+3 (16 positions)
   for (size_t m = 0; m < order.size(); ++m) perm |= (uint64_t)order[m] << (4 * m);
   if (skip) perm = ((uint64_t)kKeySkip << 32) | kKeySkip;
-  hipEvent_t ev = nullptr;
-  uint64_t seq = 0;
   bool first = false;  // the first round released for its epoch
   const int kk = ks->kq_key.load();
-  uint32_t need = keyq_next_epoch(s->kq, kk);
+  const uint32_t need = keyq_next_epoch(s->kq, kk);
+  const int slot = (int)(need % byteps_server::kKqRing);
   Lane& RL = *s->lanes[ks->lane];
-  if (!s->kq_off.load() && s->kq_pub_epoch.load(std::memory_order_acquire) >= need) {
-    // the epoch's consumer is launched and its slot published: no lock (the
-    // slot cannot be reused before this epoch completes, which needs this key)
-    const int slot = (int)(need % byteps_server::kKqRing);
-    ev = s->kq_ev[slot];
-    seq = s->kq_ev_seq[slot];
-    if (stream) {
-      RL.where = "key_release: wait d2h";
-      // behind the lane's pull copies too (a store is rewritten by the fold)
-      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
-      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
-      RL.where = "key_release: release kernel";
-    }
-    if (int rc = keyq_release(s->kq, kk, perm, stream, &first)) return rc;
-  } else {
+  if (s->kq_off.load()) return 1;
+  if (s->kq_decided.load(std::memory_order_acquire) < need) {
+    // this release opens epoch `need` (no lock otherwise: a decided epoch's
+    // kind and ring slot stay put until it completes, which needs this key)
     if (stream) RL.where = "key_release: kq_mu";
     std::lock_guard<std::mutex> g(s->kq_mu);
     if (stream) RL.where = "key_release: launch";
     if (s->kq_off.load()) return 1;
-    uint32_t launched = 0;
-    keyq_state(s->kq, kk, &need, &launched);
-    if (int rc = kq_launch_upto(s, need)) return rc;
-    if (stream) {
-      RL.where = "key_release: wait d2h";
-      const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
-      if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
-      RL.where = "key_release: release kernel";
+    if (s->kq_decided.load(std::memory_order_relaxed) < need) {
+      if (skip && keyq_launched(s->kq) < need) {
+        if (!keyq_advance(s->kq, need))
+          return fail(BYTEPS_REDUCE_EARGS, "device releases: epoch %u opened out of order", need);
+        s->kq_kind[slot] = byteps_server::kLaneEpoch;
+        s->kq_decided.store(need, std::memory_order_release);
+        s->n_lane_epochs.fetch_add(1, std::memory_order_relaxed);
+      } else if (int rc = kq_launch_upto(s, need)) {
+        return rc;
+      }
     }
-    if (int rc = keyq_release(s->kq, kk, perm, stream, &first)) return rc;
-    const int slot = (int)(need % byteps_server::kKqRing);
-    ev = s->kq_ev[slot];
-    seq = s->kq_ev_seq[slot];
   }
+  if (s->kq_kind[slot] == byteps_server::kLaneEpoch) {
+    const uint64_t sk = ((uint64_t)kKeySkip << 32) | kKeySkip;
+    if (int rc = keyq_release(s->kq, kk, sk, nullptr)) return rc;
+    return skip ? 0 : 1;
+  }
+  const hipEvent_t ev = s->kq_ev[slot];
+  const uint64_t seq = s->kq_ev_seq[slot];
+  if (stream) {
+    RL.where = "key_release: wait d2h";
+    // behind the lane's pull copies too (a store is rewritten by the fold)
+    const hipError_t we = hipStreamWaitEvent(stream, RL.d2h_mark, 0);
+    if (we != hipSuccess) return hip_fail(we, "hipStreamWaitEvent");
+    RL.where = "key_release: release kernel";
+  }
+  if (int rc = keyq_release(s->kq, kk, perm, stream, &first)) return rc;
   if (stream) RL.where = "key_release: publish";
   if (first) s->n_consumer_launches.fetch_add(1, std::memory_order_relaxed);
   if (skip) return 0;  // the round is folded by a lane launch, which publishes it
+  uint32_t se = s->kq_slot_epoch.load(std::memory_order_relaxed);
+  while (se < need && !s->kq_slot_epoch.compare_exchange_weak(se, need)) {
+  }
   s->n_key_releases.add();
   ks->kq_round_epoch = need;
   return finish_round(s, ks, order, /*mark=*/false, ev, seq, /*keyed=*/true);

@@ -365,6 +365,24 @@ struct byteps_server {
   std::mutex kq_park_mu;
   std::atomic<uint64_t> kq_done_seq{0};
   std::atomic<uint32_t> kq_pub_epoch{0};  // epochs launched with their kq_ev slot written
+  // Per-epoch release choice (round 6): an epoch's kind is decided in epoch
+  // order, by its first release or by its consumer's launch (ahead): a
+  // consumer epoch is folded by a keyed consumer launch; a lane epoch — opened
+  // by a copied round while no consumer was launched for it — has none, and
+  // every round in it folds with a lane launch (its keys only get skip words,
+  // which keep their epochs in step).  kq_kind[e % kKqRing] is written before
+  // kq_decided publishes e.
+  static constexpr uint8_t kConsumerEpoch = 1, kLaneEpoch = 2;
+  uint8_t kq_kind[kKqRing] = {};
+  std::atomic<uint32_t> kq_decided{0};
+  // the highest epoch a slot-written round was released into (a consumer
+  // epoch with one launches its successor ahead; an all-copied one does not)
+  std::atomic<uint32_t> kq_slot_epoch{0};
+  // a consumer epoch still open this long after its first release is closed:
+  // its keys not released yet get skip words and their rounds go to the next
+  // epoch (kq_close_epoch) — no key has to be pushed in every epoch
+  static constexpr int kKeyedCloseMs = 100;
+  std::atomic<uint64_t> n_epochs_closed{0}, n_lane_epochs{0};
   std::vector<bpsr::PullJob> kq_parked; // pulls of keyed rounds not published yet (kq_park_mu)
   std::atomic<uint64_t> n_consumer_launches{0};  // epochs a round was released for
   std::atomic<uint64_t> n_consumer_retired{0};   // epochs launched ahead and retired idle
@@ -429,6 +447,7 @@ int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, h
 int kq_launch_upto(byteps_server* s, uint32_t need);
 void kq_launch_ahead(byteps_server* s, uint32_t epoch);
 bool kq_retire(byteps_server* s, uint32_t epoch);
+void kq_close_epoch(byteps_server* s, uint32_t epoch);
 void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq);
 void wait_published(byteps_server* s, KeyState* ks, uint64_t seq);
 int execute(byteps_server* s, const FoldJob& j);

@@ -366,13 +366,14 @@ class PSServer:
 
     def stats(self) -> dict:
         """Launch telemetry since create (byteps_server_stats)."""
-        out = (_u64 * 12)()
-        _check(self.lib.byteps_server_stats(self.handle, out, 12))
+        out = (_u64 * 14)()
+        _check(self.lib.byteps_server_stats(self.handle, out, 14))
         return {"fold_launches": out[0], "rounds_folded": out[1], "pull_launches": out[2],
                 "pulls": out[3], "issuer_ns": out[4], "push_copy_launches": out[5],
                 "consumer_launches": out[6], "key_releases": out[7],
                 "service_pulls": out[8], "service_launches": out[9],
-                "service_pushes": out[10], "consumers_retired": out[11]}
+                "service_pushes": out[10], "consumers_retired": out[11],
+                "epochs_closed": out[12], "lane_epochs": out[13]}
 
     # batched calls (server.h): one lane-wide launch for many keys
     def push_ready_many(self, keys, worker: int) -> None:

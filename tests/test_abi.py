@@ -151,10 +151,11 @@ def test_server_config_and_errors_without_gpu(monkeypatch):
     assert c.engine_blocking == 1
     monkeypatch.setenv("BYTEPS_SERVER_ENGINE_BLOCKING", "0")
     assert server.config_from_env().engine_blocking == 0
-    # the dedicated server process receives into host memory: launches (server.h)
-    assert c.release == server.RELEASE_LAUNCH
-    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")   # read at create, not here
-    assert server.config_from_env().release == server.RELEASE_LAUNCH
+    # the dedicated server process: device releases (round 6, server.h — its
+    # copied rounds run no consumer, its slot-written ones fold on the device)
+    assert c.release == server.RELEASE_DEVICE
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "launch")   # read at create, not here
+    assert server.config_from_env().release == server.RELEASE_DEVICE
     lib = server._lib()
     bad = server.ServerConfig(0, 4, 0, 0, 0)
     h = ctypes.c_void_p()

@@ -1819,7 +1819,9 @@ def test_device_release_rounds_bit_exact(port, N, dt, monkeypatch):
     import os
     copied = 1 if os.environ.get("BPSR_SERVER_PULL_SERVICE", "1") != "0" else 2
     assert st["key_releases"] == (R - copied) * len(keys)
-    assert st["consumer_launches"] == R                          # one launch per epoch
+    # one epoch per round: a consumer epoch, or — the copied round, when the
+    # consumer launched ahead for it retired idle first — a lane epoch
+    assert st["consumer_launches"] + st["lane_epochs"] == R, st
     assert 1 <= st["fold_launches"] - st0["fold_launches"] <= copied * len(keys)
 
 
@@ -1898,17 +1900,17 @@ def test_device_release_epoch_launched_ahead_and_retired(port, monkeypatch):
     assert sync_s < 1.0 and close_s < 1.0, (sync_s, close_s)
 
 
-@pytest.mark.parametrize("release", [None, "device"], ids=["env-default", "device"])
+@pytest.mark.parametrize("release", [None, "launch"], ids=["env-default", "launch"])
 def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
     """The dedicated server process (server.cc:339-400) builds its server from
-    the environment (byteps_server_config_from_env): launches by default (its
-    pushes land in host memory, server.h), and BPSR_SERVER_RELEASE=device
-    turns device releases on — one consumer launch per round, no fold
-    launches.  4 workers, push_ready rounds from the slots, pulls into device
-    memory: bit-exact with the oracle's left fold in the recorded order either
-    way."""
+    the environment (byteps_server_config_from_env): device releases by
+    default (round 6: a server whose pushes are copied runs no consumer, and
+    no key has to come every epoch, server.h) — one consumer launch per
+    round, no fold launches — and BPSR_SERVER_RELEASE=launch keeps launches.
+    4 workers, push_ready rounds from the slots, pulls into device memory:
+    bit-exact with the oracle's left fold in the recorded order either way."""
     from prophet_amd.reducer import GpuReducer
-    from prophet_amd.server import RELEASE_LAUNCH, PSServer
+    from prophet_amd.server import RELEASE_DEVICE, PSServer
     monkeypatch.delenv("BPSR_SERVER_RELEASE", raising=False)
     if release:
         monkeypatch.setenv("BPSR_SERVER_RELEASE", release)
@@ -1918,7 +1920,7 @@ def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
     keys = [11, 12, 13]
     es = elem_size(dt)
     srv = PSServer.from_env()
-    assert srv.cfg.release == RELEASE_LAUNCH and srv.cfg.num_workers == N
+    assert srv.cfg.release == RELEASE_DEVICE and srv.cfg.num_workers == N
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(device=dev)      # never the legacy NULL stream (server.h)
     with torch.cuda.stream(st):
@@ -1950,7 +1952,7 @@ def test_server_from_env_folds_by_device_releases(port, release, monkeypatch):
                 st0 = srv.stats()
     s1 = srv.stats()
     srv.close()
-    if release == "device":
+    if release is None:
         assert s1["consumer_launches"] == R and s1["key_releases"] == R * len(keys)
         assert s1["fold_launches"] == st0["fold_launches"]
     else:
@@ -2004,56 +2006,74 @@ def test_order_after_orders_device_released_push_ready(port, monkeypatch):
     assert np.array_equal(got, want)
 
 
-def test_device_release_server_with_copied_rounds_keeps_launches(port, monkeypatch):
-    """Device releases on, but the first round after the init round is copied
-    (pushes from host memory, the ps-lite shape): the server builds no keyed
-    queue and folds every round with launches — no consumer waits beside the
-    lanes (config 1 took 4x longer with one, r05s55) — and the later
-    push_ready rounds stay on launches too; every pull exact."""
+def test_device_release_server_mixed_copied_and_slot_written_rounds(port, monkeypatch):
+    """Device releases on, the per-epoch release choice (server.h): copied
+    rounds (pushes from host memory, the ps-lite shape) before any round comes
+    through the slots fold with launches and build no keyed queue — no
+    consumer waits beside the lanes (config 1 took 4x longer with one, r05s55);
+    the first push_ready round builds it; from then on an epoch opened by a
+    copied round is a lane epoch (no consumer) and one opened by a
+    slot-written round a consumer epoch.  Rounds: init (copied), copied,
+    push_ready, push_ready, copied, copied, push_ready: every pull exact
+    against the oracle's fold in the recorded order; the slot-written rounds
+    are device-released, the copied ones fold with launches, and the copied
+    run after the queue exists has at least one lane epoch."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
     dt, N, n = DType.FLOAT32, 2, 70_001
     srv = PSServer(N)
     dev = torch.device("cuda:0")
     out = np.zeros(n * 4, np.uint8)
-    for r in range(4):
-        for k in (1, 2):
-            if r < 2:                                        # init round + a copied round
+    kinds = ["copied", "copied", "slot", "slot", "copied", "copied", "slot"]
+    stats = []
+    for r, kind in enumerate(kinds):
+        if kind == "copied":                             # host data: copied by the lanes
+            for k in (1, 2):
                 ts = [threading.Thread(target=srv.push, args=(k, w, data(dt, n, w, r, k), dt))
                       for w in range(N)]
                 for t in ts:
                     t.start()
                 for t in ts:
                     t.join(timeout=60)
-            else:                                            # then push_ready rounds
-                for w in range(N):                           # (no consumer runs: a NULL-
-                    x = torch.from_numpy(data(dt, n, w, r, k)).to(dev)   # stream copy is fine)
-                    _ptr_copy(srv.recv_slot(k, w), x)
-                    torch.cuda.current_stream(dev).synchronize()
+        else:                                            # the transport wrote the slots, all
+            for k in (1, 2):                             # before the first release (a NULL-
+                for w in range(N):                       # stream copy waits for a running
+                    x = torch.from_numpy(data(dt, n, w, r, k)).to(dev)   # consumer; one
+                    _ptr_copy(srv.recv_slot(k, w), x)    # launched ahead and idle retires
+            torch.cuda.current_stream(dev).synchronize()  # within 1 ms)
+            for k in (1, 2):
+                for w in range(N):
                     srv.push_ready(k, w)
-        if r == 0:                                           # the init round has no pulls
-            continue
-        for k in (1, 2):
-            want = np.zeros(n * 4, np.uint8)
-            port.sum_n(want, [data(dt, n, w, r, k) for w in srv.key_info(k)[2]], n * 4, dt)
-            for w in range(N):
-                srv.pull(k, out)
-                assert np.array_equal(out, want), (r, k, w)
-    st = srv.stats()
+        if r > 0:                                        # the init round has no pulls
+            for k in (1, 2):
+                want = np.zeros(n * 4, np.uint8)
+                port.sum_n(want, [data(dt, n, w, r, k) for w in srv.key_info(k)[2]], n * 4, dt)
+                for w in range(N):
+                    srv.pull(k, out)
+                    assert np.array_equal(out, want), (r, kind, k, w)
+        stats.append(srv.stats())
     srv.close()
-    assert st["consumer_launches"] == 0 and st["key_releases"] == 0
+    # copied rounds before the first slot-written one: launches, no queue
+    assert stats[1]["key_releases"] == 0 and stats[1]["consumer_launches"] == 0, stats[1]
+    slots = sum(1 for k in kinds if k == "slot")
+    assert stats[-1]["key_releases"] == 2 * slots, stats[-1]
+    for r in (4, 5):                                     # copied rounds: lane folds
+        assert stats[r]["fold_launches"] > stats[r - 1]["fold_launches"], (r, stats)
+        assert stats[r]["key_releases"] == stats[r - 1]["key_releases"], (r, stats)
+    assert stats[-1]["lane_epochs"] >= 1, stats[-1]
 
 
-def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
-    """The keyed queue's contract: every key completes one round per epoch.  A
-    round in which one key is never pushed makes that epoch's consumer give up
-    after BPSR_SERVER_RELEASE_TIMEOUT_S: the key released in it fails with
-    ETIMEOUT (no stale data), the server turns device releases off, and the
-    late key's round then folds with a launch, exactly.  Round 0 (init) is
-    copied pushes; round 1 is push_ready, so the first finished round builds
-    the keyed queue (a server whose first round is copied keeps launches:
-    test_device_release_server_with_copied_rounds_keeps_launches)."""
-    from prophet_amd.reducer import ETIMEOUT, ReduceError
+def test_device_release_epoch_closes_for_a_missing_key(port, monkeypatch):
+    """No key has to be pushed in every epoch (server.h): a round in which
+    key 2 is not pushed in time leaves its epoch open only until the host
+    closes it, 100 ms after its first release — key 2 gets a skip word, key
+    1's round is folded and pulled exactly, nothing fails (the reference folds
+    every key on its own) and device releases stay on.  Key 2's late round
+    (copied pushes) then folds exactly in a later epoch; every later round is
+    exact, and the keys' rounds are device-released in one epoch again by
+    round 4.  Round 0 (init) is copied pushes,
+    round 1 push_ready (the first slot-written round builds the keyed queue).
+    The device timeout is set low (0.5 s) to show the host close comes first."""
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
     monkeypatch.setenv("BPSR_SERVER_RELEASE_TIMEOUT_S", "0.5")
@@ -2067,36 +2087,50 @@ def test_device_release_timeout_fails_loudly_then_launches(port, monkeypatch):
         for t in ts:
             t.join(timeout=60)
     dev = torch.device("cuda:0")
-    for k in (1, 2):                                     # round 1: push_ready, both keys; every
-        for w in range(N):                               # slot written before the first release
-            x = torch.from_numpy(data(dt, n, w, 1, k)).to(dev)   # (the epoch's consumer then
-            _ptr_copy(srv.recv_slot(k, w), x)                   # runs; work on this NULL
-    torch.cuda.current_stream(dev).synchronize()                # stream would wait for it)
-    for k in (1, 2):
-        for w in range(N):
-            srv.push_ready(k, w)
     out = np.zeros(n * 4, np.uint8)
-    for k in (1, 2):
+
+    def slot_round(r, keys):
+        for k in keys:                                   # every slot written before the
+            for w in range(N):                           # first release (the epoch's consumer
+                x = torch.from_numpy(data(dt, n, w, r, k)).to(dev)   # then waits; NULL-stream
+                _ptr_copy(srv.recv_slot(k, w), x)                   # work would wait for it)
+        torch.cuda.current_stream(dev).synchronize()
+        for k in keys:
+            for w in range(N):
+                srv.push_ready(k, w)
+
+    def check(r, k):
+        want = np.zeros(n * 4, np.uint8)
+        port.sum_n(want, [data(dt, n, w, r, k) for w in srv.key_info(k)[2]], n * 4, dt)
         for w in range(N):
             srv.pull(k, out)
-    # round 2: key 1 only, written into its slots by the "transport" and
-    # released from the host (push_ready) — a device-released round; key 2
-    # never comes.  (Copied pushes would fold with a lane launch and pass the
-    # consumer with a skip word, so they could not show the timeout.)
-    for w in range(N):
-        x = torch.from_numpy(data(dt, n, w, 2, 1)).to(dev)
-        _ptr_copy(srv.recv_slot(1, w), x)
-        torch.cuda.current_stream(dev).synchronize()   # before the epoch opens
-    for w in range(N):
-        srv.push_ready(1, w)
-    with pytest.raises(ReduceError) as e:
-        srv.pull(1, out)
-    assert e.value.code == ETIMEOUT
-    for w in range(N):                                   # key 2's round 2, late: a launch
+            assert np.array_equal(out, want), (r, k, w)
+
+    slot_round(1, (1, 2))
+    for k in (1, 2):
+        check(1, k)
+    # round 2: key 1 only; key 2 does not come before the epoch closes
+    t0 = time.time()
+    slot_round(2, (1,))
+    check(2, 1)                                          # answered once the epoch is closed
+    waited = time.time() - t0
+    for w in range(N):                                   # key 2's round 2, late, copied
         srv.push(2, w, data(dt, n, w, 2, 2), dt)
-    srv.pull(2, out)
-    want = np.zeros(n * 4, np.uint8)
-    port.sum_n(want, [data(dt, n, w, 2, 2) for w in srv.key_info(2)[2]], n * 4, dt)
-    assert np.array_equal(out, want)
-    assert srv.stats()["consumer_launches"] == 2
+    check(2, 2)
+    st2 = srv.stats()
+    # Epochs are not rounds: key 2's late round went to the epoch after the
+    # closed one, where key 1's round 3 lands too, so round 3 of the two keys
+    # sits in neighbouring epochs (key 1's may be a lane epoch, opened by key
+    # 2's copied round) until a close skips key 1 once more; round 4 is in step.
+    slot_round(3, (1, 2))
+    for k in (1, 2):
+        check(3, k)
+    st3 = srv.stats()
+    slot_round(4, (1, 2))
+    for k in (1, 2):
+        check(4, k)
+    st4 = srv.stats()
     srv.close()
+    assert st2["epochs_closed"] >= 1, st2
+    assert waited < 0.45, waited                         # the host close, not the device timeout
+    assert st4["key_releases"] - st3["key_releases"] == 2, (st3, st4)   # in step again
