@@ -714,7 +714,14 @@ struct byteps_reduce_blockq {
   uint32_t* khdone = nullptr;       // pinned host, one completion word per block
   uint32_t* khdone_dev = nullptr;
   uint32_t opened = 0;              // highest epoch a round was released for (keyq_opened)
+#ifdef BPSR_KEYED_TRACE
+  unsigned long long* ktrace = nullptr;  // probe builds: kKtraceSlots launches' stamps
+  size_t ktrace_per = 0;
+#endif
 };
+#ifdef BPSR_KEYED_TRACE
+constexpr uint32_t kKtraceSlots = 64;
+#endif
 
 // Per device, created on first use, never destroyed: three consumer queues
 // (all-CU-masked streams, each a hardware queue of its own; queue 0 is
@@ -736,6 +743,7 @@ struct ConsumerDev {
   uint64_t qid[3] = {0, 0, 0};
   hipStream_t rq = nullptr;
   uint64_t rqid = 0;
+
   std::vector<std::pair<hipStream_t, uint64_t>> spare;
   uint64_t* idw = nullptr;              // pinned word read_queue_id writes (host view)
   uint64_t* idw_dev = nullptr;          // ... its device view
@@ -989,7 +997,35 @@ static hipError_t flush_joins(byteps_reduce_blockq* q, bool all) {
   return e;
 }
 
+#ifdef BPSR_KEYED_TRACE
+// Probe builds: the keyed consumer's stamps to $BPSR_KEYED_TRACE_OUT — a
+// header (launch epoch, slots, words per slot, tiles, keys, clock kHz), the
+// tiles' first records (block_first), then the slots.
+static void dump_ktrace(byteps_reduce_blockq* q) {
+  const char* path = getenv("BPSR_KEYED_TRACE_OUT");
+  if (!q->ktrace || !path) return;
+  (void)hipDeviceSynchronize();
+  std::vector<unsigned long long> buf(q->ktrace_per * kKtraceSlots);
+  std::vector<uint32_t> bf((size_t)q->nblocks + 1);
+  if (hipMemcpy(buf.data(), q->ktrace, 8 * buf.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+  if (hipMemcpy(bf.data(), q->flags + q->nblocks, 4 * bf.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  FILE* f = fopen(path, "wb");
+  if (!f) return;
+  const unsigned long long hdr[6] = {q->launch_epoch, kKtraceSlots, q->ktrace_per, q->ti.tiles,
+                                     (unsigned long long)q->nblocks, q->clock_khz};
+  fwrite(hdr, 8, 6, f);
+  fwrite(bf.data(), 4, bf.size(), f);
+  fwrite(buf.data(), 8, buf.size(), f);
+  fclose(f);
+}
+#endif
+
 static void blockq_free(byteps_reduce_blockq* q) {
+#ifdef BPSR_KEYED_TRACE
+  dump_ktrace(q);
+  if (q->ktrace) (void)hipFree(q->ktrace);
+#endif
   // a launch still waiting for releases ends at its timeout at the latest
   for (auto& p : q->pend_join) {
     (void)hipEventSynchronize(p.ev);
@@ -1483,8 +1519,9 @@ int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double 
   q->wide = wide;
   if (timeout_s > 0) q->timeout_s = timeout_s;
   const size_t nw = (size_t)nkeys * (wide ? 2 : 1);  // words per copy (device / host parity)
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q->kwords), sizeof(uint64_t) * nw);
-  if (e == hipSuccess) e = hipMemset(q->kwords, 0, sizeof(uint64_t) * nw);
+  const size_t kbytes = sizeof(uint64_t) * nw * kKeyWordStride;  // one word per line
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&q->kwords), kbytes);
+  if (e == hipSuccess) e = hipMemset(q->kwords, 0, kbytes);
   void* p = nullptr;
   void* d = nullptr;
   if (e == hipSuccess)
@@ -1495,8 +1532,9 @@ int keyq_create(const byteps_bucket_desc* buckets, int nkeys, int dtype, double 
     e = hipHostGetDevicePointer(&d, p, 0);
     q->khwords_dev = static_cast<uint64_t*>(d);
   }
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->kcnt), sizeof(uint32_t) * (size_t)nkeys);
-  if (e == hipSuccess) e = hipMemset(q->kcnt, 0, sizeof(uint32_t) * (size_t)nkeys);
+  const size_t cbytes = sizeof(uint32_t) * (size_t)nkeys * kKeyCntStride;  // one per line
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&q->kcnt), cbytes);
+  if (e == hipSuccess) e = hipMemset(q->kcnt, 0, cbytes);
   if (e == hipSuccess)
     e = hipHostMalloc(&p, sizeof(uint32_t) * (size_t)nkeys, hipHostMallocCoherent | hipHostMallocMapped);
   if (e == hipSuccess) {
@@ -1547,6 +1585,16 @@ int keyq_launch(byteps_reduce_blockq* q, hipEvent_t stop, hipStream_t* stream, u
   Q.kcnt = q->kcnt;
   Q.khdone = q->khdone_dev;
   Q.grid = q->ti.tiles + 1;
+#ifdef BPSR_KEYED_TRACE
+  if (!q->ktrace) {
+    q->ktrace_per = 4 * (size_t)q->ti.tiles + (size_t)q->nblocks;
+    if (hipMalloc(reinterpret_cast<void**>(&q->ktrace), 8 * q->ktrace_per * kKtraceSlots) != hipSuccess)
+      return fail(BYTEPS_REDUCE_EHIP, "keyed trace buffer");
+    (void)hipMemset(q->ktrace, 0, 8 * q->ktrace_per * kKtraceSlots);
+    (void)hipDeviceSynchronize();
+  }
+  Q.ktrace = q->ktrace + (size_t)(ep % kKtraceSlots) * q->ktrace_per;
+#endif
   // Residency: at most 2 consumer workgroups per CU, and room left beside
   // them for the work a missing release may still need — a push copy into a
   // slot (the copy kernel asks for 40 KiB of LDS) or a release kernel: 58 KiB
@@ -1605,8 +1653,9 @@ int keyq_release(byteps_reduce_blockq* q, int key, uint64_t perm, hipStream_t s,
   const uint64_t w2 = key_word((uint32_t)(perm >> 32), ep);  // wide: positions 8..15
   const size_t second = (size_t)q->nblocks + (size_t)key;
   if (s) {
-    const hipError_t e = launch_key_release(q->kwords, (uint32_t)key, w,
-                                            q->wide ? q->kwords + second : nullptr, w2, s);
+    const hipError_t e =
+        launch_key_release(q->kwords, (uint32_t)key * kKeyWordStride, w,
+                           q->wide ? q->kwords + second * kKeyWordStride : nullptr, w2, s);
     if (e != hipSuccess) return hip_fail(e, "keyed release");
   } else {
     // the second word first: the helper forwards a block once both carry the epoch
@@ -1640,7 +1689,8 @@ bool keyq_failed(byteps_reduce_blockq* q) {
 std::string keyq_debug(byteps_reduce_blockq* q) {
   std::lock_guard<std::mutex> g(q->mu);
   std::vector<uint64_t> dev((size_t)q->nblocks);
-  const hipError_t e = hipMemcpy(dev.data(), q->kwords, dev.size() * 8, hipMemcpyDeviceToHost);
+  const hipError_t e = hipMemcpy2D(dev.data(), 8, q->kwords, 8 * kKeyWordStride, 8, dev.size(),
+                                  hipMemcpyDeviceToHost);
   char buf[512];
   int dev_at = 0, rel_at = 0, host_at = 0;
   const uint32_t ep = q->launch_epoch;

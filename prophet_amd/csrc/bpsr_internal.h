@@ -136,6 +136,12 @@ struct BlockqLaunch {
   // on entry; a launch on another stream is gated on the count
   // (launch_seq_gate).  Null in a captured launch.
   unsigned long long* started;
+#ifdef BPSR_KEYED_TRACE
+  // Probe builds only (tools/dbg/build_keyed_trace_lib.sh): the keyed
+  // consumer's wall_clock64() stamps — per tile entry, word seen, folded,
+  // counted; then per key the helper's forward.
+  unsigned long long* ktrace;
+#endif
 };
 constexpr uint32_t kSeqLast = 8;  // one per XCD: workgroups are dealt round-robin over 8
 inline uint32_t seq_counted(uint32_t grid) { return grid < kSeqLast ? grid : kSeqLast; }
@@ -149,6 +155,13 @@ hipError_t launch_seq_gate(const unsigned long long* started, unsigned long long
 // word (wide queues, 9..16 sources); kKeySkip: the round is folded
 // elsewhere, the tiles only pass.
 constexpr uint32_t kKeySkip = 0xffffffffu;
+// A keyed queue's device words lie one per 128-B line (word b at
+// kwords[b * kKeyWordStride], a wide queue's second words after the first
+// ones): the tiles polling one key's word, and the helper storing the next,
+// do not queue on the same few lines (round 6).
+constexpr uint32_t kKeyWordStride = 16;
+// ... and its tile counters one per 128-B line too (kcnt[b * kKeyCntStride]).
+constexpr uint32_t kKeyCntStride = 32;
 constexpr int kKeyedMaxSrcs = 16;
 constexpr int kKeyedNarrowSrcs = 8;   // one word per block
 inline uint64_t key_word(uint32_t perm, uint32_t epoch) {
@@ -286,7 +299,8 @@ hipError_t launch_blockq(const BlockqLaunch& Q, int vpt, int pol, size_t lds, bo
                          int dtype, int mode, hipStream_t s);
 hipError_t launch_blockq_release(uint32_t* flags, uint32_t first, uint32_t count, uint32_t epoch,
                                  hipStream_t s);
-// Stream-ordered keyed release: kwords[block] = word (system scope, release);
+// Stream-ordered keyed release: kwords[block] = word (system scope, release;
+// block: the word's index, key * kKeyWordStride);
 // a wide queue's second word first (word2_at = &kwords[nblocks + block], else
 // null).
 hipError_t launch_key_release(uint64_t* kwords, uint32_t block, uint64_t word,

@@ -694,14 +694,20 @@ __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
   const uint64_t t0 = wall_clock64();
   for (;;) {
     bool pending = false;
+    const uint32_t err = ld_err(Q);  // with the sweep's loads, not after them
     for (uint32_t base = first; base < Q.nblocks; base += kBlock) {
       const uint32_t b = base + lane;
-      if (b < Q.nblocks && (uint32_t)ld_agent64(Q.kwords + b) != Q.epoch) {
-        const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);
-        // a wide queue's second words follow the first ones (the host stores
-        // the second before the first; a tile checks the second's epoch too)
-        const uint64_t h2 =
-            Q.wide ? ld_sys64(Q.khwords + 2 * (uint64_t)(Q.nblocks + b) + par) : 0;
+      if (b >= Q.nblocks) continue;
+      // the device word and the host words load together (one PCIe round
+      // trip per sweep, not a device load and then a dependent host load):
+      // a release waits at most one sweep before its tiles see it
+      const uint64_t d = ld_agent64(Q.kwords + (uint64_t)b * kKeyWordStride);
+      const uint64_t h = ld_sys64(Q.khwords + 2 * (uint64_t)b + par);
+      // a wide queue's second words follow the first ones (the host stores
+      // the second before the first; a tile checks the second's epoch too)
+      const uint64_t h2 =
+          Q.wide ? ld_sys64(Q.khwords + 2 * (uint64_t)(Q.nblocks + b) + par) : 0;
+      if ((uint32_t)d != Q.epoch) {
         // relaxed: the word publishes no data of this workgroup (the round's
         // data landed before the host's store), and a release at system
         // scope would write back the XCD's whole L2 — once per key, while the
@@ -709,9 +715,13 @@ __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
         // 0.49 ms instead of ~0.1 for config 3's 165 keys)
         if ((uint32_t)h == Q.epoch && (!Q.wide || (uint32_t)h2 == Q.epoch)) {
           if (Q.wide)
-            __hip_atomic_store(Q.kwords + Q.nblocks + b, h2, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(Q.kwords + b, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(Q.kwords + (uint64_t)(Q.nblocks + b) * kKeyWordStride, h2,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(Q.kwords + (uint64_t)b * kKeyWordStride, h, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+#ifdef BPSR_KEYED_TRACE
+          Q.ktrace[4 * (uint64_t)Q.L.tiles + b] = wall_clock64();
+#endif
         } else {
           pending = true;
         }
@@ -720,7 +730,7 @@ __device__ __forceinline__ void forward_host_keys(const BlockqLaunch& Q) {
     if (__ballot(pending) == 0) return;
     // a tile gave up, or this wave does: the host reads the mirror word
     const bool late = wall_clock64() - t0 > Q.timeout_ticks;
-    if (late || ld_err(Q)) {
+    if (late || err) {
       if (lane == 0) {
         __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(Q.herr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -754,6 +764,8 @@ struct PermSrcs16 {
 // for full tiles of a write-through launch; any other tile also writes back
 // its XCD's L2 first), one lane counts the tile for its block, and the
 // block's last tile of the epoch stores the epoch into the block's host word.
+// (Counting per wave without waiting, with the helper publishing completion,
+// measured slower: 0.130 against 0.108 ms per config-3 round, r06s33.)
 template <int NT>
 __device__ __forceinline__ void key_tile_done(const BlockqLaunch& Q, uint32_t blk,
                                               bool written_through) {
@@ -765,8 +777,8 @@ __device__ __forceinline__ void key_tile_done(const BlockqLaunch& Q, uint32_t bl
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     const uint32_t nt = Q.block_first[blk + 1] - Q.block_first[blk];
-    const uint32_t old =
-        __hip_atomic_fetch_add(Q.kcnt + blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t old = __hip_atomic_fetch_add(Q.kcnt + (uint64_t)blk * kKeyCntStride, 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((old + 1) % nt == 0)
       __hip_atomic_store(Q.khdone + blk, Q.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -780,16 +792,21 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
     return;
   }
   const uint32_t t = blockIdx.x - Q.helper;
+#ifdef BPSR_KEYED_TRACE
+  unsigned long long* kt = Q.ktrace + 4 * (uint64_t)t;
+  if (threadIdx.x == 0) kt[0] = wall_clock64();
+#endif
   const unsigned char* rec = Q.L.recs + (uint64_t)t * Q.L.rec_stride;
   const RecRegs r = load_record(rec);
   const uint32_t blk = reinterpret_cast<const TileHead*>(rec)->block;
   const uint32_t pf = prefetch_record(Q.L, t);
-  uint64_t w = ld_agent64(Q.kwords + blk);
+  const uint64_t* wp = Q.kwords + (uint64_t)blk * kKeyWordStride;
+  uint64_t w = ld_agent64(wp);
   if ((uint32_t)w != Q.epoch) {
     const uint64_t t0 = wall_clock64();
     for (;;) {
       __builtin_amdgcn_s_sleep(8);
-      w = ld_agent64(Q.kwords + blk);
+      w = ld_agent64(wp);
       if ((uint32_t)w == Q.epoch) break;
       if (ld_err(Q)) return;
       if (wall_clock64() - t0 > Q.timeout_ticks) {
@@ -804,6 +821,9 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
     // per waiting tile would invalidate the XCD's L2 each time
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+#ifdef BPSR_KEYED_TRACE
+  if (threadIdx.x == 0) kt[1] = wall_clock64();
+#endif
   const uint32_t perm = (uint32_t)(w >> 32);
   if (perm == kKeySkip) {
     keep_prefetch(pf);
@@ -813,11 +833,12 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
   if (Q.wide) {
     // 9..16 workers: the order's positions 8..15 are in the block's second
     // word, released before the first (it may still be on its way here)
-    uint64_t hi = ld_agent64(Q.kwords + Q.nblocks + blk);
+    const uint64_t* hp = Q.kwords + (uint64_t)(Q.nblocks + blk) * kKeyWordStride;
+    uint64_t hi = ld_agent64(hp);
     const uint64_t t0 = wall_clock64();
     while ((uint32_t)hi != Q.epoch) {
       __builtin_amdgcn_s_sleep(2);
-      hi = ld_agent64(Q.kwords + Q.nblocks + blk);
+      hi = ld_agent64(hp);
       if (wall_clock64() - t0 > Q.timeout_ticks) {
         __hip_atomic_store(&Q.ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -868,7 +889,13 @@ __global__ __launch_bounds__(kBlock) void blockq_key_kernel(BlockqLaunch Q) {
                                                      threadIdx.x);
   }
   keep_prefetch(pf);
+#ifdef BPSR_KEYED_TRACE
+  if (threadIdx.x == 0) kt[2] = wall_clock64();
+#endif
   key_tile_done<NT>(Q, blk, r.kind == kTileFull && NT == kPolWt);
+#ifdef BPSR_KEYED_TRACE
+  if (threadIdx.x == 0) kt[3] = wall_clock64();
+#endif
 }
 
 // ------------------------------------------------------------- launchers ----
