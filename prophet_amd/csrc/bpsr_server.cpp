@@ -266,7 +266,8 @@ int copy_in(byteps_server* s, KeyState* ks, int w, const void* data, size_t len,
   Lane& L = *s->lanes[ks->lane];
   ks->round_copied = true;
   hipError_t e = hipSuccess;
-  if (ks->has_done) e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
+  // a keyed fold: its key's word on the host (wait_keyed_slots)
+  if (ks->has_done && !wait_keyed_slots(s, ks)) e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
   if (e == hipSuccess)
     e = hipMemcpyAsync(ks->slot[w], data, len,
                        loc == BYTEPS_SERVER_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
@@ -978,7 +979,8 @@ void issue_copies(byteps_server* s, Lane& L, std::vector<CopyJob>& jobs) {
     L.where = "copies: key locks";
     for (auto& j : jobs) {  // keyed folds run on the consumer's stream
       std::lock_guard<std::mutex> g(j.ks->mu);
-      if (!rc && j.ks->keyed && j.ks->has_done && j.ks->fold_ev != last) {
+      if (!rc && j.ks->keyed && j.ks->has_done && !wait_keyed_slots(s, j.ks) &&
+          j.ks->fold_ev != last) {
         last = j.ks->fold_ev;
         if ((e = hipStreamWaitEvent(L.copy, last, 0)) != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
       }
@@ -1581,7 +1583,7 @@ int byteps_server_recv_slot(byteps_server* s, uint64_t key, int worker, void** s
   std::unique_lock<std::mutex> lk(ks->mu);
   ks->cv.wait(lk, [&] { return ks->pending == 0 || ks->error; });  // every fold issued
   if (ks->error) return key_error(ks);
-  if (ks->has_done) {  // the slot may be read by the last issued fold
+  if (ks->has_done && !wait_keyed_slots(s, ks)) {  // the slot may be read by the last issued fold
     hipError_t e = hipEventSynchronize(ks->fold_ev);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   }

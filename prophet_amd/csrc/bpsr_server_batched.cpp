@@ -78,7 +78,7 @@ int push_many_host(byteps_server* s, std::vector<KeyState*>& ks_of, const void* 
       {
         std::lock_guard<std::mutex> g(ks->mu);
         // keyed folds run on the consumer's stream, not behind the fold mark
-        if (e == hipSuccess && ks->keyed && ks->has_done)
+        if (e == hipSuccess && ks->keyed && ks->has_done && !wait_keyed_slots(s, ks))
           e = hipStreamWaitEvent(L.copy, ks->fold_ev, 0);
         if (e == hipSuccess)
           e = hipMemcpyAsync(ks->slot[worker], datas[i], lens[i], hipMemcpyHostToDevice, L.copy);
@@ -212,7 +212,8 @@ int byteps_server_push_many(byteps_server* s, const uint64_t* keys, const void* 
       std::vector<hipEvent_t> waits;
       for (int i : by_lane[l]) {
         std::lock_guard<std::mutex> g(ks_of[i]->mu);
-        if (ks_of[i]->keyed && ks_of[i]->has_done) waits.push_back(ks_of[i]->fold_ev);
+        if (ks_of[i]->keyed && ks_of[i]->has_done && !wait_keyed_slots(s, ks_of[i]))
+          waits.push_back(ks_of[i]->fold_ev);
       }
       std::sort(waits.begin(), waits.end());
       waits.erase(std::unique(waits.begin(), waits.end()), waits.end());

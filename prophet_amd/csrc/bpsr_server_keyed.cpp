@@ -107,14 +107,49 @@ void kq_launch_ahead(byteps_server* s, uint32_t epoch) {
 
 // Skip words for every key not yet released for `epoch` (each under its
 // key's lock, as a release is): the epoch's consumer passes them and
-// completes, and those keys' next rounds go to the next epoch.
+// completes, and those keys' next rounds go to the next epoch.  A key may
+// lag more than one epoch: lane epochs (no consumer) do not wait for every
+// key, so a key whose round is late can still be short of a lane epoch
+// before this one; it is skipped through those too (its late round then
+// folds in the next epoch) — skipping only keys at exactly `epoch` left this
+// consumer waiting for a key whose next round needed the epochs queued
+// behind it (the device timeout, found by
+// test_device_release_mixed_kinds_and_late_keys_stress).
 static void skip_unreleased(byteps_server* s, uint32_t epoch) {
   const uint64_t skip = ((uint64_t)kKeySkip << 32) | kKeySkip;
   for (KeyState* k : s->kq_keys) {
-    std::lock_guard<std::mutex> g(k->mu);
     const int kk = k->kq_key.load();
-    if (kk >= 0 && keyq_next_epoch(s->kq, kk) == epoch) (void)keyq_release(s->kq, kk, skip, nullptr);
+    // a key released for this epoch is not locked at all: its lock may be
+    // held by a push waiting for that key's own fold (wait_keyed_slots),
+    // which can sit in an epoch behind this one
+    if (kk < 0 || !epoch_reached(epoch, keyq_next_epoch(s->kq, kk))) continue;
+    std::lock_guard<std::mutex> g(k->mu);
+    while (epoch_reached(epoch, keyq_next_epoch(s->kq, kk)))  // next <= epoch (wrap-safe)
+      (void)keyq_release(s->kq, kk, skip, nullptr);
   }
+}
+
+// Wait on the host until key `kq_key`'s fold in consumer epoch `epoch` has
+// read its slots: the key's own completion word, not the epoch's event.  An
+// epoch can hold for a late key until the completer closes it, and a lane
+// copy stream put behind the epoch's event holds every later copy of the lane
+// with it — a blocking push of another key then waited under that key's lock,
+// which the close needed (the device timeout of
+// test_device_release_mixed_kinds_and_late_keys_stress).  False: the queue
+// failed or is not there; the caller then orders on the event as before.
+bool wait_keyed_slots(byteps_server* s, int kq_key, uint32_t epoch) {
+  if (kq_key < 0 || !epoch || !s->kq) return false;
+  for (int i = 0;; ++i) {
+    if (keyq_key_done(s->kq, kq_key, epoch)) return true;
+    if (keyq_failed(s->kq)) return false;
+    if (i < 4096)
+      __builtin_ia32_pause();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+  }
+}
+bool wait_keyed_slots(byteps_server* s, const KeyState* ks) {
+  return ks->keyed && ks->has_done && wait_keyed_slots(s, ks->kq_key.load(), ks->kq_round_epoch);
 }
 
 // Retire an epoch launched ahead that no round has begun (skip_unreleased),
@@ -247,6 +282,16 @@ void kq_epoch_done(byteps_server* s, uint32_t epoch, uint64_t seq) {
         }
         fprintf(stderr, "  keys released for this epoch %d of %zu, deferred jobs %d\n",
                 rounds_done, s->kq_keys.size(), pending);
+        fprintf(stderr, "  launched %u decided %u opened %u slot-epoch %u; kinds:",
+                keyq_launched(s->kq), s->kq_decided.load(), keyq_opened(s->kq),
+                s->kq_slot_epoch.load());
+        for (uint32_t e = epoch > 4 ? epoch - 4 : 1; e <= s->kq_decided.load(); ++e)
+          fprintf(stderr, " %u:%d", e, (int)s->kq_kind[e % byteps_server::kKqRing]);
+        fprintf(stderr, "\n  next epoch per key:");
+        for (KeyState* k : s->kq_keys)
+          fprintf(stderr, " %llu:%u", (unsigned long long)k->key,
+                  keyq_next_epoch(s->kq, k->kq_key.load()));
+        fprintf(stderr, "\n");
       }
       s->kq_off.store(true);
       for (KeyState* k : s->kq_keys)

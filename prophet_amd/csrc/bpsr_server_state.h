@@ -442,6 +442,8 @@ int finish_round(byteps_server* s, KeyState* ks, const std::vector<int>& order,
 int injected_failure(byteps_server* s);
 void build_kq(byteps_server* s, int dtype);
 bool keyed_member(byteps_server* s, KeyState* ks);
+bool wait_keyed_slots(byteps_server* s, int kq_key, uint32_t epoch);
+bool wait_keyed_slots(byteps_server* s, const KeyState* ks);
 int key_release(byteps_server* s, KeyState* ks, const std::vector<int>& order, hipStream_t stream,
                 bool skip = false);
 int kq_launch_upto(byteps_server* s, uint32_t need);

@@ -2063,6 +2063,101 @@ def test_device_release_server_mixed_copied_and_slot_written_rounds(port, monkey
     assert stats[-1]["lane_epochs"] >= 1, stats[-1]
 
 
+def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch):
+    """The per-epoch release choice under concurrency (server.h): 4 worker
+    threads, 5 keys, 8 rounds; every (round, key, worker) push is, at random,
+    written into the slot by the "transport" (push_ready), a non-blocking
+    device push (lane copy) or a blocking host push (copied), keys arrive in
+    a different random order per worker and round, and in two rounds one key
+    comes 150 ms late (its epoch closes without it).  Rounds with any copied
+    push fold with lane launches, the others on the device; epochs open as
+    consumer or lane epochs as their first release decides.  Every pull of
+    every round equals the oracle's left fold in the recorded arrival order."""
+    from prophet_amd.reducer import GpuReducer
+    from prophet_amd.server import PSServer
+    monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
+    dt, N, R = DType.FLOAT32, 4, 8
+    sizes = [3, 1000, 4096 + 1, 65_536, 200_003]
+    keys = list(range(300, 300 + len(sizes)))
+    es = elem_size(dt)
+    rng0 = random.Random(4242)
+    kind = {(r, j, w): rng0.choice(("slot", "slot", "async", "host"))
+            for r in range(1, R + 1) for j in range(len(keys)) for w in range(N)}
+    late = {(3, 1), (6, 4)}                              # (round, key index)
+    srv = PSServer(N, engine_lanes=2)
+    dev = torch.device("cuda:0")
+    host = {(w, r, j): data(dt, n, w, r, j)
+            for w in range(N) for r in range(R + 1) for j, n in enumerate(sizes)}
+    src = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(N)]
+    bar = threading.Barrier(N + 1)
+    errors, pulled = [], {}
+
+    def worker(w):
+        torch.cuda.set_stream(streams[w])
+        try:
+            rng = random.Random(900 + w)
+            for j, k in enumerate(keys):
+                srv.push(k, w, src[(w, 0, j)], dt)       # init round
+            for r in range(1, R + 1):
+                order = list(range(len(keys)))
+                rng.shuffle(order)
+                for j in order:
+                    if (r, j) in late and w == 0:
+                        time.sleep(0.15)
+                    kd = kind[(r, j, w)]
+                    if kd == "slot":
+                        st = torch.cuda.current_stream(dev)
+                        x = src[(w, r, j)]
+                        GpuReducer().copy(srv.recv_slot(keys[j], w), x, x.numel(), stream=st)
+                        st.synchronize()
+                        srv.push_ready(keys[j], w)
+                    elif kd == "async":
+                        srv.push_async(keys[j], w, src[(w, r, j)], dt)
+                    else:
+                        srv.push(keys[j], w, host[(w, r, j)], dt)
+                outs = []
+                for j, k in enumerate(keys):
+                    o = torch.empty(sizes[j] * es, dtype=torch.uint8, device=dev)
+                    srv.pull(k, o)
+                    outs.append(o.cpu().numpy())
+                pulled[(w, r)] = outs
+                bar.wait(timeout=120)
+                bar.wait(timeout=120)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(N)]
+    for t in ts:
+        t.start()
+    try:
+        for r in range(1, R + 1):
+            try:
+                bar.wait(timeout=240)
+            except threading.BrokenBarrierError:
+                raise AssertionError(f"a worker failed: {errors}")
+            assert not errors, errors
+            for j, k in enumerate(keys):
+                rounds, _, order = srv.key_info(k)
+                assert rounds == r and sorted(order) == list(range(N)), (r, k, order)
+                n = sizes[j] * es
+                want = np.zeros(n, np.uint8)
+                port.sum_n(want, [host[(w, r, j)] for w in order], n, dt)
+                for w in range(N):
+                    assert_bytes_match(dt, pulled[(w, r)][j], want, nan_class_f32_f64=False,
+                                       what=f"r{r} key {k} w{w}")
+            bar.wait(timeout=120)
+    finally:
+        for t in ts:
+            t.join(timeout=60)
+    st = srv.stats()
+    srv.close()
+    assert not errors, errors
+    assert st["key_releases"] > 0 and st["fold_launches"] > 0, st
+
+
 def test_device_release_epoch_closes_for_a_missing_key(port, monkeypatch):
     """No key has to be pushed in every epoch (server.h): a round in which
     key 2 is not pushed in time leaves its epoch open only until the host
