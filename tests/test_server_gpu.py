@@ -2063,7 +2063,8 @@ def test_device_release_server_mixed_copied_and_slot_written_rounds(port, monkey
     assert stats[-1]["lane_epochs"] >= 1, stats[-1]
 
 
-def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch):
+@pytest.mark.parametrize("pulls", ["device", "mixed"])
+def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch, pulls):
     """The per-epoch release choice under concurrency (server.h): 4 worker
     threads, 5 keys, 8 rounds; every (round, key, worker) push is, at random,
     written into the slot by the "transport" (push_ready), a non-blocking
@@ -2072,7 +2073,11 @@ def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch):
     comes 150 ms late (its epoch closes without it).  Rounds with any copied
     push fold with lane launches, the others on the device; epochs open as
     consumer or lane epochs as their first release decides.  Every pull of
-    every round equals the oracle's left fold in the recorded arrival order."""
+    every round equals the oracle's left fold in the recorded arrival order.
+    pulls="mixed": each pull is, at random, a copy into a device tensor, a
+    copy into host memory or a host view of the store's mirror (the mirror's
+    D2H waits for a device-released round's epoch on the lane's d2h stream),
+    with other kind and late-key draws."""
     from prophet_amd.reducer import GpuReducer
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
@@ -2080,10 +2085,12 @@ def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch):
     sizes = [3, 1000, 4096 + 1, 65_536, 200_003]
     keys = list(range(300, 300 + len(sizes)))
     es = elem_size(dt)
-    rng0 = random.Random(4242)
+    rng0 = random.Random(4242 if pulls == "device" else 77)
     kind = {(r, j, w): rng0.choice(("slot", "slot", "async", "host"))
             for r in range(1, R + 1) for j in range(len(keys)) for w in range(N)}
-    late = {(3, 1), (6, 4)}                              # (round, key index)
+    pkind = {(r, j, w): "device" if pulls == "device" else rng0.choice(("device", "host", "view"))
+             for r in range(1, R + 1) for j in range(len(keys)) for w in range(N)}
+    late = {(3, 1), (6, 4)} if pulls == "device" else {(2, 0), (5, 2), (7, 3)}
     srv = PSServer(N, engine_lanes=2)
     dev = torch.device("cuda:0")
     host = {(w, r, j): data(dt, n, w, r, j)
@@ -2119,9 +2126,17 @@ def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch):
                         srv.push(keys[j], w, host[(w, r, j)], dt)
                 outs = []
                 for j, k in enumerate(keys):
-                    o = torch.empty(sizes[j] * es, dtype=torch.uint8, device=dev)
-                    srv.pull(k, o)
-                    outs.append(o.cpu().numpy())
+                    pk = pkind[(r, j, w)]
+                    if pk == "view":
+                        outs.append(np.frombuffer(srv.pull_view(k), np.uint8).copy())
+                    elif pk == "host":
+                        o = np.empty(sizes[j] * es, np.uint8)
+                        srv.pull(k, o)
+                        outs.append(o)
+                    else:
+                        o = torch.empty(sizes[j] * es, dtype=torch.uint8, device=dev)
+                        srv.pull(k, o)
+                        outs.append(o.cpu().numpy())
                 pulled[(w, r)] = outs
                 bar.wait(timeout=120)
                 bar.wait(timeout=120)
