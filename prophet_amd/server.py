@@ -220,9 +220,10 @@ class PSServer:
     @classmethod
     def from_env(cls) -> "PSServer":
         """The dedicated server process's server (byteps_server(),
-        server.cc:339-400): byteps_server_config_from_env — launches by
-        default (its pushes land in host memory; BPSR_SERVER_RELEASE=device
-        for pushes that land in HBM, server.h)."""
+        server.cc:339-400): byteps_server_config_from_env — device releases
+        by default (each epoch's first release picks a consumer or lane
+        launches, so copied and slot-written rounds mix freely, server.h);
+        BPSR_SERVER_RELEASE=launch keeps one launch per round."""
         c = config_from_env()
         return cls(c.num_workers, c.engine_lanes, c.policy, bool(c.async_mode), c.device,
                    bool(c.enable_schedule), bool(c.engine_blocking), c.release)
