@@ -1467,16 +1467,29 @@ int byteps_server_push(byteps_server* s, uint64_t key, int worker, const void* d
   // its init push) is not folded yet: hold it until the slot is free.
   ks->cv.wait(lk, [&] { return can_push(s, ks, worker); });
   if (ks->error) return key_error(ks);
-  if ((rc = copy_in(s, ks, worker, data, len, location))) return rc;
+  if ((rc = copy_in(s, ks, worker, data, len, location, /*wait=*/false))) return rc;
+  // The caller's buffer goes back once its copy has landed, waited for with
+  // the key's lock released: the copy stream can sit behind a lane fold that
+  // waits for a keyed epoch, and that epoch's close may need this lock to
+  // skip the key (DESIGN.md §9.x "slot reuse after a device release").  The
+  // round's fold is ordered behind the copy on the device, so the arrival
+  // need not wait for it.  (A later copy of the key re-records the event on
+  // the same in-order stream: waiting for it covers this one.)
+  const hipEvent_t copied = ks->copied;
+  auto landed = [&](int r) {
+    if (lk.owns_lock()) lk.unlock();
+    const hipError_t e = hipEventSynchronize(copied);
+    return r ? r : (e == hipSuccess ? 0 : hip_fail(e, "push copy"));
+  };
   thread_local std::vector<FoldJob> defer;  // keeps its capacity: no allocation per call
   defer.clear();
-  if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return rc;
+  if ((rc = arrive_and_wait_init(s, ks, worker, lk, s->combine ? &defer : nullptr))) return landed(rc);
   if (!defer.empty()) {
     lk.unlock();
-    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return rc;
+    if (issue_combined(s, defer) && (rc = own_key_status(ks))) return landed(rc);
     lk.lock();
   }
-  return s->blocking ? finish_blocking(s, ks, lk) : 0;
+  return landed(s->blocking ? finish_blocking(s, ks, lk) : 0);
 }
 
 int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const void* data,
