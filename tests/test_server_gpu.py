@@ -2063,7 +2063,7 @@ def test_device_release_server_mixed_copied_and_slot_written_rounds(port, monkey
     assert stats[-1]["lane_epochs"] >= 1, stats[-1]
 
 
-@pytest.mark.parametrize("pulls", ["device", "mixed"])
+@pytest.mark.parametrize("pulls", ["device", "mixed", "mixed8"])
 def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch, pulls):
     """The per-epoch release choice under concurrency (server.h): 4 worker
     threads, 5 keys, 8 rounds; every (round, key, worker) push is, at random,
@@ -2077,7 +2077,8 @@ def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch, pull
     pulls="mixed": each pull is, at random, a copy into a device tensor, a
     copy into host memory or a host view of the store's mirror (the mirror's
     D2H waits for a device-released round's epoch on the lane's d2h stream),
-    with other kind and late-key draws."""
+    with other kind and late-key draws.  pulls="mixed8": the same with 8
+    workers (the release word's widest single-word order)."""
     from prophet_amd.reducer import GpuReducer
     from prophet_amd.server import PSServer
     monkeypatch.setenv("BPSR_SERVER_RELEASE", "device")
@@ -2085,7 +2086,9 @@ def test_device_release_mixed_kinds_and_late_keys_stress(port, monkeypatch, pull
     sizes = [3, 1000, 4096 + 1, 65_536, 200_003]
     keys = list(range(300, 300 + len(sizes)))
     es = elem_size(dt)
-    rng0 = random.Random(4242 if pulls == "device" else 77)
+    rng0 = random.Random({"device": 4242, "mixed": 77}.get(pulls, 5))
+    if pulls == "mixed8":
+        N = 8
     kind = {(r, j, w): rng0.choice(("slot", "slot", "async", "host"))
             for r in range(1, R + 1) for j in range(len(keys)) for w in range(N)}
     pkind = {(r, j, w): "device" if pulls == "device" else rng0.choice(("device", "host", "view"))
