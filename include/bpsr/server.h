@@ -185,8 +185,10 @@ int byteps_server_push_async(byteps_server* s, uint64_t key, int worker, const v
 
 /* Zero-copy transport path: where worker `worker`'s push for `key` must land,
  * then the arrival notice once the bytes are there (visible to the device).
- * recv_slot waits until the key's last issued fold (or init copy) is done, so
- * the slot is free to be written once it returns — provided the worker's
+ * recv_slot waits until the key's last issued fold (or init copy) is done — a
+ * device-released round: until the key's own completion word says so, not
+ * for its whole epoch — so the slot is free to be written once it returns —
+ * provided the worker's
  * previous push of the key has been folded, i.e. the transport writes a
  * worker's round r + 1 only after that worker pulled round r (BytePS's
  * push-then-pull order per key; the init round is complete once the init
